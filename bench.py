@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""Headline benchmark: env-steps/s of the vectorised LB environment (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--servers S]
+
+One rank per GPU (torchrun for N > 1).  Weak scaling: every GPU steps its own shard of B envs
+(global ids [rank*B, (rank+1)*B) key the RNG, so shards never communicate); the only collectives
+are the timing barrier and the max/sum reductions of the result.  A "step" is one VecEnv.step of
+every env: random-policy actions drawn on the GPU, dynamics kernel, observe kernel (features,
+reward, done), episode bookkeeping and the masked auto-reset launch.
+
+Default N=1 workload: 65536 envs x 4 servers (north-star point; BASELINE configs[1] is the same
+random-policy rollout at 4096 envs and is a parity-test case).  Prints ONE JSON line (rank 0)
+with a `roofline` object for the dominant kernel (HIP-event timed inside the timed region) and a
+`cpu_baseline` (the C oracle on host cores, bounded sample of the same workload).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = ("env-steps/sec (whole node), 4-server LB env, batch 4k→512k at 1/2/4/8 MI355X")
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
+K = 128
+
+
+def algorithmic_bytes(S: int):
+    """Bytes each kernel must move per env-step with the state layout of DESIGN.md §4.
+
+    observe : read 3 reservoir arrays (fct, dur, ts: 128 x 4 B each) + hc + res_count per server,
+              ep_step/ep_return read+write, obs 44 B/server, reward 4, done 1, ep outputs 12.
+    dynamics: read+write env header (8 x 4 B) and per-server hc/last_tc/res_count, action 8 B and
+              assign-count 4 B per server (ring and reservoir-insert traffic is data dependent
+              and not counted: a lower bound).
+    """
+    obs = S * (3 * K * 4 + 8 + 44) + 12 + 12 + 4 + 1 + 12
+    dyn = 2 * 32 + S * (2 * 12 + 8 + 4)
+    return {"observe": obs, "dynamics": dyn}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--servers", type=int, default=4)
+    ap.add_argument("--seed", type=int, default=20260109)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, seconds: float):
+    """Oracle (C restatement, identical dynamics/features) on host cores, bounded sample."""
+    import numpy as np
+
+    import oracle
+    from marllb_amd.env import make_config
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    threads = max(1, min(16, avail))
+    nb = 2048
+    cfg = make_config(nb, args.servers, seed=args.seed, env_id_offset=0)
+    ora = oracle.OracleEnv(cfg, threads=threads)
+    ora.reset()
+    rng = np.random.default_rng(1)
+    acts = [rng.integers(0, 3, (nb, args.servers)).astype(np.int64) for _ in range(8)]
+    ora.step(acts[0])  # warm caches / thread pool
+    n, t0 = 0, time.perf_counter()
+    while True:
+        ora.step(acts[n % len(acts)])
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and n >= 3:
+            break
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": nb * n / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{nb} of the {args.batch} envs (global ids 0-{nb - 1}), S={args.servers}, "
+                      f"{n} random-policy steps, {el:.1f} s, oracle/lbsim_oracle.c "
+                      f"(OpenMP {threads} threads) on {cpu_model or 'host CPU'}"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from marllb_amd import _lib
+    from marllb_amd.env import VecLoadBalanceEnv
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("for --gpus N > 1 launch with torch.distributed.run --nproc-per-node N")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    B, S = args.batch, args.servers
+    env = VecLoadBalanceEnv(B, S, device=dev, seed=args.seed, env_id_offset=rank * B,
+                            autoreset=True, max_steps=10000)
+    env.reset()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(args.seed + rank)
+
+    def one_step():
+        a = torch.randint(0, 3, (B, S), device=dev, dtype=torch.int64, generator=gen)
+        env.step(a)
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    lib = _lib.load()
+    env.handle.check(lib.lbsim_profile_begin(env.handle.h, 4 * args.steps + 8))
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    ms = (ctypes.c_double * 4)()
+    cnt = (ctypes.c_int64 * 4)()
+    env.handle.check(lib.lbsim_profile_end(env.handle.h, ms, cnt))
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if rank == 0:
+        value = world * B * args.steps / elapsed
+        names = ["dynamics_kernel", "observe_kernel"]
+        avg = {names[i]: ms[i] / max(1, cnt[i]) for i in range(2)}
+        dom = max(avg, key=avg.get)
+        ab = algorithmic_bytes(S)["observe" if dom == "observe_kernel" else "dynamics"] * B
+        achieved = ab / (avg[dom] * 1e-3) / 1e9
+        traffic = None
+        tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(tfile):
+            t = json.load(open(tfile))
+            if t.get("batch") == B and t.get("servers") == S and dom in t.get("bytes_per_launch", {}):
+                traffic = t["bytes_per_launch"][dom]
+        out = {
+            "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32/int32 (f64 reward)",
+            "data": "synthetic: Philox4x32-10 Poisson arrivals lambda=400/s, Exp(1) work, "
+                    "mu=lambda/(0.8 S) per server, random discrete policy",
+            "config": {"workload": "LB env random-policy rollout, 4 servers (BASELINE configs[1] "
+                                   "rollout at the north-star batch)",
+                       "envs_per_gpu": B, "servers": S, "global_batch": world * B,
+                       "step_interval_s": 0.25, "assign_policy": "sed", "autoreset": True,
+                       "parallelism": f"env-shard x{world}"},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic, "algorithmic_bytes_per_launch": ab,
+                         "avg_launch_ms": avg[dom],
+                         "kernel_avg_ms": avg},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

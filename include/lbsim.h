@@ -1,0 +1,204 @@
+/*
+ * lbsim.h — C ABI of the MI355X-native vectorised load-balancing environment.
+ *
+ * One handle = B independent LB environments (a shard of the global env range) resident in the
+ * HBM of one GPU.  Every entry point is extern "C", takes plain pointers and sizes, never throws,
+ * and returns an int status (LBSIM_OK or a negative LBSIM_E* code; message via lbsim_last_error).
+ *
+ * Buffers passed to reset/step/reward/features are DEVICE pointers owned by the caller (e.g. a
+ * torch tensor's data_ptr()); nothing is allocated inside lbsim_reset/lbsim_step, so both can be
+ * captured into a hipGraph.  `stream` is a hipStream_t (NULL = default stream).  Calls on one
+ * handle are stream-ordered and NOT thread-safe across host threads.
+ *
+ * Reference interfaces replaced (paths relative to the MARLLB reference tree):
+ *   LoadBalanceEnv.__init__ / _setup_spaces   simulation-mode/problem-03-rl-environment/src/env.py:71-184
+ *   LoadBalanceEnv.reset                      env.py:186-213
+ *   LoadBalanceEnv.step                       env.py:215-286
+ *   LoadBalanceEnv.seed / close               env.py:321-330
+ *   RewardFunction.compute + active rule      src/rewards.py:290-381, env.py:391-423
+ *   ReservoirSampler.add / get_features       problem-01-reservoir-sampling/src/reservoir.py:50-196
+ *   C twin reservoir_add / compute_stats      problem-01-reservoir-sampling/src/reservoir.h:118-268
+ *   server assignment SED/SED2/LSQ/LSQ2       src/vpp/lb/node.c:388-441
+ *   flow-completion samples (fct, duration)   src/vpp/lb/lbhash.h:87-172
+ * Full semantics: DESIGN.md §3 (the simulator spec the GPU kernels and oracle/ both implement).
+ */
+#ifndef LBSIM_H
+#define LBSIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LBSIM_ABI_VERSION 1
+#define LBSIM_MAX_SERVERS 16   /* S <= 16 (QMIX config C5 uses 4 agents x 4 servers)        */
+#define LBSIM_RESERVOIR_K 128  /* reservoir.py:31 capacity=128, reservoir.h:24               */
+#define LBSIM_NUM_FEATURES 11  /* env.py:46-48 (S, 11) observation                           */
+#define LBSIM_MAX_DISCRETE 8
+
+/* ---- status codes (never thrown across the ABI) ---- */
+#define LBSIM_OK 0
+#define LBSIM_EINVAL (-1)  /* bad argument / config (Python facade re-raises ValueError)      */
+#define LBSIM_ENOMEM (-2)  /* device allocation failed                                        */
+#define LBSIM_EDEVICE (-3) /* HIP runtime error (no GPU, launch failure, ...)                 */
+#define LBSIM_ESHAPE (-4)  /* buffer size does not match the handle's B/S                     */
+#define LBSIM_ENOTSUP (-5) /* option not built in this version                                */
+
+/* ---- enums ---- */
+enum lbsim_action_type { LBSIM_ACTION_DISCRETE = 0, LBSIM_ACTION_CONTINUOUS = 1 };
+enum lbsim_dtype { LBSIM_DTYPE_I32 = 0, LBSIM_DTYPE_I64 = 1, LBSIM_DTYPE_F32 = 2 };
+
+/* rewards.py:297-307 SUPPORTED_METRICS, same order */
+enum lbsim_reward_metric {
+  LBSIM_METRIC_JAIN = 0,
+  LBSIM_METRIC_VARIANCE = 1,
+  LBSIM_METRIC_STD = 2,
+  LBSIM_METRIC_CV = 3,
+  LBSIM_METRIC_MAX = 4,
+  LBSIM_METRIC_MIN = 5,
+  LBSIM_METRIC_PRODUCT = 6,
+  LBSIM_METRIC_RANGE = 7,
+  LBSIM_METRIC_GINI = 8
+};
+
+/* node.c:393-441: LB_SED, LB_SED2 (power of two), LB_LSQ, LB_LSQ2 */
+enum lbsim_assign_policy {
+  LBSIM_POLICY_SED = 0,
+  LBSIM_POLICY_SED2 = 1,
+  LBSIM_POLICY_LSQ = 2,
+  LBSIM_POLICY_LSQ2 = 3
+};
+
+enum lbsim_arrival_source { LBSIM_ARRIVAL_POISSON = 0 };
+
+/*
+ * POD configuration.  Mirrors the LoadBalanceEnv kwargs (env.py:71-87) plus the simulator knobs
+ * the reference leaves implicit.  Fill with lbsim_config_default() and override.
+ */
+typedef struct lbsim_config {
+  int32_t num_envs;          /* B: envs in this handle (this GPU's shard)                    */
+  int32_t num_servers;       /* S: 1..LBSIM_MAX_SERVERS                         env.py:73   */
+  int64_t env_id_offset;     /* global id of local env 0 (RNG key; sharding-invariant)       */
+  uint64_t seed;             /* Philox4x32-10 key                               env.py:86   */
+  int32_t action_type;       /* lbsim_action_type                               env.py:74   */
+  int32_t num_discrete;      /* len(discrete_weights)                           env.py:75   */
+  float discrete_weights[LBSIM_MAX_DISCRETE]; /* default [1.0, 1.5, 2.0]         env.py:69   */
+  float min_weight;          /* continuous clip lower bound, default 0.1        env.py:77   */
+  float max_weight;          /* continuous clip upper bound, default 10.0       env.py:76   */
+  int32_t reward_metric;     /* lbsim_reward_metric, default JAIN               env.py:78   */
+  int32_t reward_field;      /* obs column 0..10 (default 10 =                               */
+                             /* 'flow_duration_avg_decay', env.py:79,377-381);               */
+                             /* -1 = field name unknown -> reward 0.0 (rewards.py:375-376)  */
+  float step_interval;       /* simulated seconds per step, default 0.25        env.py:80   */
+  int32_t max_steps;         /* done when episode step >= max_steps (10000)     env.py:81   */
+  int32_t normalize_obs;     /* running mean/std normalisation    env.py:85,450-470   */
+  int32_t assign_policy;     /* lbsim_assign_policy, default SED                             */
+  int32_t arrival_source;    /* lbsim_arrival_source, default POISSON                        */
+  float arrival_rate;        /* lambda, flows/s per env, default 400 (poisson_for_loop)      */
+  float server_rate[LBSIM_MAX_SERVERS]; /* mu_s, flows/s each server can serve (Exp work)   */
+  float decay_factor;        /* reservoir decay, default 0.9          reservoir.py:106       */
+  int32_t queue_capacity;    /* Q: max flows in flight per server (1..64), default 32       */
+  int32_t warmup_steps;      /* simulated steps run inside reset() with weights 1.0         */
+  int32_t reserved[8];
+} lbsim_config_t;
+
+typedef struct lbsim lbsim_t; /* opaque handle */
+
+/* Library identity; never fails, no GPU needed. */
+const char* lbsim_version(void);
+int lbsim_abi_version(void);
+
+/* Fill *cfg with the reference defaults (env.py:71-87) and the simulator defaults. */
+int lbsim_config_default(lbsim_config_t* cfg);
+
+/* Validate a config without touching the GPU (ValueError paths of env.py:184, rewards.py:321). */
+int lbsim_config_validate(const lbsim_config_t* cfg, char* msg, size_t msg_len);
+
+/* Allocate device state for cfg->num_envs envs on `device`.  Replaces LoadBalanceEnv.__init__. */
+int lbsim_create(const lbsim_config_t* cfg, int device, lbsim_t** out);
+
+/* Free device state.  Replaces LoadBalanceEnv.close (env.py:321-325). */
+int lbsim_destroy(lbsim_t* h);
+
+/* Thread-local message of the last failure on this handle (or of the last create if h==NULL). */
+const char* lbsim_last_error(const lbsim_t* h);
+
+/* Re-key the RNG and rewind every env's episode counter (env.py:327-330 seed()). */
+int lbsim_seed(lbsim_t* h, uint64_t seed);
+
+/*
+ * Reset the envs whose env_mask[b] != 0 (env_mask == NULL: all envs) and write their first
+ * observation into obs_out[b, S, 11] (f32); rows of unmasked envs are left untouched.
+ * Replaces LoadBalanceEnv.reset (env.py:186-213).
+ */
+int lbsim_reset(lbsim_t* h, const uint8_t* env_mask, float* obs_out, void* stream);
+
+/*
+ * Advance every env by one step of step_interval simulated seconds.
+ *   action        [B, S]: discrete indices (I32 or I64) or continuous weights (F32)
+ *   obs_out       [B, S, 11] f32   reward_out [B] f32   done_out [B] u8
+ *   assign_count_out [B, S] i32 (optional, NULL = skip): flows assigned per server this step
+ * Replaces LoadBalanceEnv.step (env.py:215-286).
+ */
+int lbsim_step(lbsim_t* h, const void* action, int action_dtype, float* obs_out,
+               float* reward_out, uint8_t* done_out, int32_t* assign_count_out, void* stream);
+
+/*
+ * Optional outputs of one step, all device pointers, NULL = not wanted.  Written by the same
+ * launch as obs/reward/done (no extra kernel, no host sync).
+ */
+typedef struct lbsim_step_outputs {
+  float* obs;              /* [B, S, 11] f32 observation (normalised if normalize_obs)        */
+  float* reward;           /* [B] f32                                                         */
+  uint8_t* done;           /* [B] u8                                                          */
+  int32_t* assign_count;   /* [B, S] i32 flows assigned per server this step                  */
+  float* raw_obs;          /* [B, S, 11] f32 un-normalised obs (reward/active_servers basis)  */
+  int32_t* episode_length; /* [B] i32 step count of the episode after this step (info['step'])*/
+  double* episode_return;  /* [B] f64 return of the episode after this step                   */
+} lbsim_step_outputs_t;
+
+/* lbsim_step with every output optional except obs, reward and done. */
+int lbsim_step_ex(lbsim_t* h, const void* action, int action_dtype,
+                  const lbsim_step_outputs_t* out, void* stream);
+
+/* sizeof(lbsim_config_t) / sizeof(lbsim_step_outputs_t) for binding-side layout checks. */
+size_t lbsim_config_size(void);
+size_t lbsim_step_outputs_size(void);
+
+/* Per-env episode length (i32 [B]) and return (f64 [B]) into device buffers (info['episode']). */
+int lbsim_episode_stats(lbsim_t* h, int32_t* length_out, double* return_out, void* stream);
+
+/* Stateless reward of given raw observations obs[n, S, 11] -> reward_out[n] (f32), using
+ * cfg->reward_metric / reward_field and the active rule any(obs[s] > 0) (env.py:410-417,
+ * rewards.py:329-381). */
+int lbsim_reward(const lbsim_config_t* cfg, const float* obs, int64_t n, float* reward_out,
+                 void* stream);
+
+/* Stateless reservoir features: for r in [0, n): values[r, K] f32, ts_ms[r, K] u32 sample
+ * timestamps (integer ms), counts[r] u32 (samples seen; min(count, K) valid slots) ->
+ * feats_out[r, 5] = {mean, p90, std, mean_decay, p90_decay} (reservoir.py:105-196). */
+int lbsim_reservoir_features(const float* values, const uint32_t* ts_ms, const uint32_t* counts,
+                             int64_t n, float decay_factor, float* feats_out, void* stream);
+
+/*
+ * Kernel timing: between lbsim_profile_begin and lbsim_profile_end every kernel launch of this
+ * handle is bracketed by a pair of hipEvents recorded on the launch stream (at most max_launches
+ * launches are timed).  lbsim_profile_end synchronises, and returns per kernel class
+ * {0: dynamics step, 1: observe step, 2: dynamics reset, 3: observe reset} the summed event time
+ * in ms (ms_out[4]) and the number of timed launches (count_out[4]).  Used by bench.py.
+ */
+int lbsim_profile_begin(lbsim_t* h, int max_launches);
+int lbsim_profile_end(lbsim_t* h, double* ms_out, int64_t* count_out);
+
+/* Snapshot: total bytes of the device state, and copies to/from a HOST buffer of that size.
+ * Layout: DESIGN.md §4 (used by the parity tests to compare every state word with oracle/). */
+int lbsim_state_size(const lbsim_t* h, size_t* bytes_out);
+int lbsim_get_state(lbsim_t* h, void* host_buf, size_t bytes);
+int lbsim_set_state(lbsim_t* h, const void* host_buf, size_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LBSIM_H */

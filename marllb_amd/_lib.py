@@ -1,0 +1,156 @@
+"""ctypes binding of liblbsim.so (the C ABI declared in include/lbsim.h).
+
+The library is built in-tree (marllb_amd/liblbsim.so, see marllb_amd/build.py).  There is no
+fallback: if the shared object is missing or fails to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblbsim.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "lbsim.h")
+
+MAX_SERVERS = 16
+RESERVOIR_K = 128
+NUM_FEATURES = 11
+MAX_DISCRETE = 8
+
+OK, EINVAL, ENOMEM, EDEVICE, ESHAPE, ENOTSUP = 0, -1, -2, -3, -4, -5
+ACTION_DISCRETE, ACTION_CONTINUOUS = 0, 1
+DTYPE_I32, DTYPE_I64, DTYPE_F32 = 0, 1, 2
+METRICS = ["jain", "variance", "std", "cv", "max", "min", "product", "range", "gini"]
+POLICIES = ["sed", "sed2", "lsq", "lsq2"]
+
+
+class LbsimConfig(ctypes.Structure):
+    """Mirror of lbsim_config_t (include/lbsim.h)."""
+
+    _fields_ = [
+        ("num_envs", ctypes.c_int32),
+        ("num_servers", ctypes.c_int32),
+        ("env_id_offset", ctypes.c_int64),
+        ("seed", ctypes.c_uint64),
+        ("action_type", ctypes.c_int32),
+        ("num_discrete", ctypes.c_int32),
+        ("discrete_weights", ctypes.c_float * MAX_DISCRETE),
+        ("min_weight", ctypes.c_float),
+        ("max_weight", ctypes.c_float),
+        ("reward_metric", ctypes.c_int32),
+        ("reward_field", ctypes.c_int32),
+        ("step_interval", ctypes.c_float),
+        ("max_steps", ctypes.c_int32),
+        ("normalize_obs", ctypes.c_int32),
+        ("assign_policy", ctypes.c_int32),
+        ("arrival_source", ctypes.c_int32),
+        ("arrival_rate", ctypes.c_float),
+        ("server_rate", ctypes.c_float * MAX_SERVERS),
+        ("decay_factor", ctypes.c_float),
+        ("queue_capacity", ctypes.c_int32),
+        ("warmup_steps", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 8),
+    ]
+
+
+class StepOutputs(ctypes.Structure):
+    """Mirror of lbsim_step_outputs_t (include/lbsim.h); every field a device pointer or NULL."""
+
+    _fields_ = [
+        ("obs", ctypes.c_void_p),
+        ("reward", ctypes.c_void_p),
+        ("done", ctypes.c_void_p),
+        ("assign_count", ctypes.c_void_p),
+        ("raw_obs", ctypes.c_void_p),
+        ("episode_length", ctypes.c_void_p),
+        ("episode_return", ctypes.c_void_p),
+    ]
+
+
+class LbsimError(RuntimeError):
+    """A liblbsim call returned a negative status."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"liblbsim error {code}: {msg}")
+        self.code = code
+
+
+_P = ctypes.c_void_p
+_SIGNATURES = {
+    "lbsim_version": (ctypes.c_char_p, []),
+    "lbsim_abi_version": (ctypes.c_int, []),
+    "lbsim_config_default": (ctypes.c_int, [ctypes.POINTER(LbsimConfig)]),
+    "lbsim_config_validate": (ctypes.c_int, [ctypes.POINTER(LbsimConfig), ctypes.c_char_p,
+                                             ctypes.c_size_t]),
+    "lbsim_create": (ctypes.c_int, [ctypes.POINTER(LbsimConfig), ctypes.c_int,
+                                    ctypes.POINTER(_P)]),
+    "lbsim_destroy": (ctypes.c_int, [_P]),
+    "lbsim_last_error": (ctypes.c_char_p, [_P]),
+    "lbsim_seed": (ctypes.c_int, [_P, ctypes.c_uint64]),
+    "lbsim_reset": (ctypes.c_int, [_P, _P, _P, _P]),
+    "lbsim_step": (ctypes.c_int, [_P, _P, ctypes.c_int, _P, _P, _P, _P, _P]),
+    "lbsim_step_ex": (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.POINTER(StepOutputs), _P]),
+    "lbsim_config_size": (ctypes.c_size_t, []),
+    "lbsim_step_outputs_size": (ctypes.c_size_t, []),
+    "lbsim_episode_stats": (ctypes.c_int, [_P, _P, _P, _P]),
+    "lbsim_reward": (ctypes.c_int, [ctypes.POINTER(LbsimConfig), _P, ctypes.c_int64, _P, _P]),
+    "lbsim_reservoir_features": (ctypes.c_int, [_P, _P, _P, ctypes.c_int64, ctypes.c_float, _P,
+                                                _P]),
+    "lbsim_profile_begin": (ctypes.c_int, [_P, ctypes.c_int]),
+    "lbsim_profile_end": (ctypes.c_int, [_P, _P, _P]),
+    "lbsim_state_size": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_size_t)]),
+    "lbsim_get_state": (ctypes.c_int, [_P, _P, ctypes.c_size_t]),
+    "lbsim_set_state": (ctypes.c_int, [_P, _P, ctypes.c_size_t]),
+}
+
+_lib = None
+
+
+def header_functions(path: str = HEADER_PATH) -> list[str]:
+    """Names of every function declared in include/lbsim.h."""
+    txt = open(path).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(lbsim_\w+)\s*\(", txt, re.M)))
+
+
+def load() -> ctypes.CDLL:
+    """Load liblbsim.so once.  Raises if the HIP library was not built (no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} not found: build it with `python -m marllb_amd.build` "
+            "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    try:  # share torch's HIP runtime when torch is present (same SONAME, one instance)
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def default_config() -> LbsimConfig:
+    cfg = LbsimConfig()
+    check(load().lbsim_config_default(ctypes.byref(cfg)))
+    return cfg
+
+
+def validate(cfg: LbsimConfig) -> None:
+    buf = ctypes.create_string_buffer(256)
+    if load().lbsim_config_validate(ctypes.byref(cfg), buf, 256) != OK:
+        raise ValueError(buf.value.decode())
+
+
+def check(rc: int, handle=None) -> None:
+    """Raise on a negative status: ValueError for EINVAL (as the reference does), else LbsimError."""
+    if rc != OK:
+        msg = load().lbsim_last_error(handle).decode()
+        if rc == EINVAL:
+            raise ValueError(msg or "invalid argument")
+        raise LbsimError(rc, msg)

@@ -1,0 +1,510 @@
+// lbsim_api.hip — extern "C" boundary of liblbsim (include/lbsim.h) over the gfx950 kernels.
+//
+// The handle owns the device state (one hipMalloc per section, SoA); the caller
+// owns every I/O buffer.  No allocation, no host synchronisation and no host<->device copy
+// happens inside lbsim_reset / lbsim_step, so a caller may capture them into a hipGraph.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/lbsim.h"
+#include "lbsim_kernels.h"
+
+using namespace lbk;
+
+struct Profiler {
+  bool on = false;
+  std::vector<hipEvent_t> ev;  // 2 per timed launch
+  std::vector<int> cls;        // kernel class per timed launch
+  size_t used = 0;
+};
+
+struct lbsim {
+  lbsim_config_t cfg;
+  Profiler prof;
+  int device;
+  int B, S, Q;
+  DevState st;
+  SimParams prm;
+  std::vector<void*> allocs;
+  bool initialised;  // a full reset has been issued
+  std::string err;
+};
+
+namespace {
+
+thread_local std::string g_create_err;
+
+int fail(lbsim_t* h, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (h) h->err = buf;
+  else g_create_err = buf;
+  return code;
+}
+
+// Scoped hipSetDevice that restores the caller's current device (torch keeps its own).
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = false;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+int bad_msg(char* msg, size_t n, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
+int bad_msg(char* msg, size_t n, const char* fmt, ...) {
+  if (msg && n) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(msg, n, fmt, ap);
+    va_end(ap);
+  }
+  return LBSIM_EINVAL;
+}
+
+int validate(const lbsim_config_t* c, char* msg, size_t n) {
+#define bad(...) bad_msg(msg, n, __VA_ARGS__)
+  if (c == nullptr) return bad("config is NULL");
+  if (c->num_envs < 1) return bad("num_envs must be >= 1 (got %d)", c->num_envs);
+  if (c->num_servers < 1 || c->num_servers > LBSIM_MAX_SERVERS)
+    return bad("num_servers must be in [1, %d] (got %d)", LBSIM_MAX_SERVERS, c->num_servers);
+  if ((int64_t)c->env_id_offset < 0 ||
+      (uint64_t)c->env_id_offset + (uint64_t)c->num_envs > 0xFFFFFFFFull)
+    return bad("global env ids must fit in 32 bits");
+  if (c->action_type != LBSIM_ACTION_DISCRETE && c->action_type != LBSIM_ACTION_CONTINUOUS)
+    return bad("Unknown action_type: %d", c->action_type);
+  if (c->action_type == LBSIM_ACTION_DISCRETE &&
+      (c->num_discrete < 1 || c->num_discrete > LBSIM_MAX_DISCRETE))
+    return bad("num_discrete must be in [1, %d]", LBSIM_MAX_DISCRETE);
+  if (c->reward_metric < LBSIM_METRIC_JAIN || c->reward_metric > LBSIM_METRIC_GINI)
+    return bad("Unsupported metric: %d", c->reward_metric);
+  if (c->reward_field < -1 || c->reward_field >= LBSIM_NUM_FEATURES)
+    return bad("reward_field must be -1 or a column in [0, 10]");
+  if (!(c->step_interval > 0.0f) || c->step_interval > 100.0f)
+    return bad("step_interval must be in (0, 100] seconds");
+  if ((int64_t)std::llround((double)c->step_interval * 1e6) < 1)
+    return bad("step_interval must be >= 1 us");
+  if (c->max_steps < 1) return bad("max_steps must be >= 1");
+  if (c->assign_policy < LBSIM_POLICY_SED || c->assign_policy > LBSIM_POLICY_LSQ2)
+    return bad("unknown assign_policy %d", c->assign_policy);
+  if (c->arrival_source != LBSIM_ARRIVAL_POISSON) return bad("unknown arrival_source");
+  if (!(c->arrival_rate >= 0.1f) || !(c->arrival_rate <= 1.0e6f))
+    return bad("arrival_rate must be in [0.1, 1e6] flows/s");
+  for (int s = 0; s < c->num_servers; ++s)
+    if (!(c->server_rate[s] >= 1.0f) || !(c->server_rate[s] <= 1.0e7f))
+      return bad("server_rate[%d] must be in [1, 1e7] flows/s", s);
+  if (!(c->decay_factor > 0.0f) || !(c->decay_factor < 1.0f))
+    return bad("decay_factor must be in (0, 1)");
+  if (c->queue_capacity < 1 || c->queue_capacity > 64)
+    return bad("queue_capacity must be in [1, 64]");
+  if (c->warmup_steps < 0 || c->warmup_steps > 100000) return bad("warmup_steps out of range");
+  return LBSIM_OK;
+#undef bad
+}
+
+void derive_params(const lbsim_config_t& c, SimParams& p) {
+  memset(&p, 0, sizeof(p));
+  p.B = c.num_envs;
+  p.S = c.num_servers;
+  p.Q = c.queue_capacity;
+  p.dt_us = (int32_t)std::llround((double)c.step_interval * 1e6);
+  p.mean_gap_us = (float)(1e6 / (double)c.arrival_rate);
+  for (int s = 0; s < MAX_S; ++s)
+    p.svc_scale[s] = s < c.num_servers ? (float)(1e6 / (double)c.server_rate[s]) : 0.0f;
+  p.key0 = (uint32_t)(c.seed & 0xFFFFFFFFull);
+  p.key1 = (uint32_t)(c.seed >> 32);
+  p.env_id_offset = (uint32_t)c.env_id_offset;
+  p.policy = c.assign_policy;
+  p.action_type = c.action_type;
+  p.num_discrete = c.num_discrete;
+  for (int i = 0; i < 8; ++i) p.dw[i] = c.discrete_weights[i];
+  p.min_w = c.min_weight;
+  p.max_w = c.max_weight;
+  p.warmup_steps = c.warmup_steps;
+  p.max_steps = c.max_steps;
+  p.reward_metric = c.reward_metric;
+  p.reward_field = c.reward_field;
+  p.decay_c = (float)(std::log2((double)c.decay_factor) / 1000.0);
+  p.normalize = c.normalize_obs ? 1 : 0;
+}
+
+// State sections in snapshot order.
+struct Section {
+  void** ptr;
+  size_t bytes;
+};
+
+std::vector<Section> sections(lbsim_t* h) {
+  const size_t B = h->B, BS = (size_t)h->B * h->S, BSQ = BS * h->Q, BSK = BS * K;
+  DevState& s = h->st;
+  std::vector<Section> v = {
+      {(void**)&s.next_arr, B * 4},   {(void**)&s.next_work, B * 4}, {(void**)&s.next_u2, B * 4},
+      {(void**)&s.next_u3, B * 4},    {(void**)&s.arr_idx, B * 4},   {(void**)&s.episode, B * 4},
+      {(void**)&s.clock, B * 4},      {(void**)&s.ep_step, B * 4},   {(void**)&s.dropped, B * 4},
+      {(void**)&s.norm_count, B * 4}, {(void**)&s.ep_return, B * 8}, {(void**)&s.hc, BS * 4},
+      {(void**)&s.last_tc, BS * 4},   {(void**)&s.res_count, BS * 4}, {(void**)&s.ring, BSQ * 8},
+      {(void**)&s.res_fct, BSK * 4},  {(void**)&s.res_dur, BSK * 4}, {(void**)&s.res_ts, BSK * 4},
+  };
+  if (h->cfg.normalize_obs) {
+    v.push_back({(void**)&s.norm_mean, BS * NF * 8});
+    v.push_back({(void**)&s.norm_std, BS * NF * 8});
+  }
+  return v;
+}
+
+__global__ void init_norm_std(double* p, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = 1.0;  // env.py:153 obs_std = ones
+}
+
+__global__ void copy_episode_stats(const int32_t* steps, const double* ret, int32_t* lo,
+                                   double* ro, int B) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  if (lo) lo[i] = steps[i];
+  if (ro) ro[i] = ret[i];
+}
+
+int launch_check(lbsim_t* h, const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(h, LBSIM_EDEVICE, "%s: %s", what, hipGetErrorString(e));
+  return LBSIM_OK;
+}
+
+// Brackets one launch with profiler events when profiling is on (class: see lbsim.h).
+struct ProfScope {
+  lbsim_t* h;
+  hipStream_t s;
+  bool rec = false;
+  ProfScope(lbsim_t* h_, hipStream_t s_, int cls) : h(h_), s(s_) {
+    Profiler& p = h->prof;
+    if (p.on && p.used + 2 <= p.ev.size()) {
+      rec = hipEventRecord(p.ev[p.used], s) == hipSuccess;
+      if (rec) p.cls.push_back(cls);
+    }
+  }
+  ~ProfScope() {
+    if (rec) {
+      (void)hipEventRecord(h->prof.ev[h->prof.used + 1], s);
+      h->prof.used += 2;
+    }
+  }
+};
+
+int launch_dynamics(lbsim_t* h, const void* action, int dtype, int32_t* assign,
+                    const uint8_t* mask, int mode, hipStream_t stream) {
+  const dim3 block(64), grid((unsigned)((h->B + 63) / 64));
+  ProfScope ps(h, stream, mode == kModeStep ? 0 : 2);
+  if (h->S <= 4)
+    hipLaunchKernelGGL(dynamics_kernel<4>, grid, block, 0, stream, h->st, h->prm, action, dtype,
+                       assign, mask, mode);
+  else if (h->S <= 8)
+    hipLaunchKernelGGL(dynamics_kernel<8>, grid, block, 0, stream, h->st, h->prm, action, dtype,
+                       assign, mask, mode);
+  else
+    hipLaunchKernelGGL(dynamics_kernel<16>, grid, block, 0, stream, h->st, h->prm, action, dtype,
+                       assign, mask, mode);
+  return launch_check(h, "dynamics_kernel");
+}
+
+int launch_observe(lbsim_t* h, const ObsOutputs& o, const uint8_t* mask, int mode,
+                   hipStream_t stream) {
+  ProfScope ps(h, stream, mode == kModeStep ? 1 : 3);
+  hipLaunchKernelGGL(observe_kernel, dim3((unsigned)h->B), dim3(64), 0, stream, h->st, h->prm, o,
+                     mask, mode);
+  return launch_check(h, "observe_kernel");
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* lbsim_version(void) { return "lbsim 0.1.0 (gfx950, HIP)"; }
+int lbsim_abi_version(void) { return LBSIM_ABI_VERSION; }
+
+int lbsim_config_default(lbsim_config_t* c) {
+  if (c == nullptr) return LBSIM_EINVAL;
+  memset(c, 0, sizeof(*c));
+  c->num_envs = 1;
+  c->num_servers = 4;
+  c->env_id_offset = 0;
+  c->seed = 0;
+  c->action_type = LBSIM_ACTION_DISCRETE;
+  c->num_discrete = 3;
+  c->discrete_weights[0] = 1.0f;
+  c->discrete_weights[1] = 1.5f;
+  c->discrete_weights[2] = 2.0f;
+  c->min_weight = 0.1f;
+  c->max_weight = 10.0f;
+  c->reward_metric = LBSIM_METRIC_JAIN;
+  c->reward_field = 10;
+  c->step_interval = 0.25f;
+  c->max_steps = 10000;
+  c->normalize_obs = 0;
+  c->assign_policy = LBSIM_POLICY_SED;
+  c->arrival_source = LBSIM_ARRIVAL_POISSON;
+  c->arrival_rate = 400.0f;
+  for (int s = 0; s < LBSIM_MAX_SERVERS; ++s) c->server_rate[s] = 125.0f;
+  c->decay_factor = 0.9f;
+  c->queue_capacity = 32;
+  c->warmup_steps = 8;
+  return LBSIM_OK;
+}
+
+int lbsim_config_validate(const lbsim_config_t* cfg, char* msg, size_t msg_len) {
+  return validate(cfg, msg, msg_len);
+}
+
+int lbsim_create(const lbsim_config_t* cfg, int device, lbsim_t** out) {
+  if (out == nullptr) return fail(nullptr, LBSIM_EINVAL, "out is NULL");
+  *out = nullptr;
+  char msg[256] = {0};
+  if (validate(cfg, msg, sizeof(msg)) != LBSIM_OK) return fail(nullptr, LBSIM_EINVAL, "%s", msg);
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(nullptr, LBSIM_EDEVICE, "no HIP device available");
+  if (device < 0 || device >= ndev)
+    return fail(nullptr, LBSIM_EINVAL, "device %d out of range [0, %d)", device, ndev);
+  DeviceGuard g(device);
+  if (!g.ok) return fail(nullptr, LBSIM_EDEVICE, "hipSetDevice(%d) failed", device);
+
+  lbsim_t* h = new lbsim_t();
+  h->cfg = *cfg;
+  h->device = device;
+  h->B = cfg->num_envs;
+  h->S = cfg->num_servers;
+  h->Q = cfg->queue_capacity;
+  h->initialised = false;
+  memset(&h->st, 0, sizeof(h->st));
+  derive_params(*cfg, h->prm);
+  for (Section& sec : sections(h)) {
+    void* p = nullptr;
+    if (hipMalloc(&p, sec.bytes) != hipSuccess) {
+      lbsim_destroy(h);
+      return fail(nullptr, LBSIM_ENOMEM, "hipMalloc(%zu) failed", sec.bytes);
+    }
+    h->allocs.push_back(p);
+    *sec.ptr = p;
+    if (hipMemset(p, 0, sec.bytes) != hipSuccess) {
+      lbsim_destroy(h);
+      return fail(nullptr, LBSIM_EDEVICE, "hipMemset failed");
+    }
+  }
+  if (cfg->normalize_obs) {
+    const size_t n = (size_t)h->B * h->S * NF;
+    hipLaunchKernelGGL(init_norm_std, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, nullptr,
+                       h->st.norm_std, n);
+  }
+  if (hipDeviceSynchronize() != hipSuccess) {
+    lbsim_destroy(h);
+    return fail(nullptr, LBSIM_EDEVICE, "device init failed");
+  }
+  *out = h;
+  return LBSIM_OK;
+}
+
+int lbsim_destroy(lbsim_t* h) {
+  if (h == nullptr) return LBSIM_OK;
+  {
+    DeviceGuard g(h->device);
+    for (void* p : h->allocs) (void)hipFree(p);
+    for (hipEvent_t e : h->prof.ev) (void)hipEventDestroy(e);
+  }
+  delete h;
+  return LBSIM_OK;
+}
+
+const char* lbsim_last_error(const lbsim_t* h) {
+  return h ? h->err.c_str() : g_create_err.c_str();
+}
+
+int lbsim_seed(lbsim_t* h, uint64_t seed) {
+  if (h == nullptr) return LBSIM_EINVAL;
+  DeviceGuard g(h->device);
+  h->cfg.seed = seed;
+  h->prm.key0 = (uint32_t)(seed & 0xFFFFFFFFull);
+  h->prm.key1 = (uint32_t)(seed >> 32);
+  if (hipMemset(h->st.episode, 0, (size_t)h->B * 4) != hipSuccess)
+    return fail(h, LBSIM_EDEVICE, "hipMemset failed");
+  return LBSIM_OK;
+}
+
+int lbsim_reset(lbsim_t* h, const uint8_t* env_mask, float* obs_out, void* stream) {
+  if (h == nullptr) return LBSIM_EINVAL;
+  if (obs_out == nullptr) return fail(h, LBSIM_EINVAL, "obs_out is NULL");
+  DeviceGuard g(h->device);
+  const hipStream_t s = (hipStream_t)stream;
+  int rc = launch_dynamics(h, nullptr, 0, nullptr, env_mask, kModeReset, s);
+  if (rc != LBSIM_OK) return rc;
+  const ObsOutputs o{obs_out, nullptr, nullptr, nullptr, nullptr, nullptr};
+  rc = launch_observe(h, o, env_mask, kModeReset, s);
+  if (rc != LBSIM_OK) return rc;
+  if (env_mask == nullptr) h->initialised = true;
+  return LBSIM_OK;
+}
+
+int lbsim_step(lbsim_t* h, const void* action, int action_dtype, float* obs_out,
+               float* reward_out, uint8_t* done_out, int32_t* assign_count_out, void* stream) {
+  lbsim_step_outputs_t o;
+  memset(&o, 0, sizeof(o));
+  o.obs = obs_out;
+  o.reward = reward_out;
+  o.done = done_out;
+  o.assign_count = assign_count_out;
+  return lbsim_step_ex(h, action, action_dtype, &o, stream);
+}
+
+size_t lbsim_config_size(void) { return sizeof(lbsim_config_t); }
+size_t lbsim_step_outputs_size(void) { return sizeof(lbsim_step_outputs_t); }
+
+int lbsim_step_ex(lbsim_t* h, const void* action, int action_dtype,
+                  const lbsim_step_outputs_t* out, void* stream) {
+  if (h == nullptr) return LBSIM_EINVAL;
+  if (!h->initialised) return fail(h, LBSIM_EINVAL, "call lbsim_reset before lbsim_step");
+  if (out == nullptr || action == nullptr || out->obs == nullptr || out->reward == nullptr ||
+      out->done == nullptr)
+    return fail(h, LBSIM_EINVAL, "action/obs/reward/done buffers must be non-NULL");
+  if (h->cfg.action_type == LBSIM_ACTION_DISCRETE) {
+    if (action_dtype != LBSIM_DTYPE_I32 && action_dtype != LBSIM_DTYPE_I64)
+      return fail(h, LBSIM_EINVAL, "discrete actions must be int32 or int64");
+  } else if (action_dtype != LBSIM_DTYPE_F32) {
+    return fail(h, LBSIM_EINVAL, "continuous actions must be float32");
+  }
+  DeviceGuard g(h->device);
+  const hipStream_t s = (hipStream_t)stream;
+  int rc = launch_dynamics(h, action, action_dtype, out->assign_count, nullptr, kModeStep, s);
+  if (rc != LBSIM_OK) return rc;
+  const ObsOutputs o{out->obs, out->reward, out->done, out->raw_obs, out->episode_length,
+                     out->episode_return};
+  return launch_observe(h, o, nullptr, kModeStep, s);
+}
+
+int lbsim_episode_stats(lbsim_t* h, int32_t* length_out, double* return_out, void* stream) {
+  if (h == nullptr) return LBSIM_EINVAL;
+  DeviceGuard g(h->device);
+  hipLaunchKernelGGL(copy_episode_stats, dim3((unsigned)((h->B + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, h->st.ep_step, h->st.ep_return, length_out, return_out,
+                     h->B);
+  return launch_check(h, "copy_episode_stats");
+}
+
+int lbsim_reward(const lbsim_config_t* cfg, const float* obs, int64_t n, float* reward_out,
+                 void* stream) {
+  if (cfg == nullptr || obs == nullptr || reward_out == nullptr || n < 0) return LBSIM_EINVAL;
+  if (cfg->num_servers < 1 || cfg->num_servers > LBSIM_MAX_SERVERS) return LBSIM_EINVAL;
+  if (cfg->reward_metric < 0 || cfg->reward_metric > 8) return LBSIM_EINVAL;
+  if (n == 0) return LBSIM_OK;
+  hipLaunchKernelGGL(reward_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, obs, n, cfg->num_servers, cfg->reward_metric,
+                     cfg->reward_field, reward_out);
+  return hipGetLastError() == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
+}
+
+int lbsim_reservoir_features(const float* values, const uint32_t* ts_ms, const uint32_t* counts,
+                             int64_t n, float decay_factor, float* feats_out, void* stream) {
+  if (values == nullptr || ts_ms == nullptr || counts == nullptr || feats_out == nullptr || n < 0)
+    return LBSIM_EINVAL;
+  if (!(decay_factor > 0.0f) || !(decay_factor < 1.0f)) return LBSIM_EINVAL;
+  if (n == 0) return LBSIM_OK;
+  const float c = (float)(std::log2((double)decay_factor) / 1000.0);
+  hipLaunchKernelGGL(features_kernel, dim3((unsigned)n), dim3(64), 0, (hipStream_t)stream, values,
+                     ts_ms, counts, c, feats_out);
+  return hipGetLastError() == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
+}
+
+int lbsim_profile_begin(lbsim_t* h, int max_launches) {
+  if (h == nullptr || max_launches < 1) return LBSIM_EINVAL;
+  DeviceGuard g(h->device);
+  Profiler& p = h->prof;
+  const size_t need = 2 * (size_t)max_launches;
+  while (p.ev.size() < need) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return fail(h, LBSIM_EDEVICE, "hipEventCreate failed");
+    p.ev.push_back(e);
+  }
+  p.used = 0;
+  p.cls.clear();
+  p.on = true;
+  return LBSIM_OK;
+}
+
+int lbsim_profile_end(lbsim_t* h, double* ms_out, int64_t* count_out) {
+  if (h == nullptr) return LBSIM_EINVAL;
+  DeviceGuard g(h->device);
+  Profiler& p = h->prof;
+  double ms[4] = {0, 0, 0, 0};
+  int64_t cnt[4] = {0, 0, 0, 0};
+  if (p.used > 0 && hipEventSynchronize(p.ev[p.used - 1]) != hipSuccess)
+    return fail(h, LBSIM_EDEVICE, "hipEventSynchronize failed");
+  for (size_t i = 0; i < p.cls.size(); ++i) {
+    float t = 0.0f;
+    if (hipEventElapsedTime(&t, p.ev[2 * i], p.ev[2 * i + 1]) != hipSuccess)
+      return fail(h, LBSIM_EDEVICE, "hipEventElapsedTime failed");
+    ms[p.cls[i]] += t;
+    cnt[p.cls[i]] += 1;
+  }
+  p.on = false;
+  p.used = 0;
+  p.cls.clear();
+  for (int i = 0; i < 4; ++i) {
+    if (ms_out) ms_out[i] = ms[i];
+    if (count_out) count_out[i] = cnt[i];
+  }
+  return LBSIM_OK;
+}
+
+int lbsim_state_size(const lbsim_t* h, size_t* bytes_out) {
+  if (h == nullptr || bytes_out == nullptr) return LBSIM_EINVAL;
+  size_t t = 0;
+  for (const Section& s : sections(const_cast<lbsim_t*>(h))) t += s.bytes;
+  *bytes_out = t;
+  return LBSIM_OK;
+}
+
+int lbsim_get_state(lbsim_t* h, void* host_buf, size_t bytes) {
+  if (h == nullptr || host_buf == nullptr) return LBSIM_EINVAL;
+  size_t need = 0;
+  lbsim_state_size(h, &need);
+  if (bytes != need) return fail(h, LBSIM_ESHAPE, "state buffer is %zu bytes, need %zu", bytes, need);
+  DeviceGuard g(h->device);
+  if (hipDeviceSynchronize() != hipSuccess) return fail(h, LBSIM_EDEVICE, "sync failed");
+  char* dst = (char*)host_buf;
+  for (const Section& s : sections(h)) {
+    if (hipMemcpy(dst, *s.ptr, s.bytes, hipMemcpyDeviceToHost) != hipSuccess)
+      return fail(h, LBSIM_EDEVICE, "hipMemcpy D2H failed");
+    dst += s.bytes;
+  }
+  return LBSIM_OK;
+}
+
+int lbsim_set_state(lbsim_t* h, const void* host_buf, size_t bytes) {
+  if (h == nullptr || host_buf == nullptr) return LBSIM_EINVAL;
+  size_t need = 0;
+  lbsim_state_size(h, &need);
+  if (bytes != need) return fail(h, LBSIM_ESHAPE, "state buffer is %zu bytes, need %zu", bytes, need);
+  DeviceGuard g(h->device);
+  if (hipDeviceSynchronize() != hipSuccess) return fail(h, LBSIM_EDEVICE, "sync failed");
+  const char* src = (const char*)host_buf;
+  for (const Section& s : sections(h)) {
+    if (hipMemcpy(*s.ptr, src, s.bytes, hipMemcpyHostToDevice) != hipSuccess)
+      return fail(h, LBSIM_EDEVICE, "hipMemcpy H2D failed");
+    src += s.bytes;
+  }
+  h->initialised = true;
+  return LBSIM_OK;
+}
+
+}  // extern "C"

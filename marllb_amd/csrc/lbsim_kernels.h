@@ -1,0 +1,774 @@
+// lbsim_kernels.h — gfx950 kernels of the vectorised LB environment.
+//
+//   dynamics_kernel<MAXS>  one LANE per env: Poisson arrivals -> SED/LSQ assignment (node.c:388-441)
+//                          -> per-server FIFO service -> completion samples (lbhash.h:116-135) ->
+//                          Algorithm R reservoir inserts (reservoir.py:50-85).  Integer/fp32
+//                          sequential work whose trip count differs per env, so lanes (not waves)
+//                          carry envs; state stays in VGPRs for the whole step.
+//   observe_kernel         one WAVE per env: per server, the 128-slot reservoirs are read
+//                          coalesced (2 slots/lane), bitonic-sorted across the wave, and reduced
+//                          into the 11-column observation (features.py:256-286), then reward
+//                          (rewards.py:290-381), done/return bookkeeping (env.py:261-281) and
+//                          optional running normalisation (env.py:450-470).
+//   features_kernel        the observe-kernel feature routine on caller-given reservoirs.
+//   reward_kernel          the observe-kernel reward routine on caller-given observations.
+//
+// Bit-reproducibility rules: compiled with -ffp-contract=off; only IEEE basic
+// ops on the state path; every floating sum that feeds an output follows numpy's pairwise order.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lbsim_math.h"
+
+namespace lbk {
+
+constexpr int K = 128;   // reservoir slots (reservoir.py:31)
+constexpr int NF = 11;   // observation columns (env.py:46-48)
+constexpr int MAX_S = 16;
+constexpr int32_t kLastNone = -(1 << 30);
+constexpr int kModeStep = 0;
+constexpr int kModeReset = 1;
+
+struct DevState {
+  // per env [B]
+  int32_t* next_arr;    // relative us of the next arrival (>= 0 after rebase)
+  float* next_work;     // Exp(1) work of the next arrival
+  uint32_t* next_u2;    // hash word of the next arrival (SED start / first 2-choice candidate)
+  uint32_t* next_u3;    // second 2-choice candidate
+  uint32_t* arr_idx;    // Philox counter of the next arrival
+  uint32_t* episode;    // episode index (RNG counter word z)
+  uint32_t* clock;      // simulated steps since reset (warm-up included)
+  int32_t* ep_step;     // user-visible step in episode (env.py:230)
+  uint32_t* dropped;    // arrivals dropped because every server queue was full (this episode)
+  int32_t* norm_count;  // running-normalisation count (env.py:461)
+  double* ep_return;    // episode return (env.py:264)
+  // per server [B*S]
+  uint32_t* hc;         // ring head | count << 16
+  int32_t* last_tc;     // completion time of the last popped flow (relative us)
+  uint32_t* res_count;  // samples offered to the reservoirs (Algorithm R count)
+  // ring [B*S*Q] of {t_complete, t_arrival}, relative us
+  int2* ring;
+  // reservoirs [B*S*K]
+  float* res_fct;
+  float* res_dur;
+  uint32_t* res_ts;     // sample time, integer ms since episode start
+  // running normalisation [B*S*11] (nullptr when disabled)
+  double* norm_mean;
+  double* norm_std;
+};
+
+struct SimParams {
+  int32_t B, S, Q;
+  int32_t dt_us;
+  float mean_gap_us;
+  float svc_scale[MAX_S];
+  uint32_t key0, key1;
+  uint32_t env_id_offset;
+  int32_t policy;
+  int32_t action_type;
+  int32_t num_discrete;
+  float dw[8];
+  float min_w, max_w;
+  int32_t warmup_steps;
+  int32_t max_steps;
+  int32_t reward_metric;
+  int32_t reward_field;
+  float decay_c;  // log2(decay_factor) / 1000, per integer millisecond of age
+  int32_t normalize;
+};
+
+// ================================================================ dynamics (one lane = one env)
+
+template <int MAXS>
+struct LaneState {
+  int32_t cnt[MAXS], head[MAXS];
+  int32_t head_tc[MAXS], head_ta[MAXS], tail_tc[MAXS], last_tc[MAXS];
+  uint32_t rcnt[MAXS];
+  int32_t assigned[MAXS];
+  float score[MAXS];
+  double den[MAXS];
+  int32_t next_arr;
+  float next_work;
+  uint32_t u2, u3, arr_idx, episode, clock, dropped;
+  uint32_t gid;
+};
+
+// SED score (n_flow_on + 1) / (1e-9 + w) in double, stored as f32 (node.c:393-399); LSQ: n.
+__device__ __forceinline__ float policy_score(int policy, int32_t cnt, double den) {
+  if (policy == 2 /*LSQ*/ || policy == 3 /*LSQ2*/) return (float)cnt;
+  return (float)((double)(cnt + 1) / den);
+}
+
+template <int MAXS>
+__device__ __forceinline__ void res_insert(const DevState& st, const SimParams& p,
+                                           LaneState<MAXS>& L, int s, size_t sbase, float fct,
+                                           float dur, uint32_t ts_ms) {
+  const uint32_t c = L.rcnt[s];
+  int slot;
+  if (c < (uint32_t)K) {
+    slot = (int)c;
+  } else {
+    const u32x4 d = philox4x32_10(
+        u32x4{c >> 1, L.gid, L.episode, (kStreamReservoir << 24) | (uint32_t)s}, p.key0, p.key1);
+    const uint32_t hi = (c & 1u) ? d.w : d.y;
+    const uint32_t lo = (c & 1u) ? d.z : d.x;
+    const uint64_t j = mulhi64_by_u33(hi, lo, (uint64_t)c + 1u);
+    slot = j < (uint64_t)K ? (int)j : -1;
+  }
+  if (slot >= 0) {
+    const size_t r = sbase * K + (size_t)slot;
+    st.res_fct[r] = fct;
+    st.res_dur[r] = dur;
+    st.res_ts[r] = ts_ms;
+  }
+  if (c != 0xFFFFFFFFu) L.rcnt[s] = c + 1u;
+}
+
+// Pop every flow of server s completed at or before time t (relative us); each completion
+// yields one fct sample (t_complete - t_arrival, lbhash.h:116-124) and one duration sample
+// (t_complete - t_service_start) that share one Algorithm R decision (reservoir.py:261-265).
+template <int MAXS>
+__device__ __forceinline__ void pop_until(const DevState& st, const SimParams& p,
+                                          LaneState<MAXS>& L, int s, size_t b, int32_t t,
+                                          uint64_t base_us) {
+  const size_t sbase = b * (size_t)p.S + (size_t)s;
+  while (L.cnt[s] > 0 && L.head_tc[s] <= t) {
+    const int32_t tc = L.head_tc[s], ta = L.head_ta[s];
+    const int32_t start = ta > L.last_tc[s] ? ta : L.last_tc[s];
+    const float fct = (float)(tc - ta) * 1.0e-6f;
+    const float dur = (float)(tc - start) * 1.0e-6f;
+    L.last_tc[s] = tc;
+    const uint32_t ts_ms = (uint32_t)((base_us + (uint64_t)(int64_t)tc) / 1000u);
+    res_insert<MAXS>(st, p, L, s, sbase, fct, dur, ts_ms);
+    int h = L.head[s] + 1;
+    if (h == p.Q) h = 0;
+    L.head[s] = h;
+    L.cnt[s] -= 1;
+    if (L.cnt[s] > 0) {
+      const int2 e = st.ring[sbase * p.Q + h];
+      L.head_tc[s] = e.x;
+      L.head_ta[s] = e.y;
+    }
+    L.score[s] = policy_score(p.policy, L.cnt[s], L.den[s]);
+  }
+}
+
+template <int MAXS>
+__device__ __forceinline__ void draw_arrival(const SimParams& p, LaneState<MAXS>& L,
+                                             int32_t t_prev) {
+  const u32x4 d = philox4x32_10(u32x4{L.arr_idx, L.gid, L.episode, kStreamArrival << 24},
+                                p.key0, p.key1);
+  const int32_t gap = (int32_t)(-lb_logf(u01_open0(d.x)) * p.mean_gap_us);
+  L.next_arr = t_prev + gap;
+  L.next_work = -lb_logf(u01_open0(d.y));
+  L.u2 = d.z;
+  L.u3 = d.w;
+}
+
+// One simulated step of dt_us with server weights w[] (env.py:230-259 with real dynamics).
+template <int MAXS>
+__device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
+                                         LaneState<MAXS>& L, size_t b, const float* w) {
+  const int S = p.S, Q = p.Q;
+  const uint64_t base_us = (uint64_t)L.clock * (uint64_t)p.dt_us;
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) {
+    if (s < S) {
+      L.den[s] = (double)w[s] + 1e-9;
+      L.score[s] = policy_score(p.policy, L.cnt[s], L.den[s]);
+    }
+  }
+  while (L.next_arr < p.dt_us) {
+    const int32_t ta = L.next_arr;
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s)
+      if (s < S) pop_until<MAXS>(st, p, L, s, b, ta, base_us);
+
+    // ---- choose a server (node.c:388-441); full servers (Q in flight) are not eligible
+    int chosen = -1;
+    if (p.policy == 1 || p.policy == 3) {  // SED2 / LSQ2: two uniform candidates
+      const int h1 = (int)(((uint64_t)L.u2 * (uint64_t)S) >> 32);
+      const int h2 = (int)(((uint64_t)L.u3 * (uint64_t)S) >> 32);
+      float s1 = 0.f, s2 = 0.f;
+      bool ok1 = false, ok2 = false;
+#pragma unroll
+      for (int s = 0; s < MAXS; ++s) {
+        if (s == h1) { s1 = L.score[s]; ok1 = L.cnt[s] < Q; }
+        if (s == h2) { s2 = L.score[s]; ok2 = L.cnt[s] < Q; }
+      }
+      if (ok1 && ok2) chosen = (s2 < s1) ? h2 : h1;
+      else if (ok1) chosen = h1;
+      else if (ok2) chosen = h2;
+    } else {  // SED / LSQ: start at the hashed server, strict '<' scan in index order
+      const int h = (int)(((uint64_t)L.u2 * (uint64_t)S) >> 32);
+      float best = 0.f;
+#pragma unroll
+      for (int s = 0; s < MAXS; ++s)
+        if (s == h && L.cnt[s] < Q) { chosen = s; best = L.score[s]; }
+#pragma unroll
+      for (int s = 0; s < MAXS; ++s) {
+        if (s < S && L.cnt[s] < Q) {
+          if (chosen < 0 || L.score[s] < best) { chosen = s; best = L.score[s]; }
+        }
+      }
+    }
+
+    if (chosen < 0) {
+      L.dropped += 1u;
+    } else {
+#pragma unroll
+      for (int s = 0; s < MAXS; ++s) {
+        if (s == chosen) {
+          const size_t sbase = b * (size_t)S + (size_t)s;
+          const int32_t start = L.cnt[s] > 0 ? (L.tail_tc[s] > ta ? L.tail_tc[s] : ta) : ta;
+          int32_t svc = (int32_t)(L.next_work * p.svc_scale[s]);
+          if (svc < 1) svc = 1;
+          const int32_t tc = start + svc;
+          int pos = L.head[s] + L.cnt[s];
+          if (pos >= Q) pos -= Q;
+          st.ring[sbase * Q + pos] = make_int2(tc, ta);
+          if (L.cnt[s] == 0) { L.head_tc[s] = tc; L.head_ta[s] = ta; }
+          L.cnt[s] += 1;
+          L.tail_tc[s] = tc;
+          L.assigned[s] += 1;
+          L.score[s] = policy_score(p.policy, L.cnt[s], L.den[s]);
+        }
+      }
+    }
+    L.arr_idx += 1u;
+    draw_arrival<MAXS>(p, L, ta);
+  }
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s)
+    if (s < S) pop_until<MAXS>(st, p, L, s, b, p.dt_us, base_us);
+
+  // ---- rebase relative times to the next step's start
+  const int32_t dt = p.dt_us;
+  L.next_arr -= dt;
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) {
+    if (s < S) {
+      const size_t sbase = b * (size_t)S + (size_t)s;
+      int pos = L.head[s];
+      for (int i = 0; i < L.cnt[s]; ++i) {
+        int2 e = st.ring[sbase * Q + pos];
+        e.x -= dt;
+        e.y -= dt;
+        st.ring[sbase * Q + pos] = e;
+        pos = (pos + 1 == Q) ? 0 : pos + 1;
+      }
+      L.head_tc[s] -= dt;
+      L.head_ta[s] -= dt;
+      L.tail_tc[s] -= dt;
+      L.last_tc[s] = (L.last_tc[s] < kLastNone + dt) ? kLastNone : L.last_tc[s] - dt;
+    }
+  }
+  L.clock += 1u;
+}
+
+__device__ __forceinline__ float action_weight(const SimParams& p, const void* action, int dtype,
+                                               size_t idx) {
+  if (p.action_type == 0) {  // discrete: discrete_weights[int(a)] (env.py:344-346)
+    int64_t a = (dtype == 1) ? ((const int64_t*)action)[idx]
+                             : (int64_t)((const int32_t*)action)[idx];
+    if (a < 0) a += p.num_discrete;  // python negative indexing
+    if (a < 0) a = 0;
+    if (a >= p.num_discrete) a = p.num_discrete - 1;
+    return p.dw[a];
+  }
+  // continuous: np.clip(f32(a), min_w, max_w) (env.py:349-351); NaN passes through
+  const float a = ((const float*)action)[idx];
+  return a < p.min_w ? p.min_w : (a > p.max_w ? p.max_w : a);
+}
+
+template <int MAXS>
+__global__ void __launch_bounds__(64)
+    dynamics_kernel(DevState st, SimParams p, const void* action, int action_dtype,
+                    int32_t* assign_out, const uint8_t* reset_mask, int mode) {
+  const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= (size_t)p.B) return;
+  const int S = p.S;
+  LaneState<MAXS> L;
+  L.gid = p.env_id_offset + (uint32_t)b;
+
+  if (mode == kModeReset) {
+    if (reset_mask != nullptr && reset_mask[b] == 0) return;
+    L.episode = st.episode[b] + 1u;
+    L.clock = 0u;
+    L.dropped = 0u;
+    L.arr_idx = 0u;
+    draw_arrival<MAXS>(p, L, 0);
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) {
+      L.cnt[s] = 0; L.head[s] = 0; L.head_tc[s] = 0; L.head_ta[s] = 0; L.tail_tc[s] = 0;
+      L.last_tc[s] = kLastNone; L.rcnt[s] = 0u; L.assigned[s] = 0;
+    }
+    float w1[MAXS];
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) w1[s] = 1.0f;
+    for (int k = 0; k < p.warmup_steps; ++k) sim_step<MAXS>(st, p, L, b, w1);
+    st.ep_step[b] = 0;
+    st.ep_return[b] = 0.0;
+  } else {
+    L.episode = st.episode[b];
+    L.clock = st.clock[b];
+    L.dropped = st.dropped[b];
+    L.arr_idx = st.arr_idx[b];
+    L.next_arr = st.next_arr[b];
+    L.next_work = st.next_work[b];
+    L.u2 = st.next_u2[b];
+    L.u3 = st.next_u3[b];
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) {
+      if (s < S) {
+        const size_t sb = b * (size_t)S + (size_t)s;
+        const uint32_t hc = st.hc[sb];
+        L.head[s] = (int32_t)(hc & 0xFFFFu);
+        L.cnt[s] = (int32_t)(hc >> 16);
+        L.last_tc[s] = st.last_tc[sb];
+        L.rcnt[s] = st.res_count[sb];
+        L.assigned[s] = 0;
+        if (L.cnt[s] > 0) {
+          const int2 e = st.ring[sb * p.Q + L.head[s]];
+          L.head_tc[s] = e.x;
+          L.head_ta[s] = e.y;
+          int tp = L.head[s] + L.cnt[s] - 1;
+          if (tp >= p.Q) tp -= p.Q;
+          L.tail_tc[s] = st.ring[sb * p.Q + tp].x;
+        } else {
+          L.head_tc[s] = 0; L.head_ta[s] = 0; L.tail_tc[s] = 0;
+        }
+      }
+    }
+    float w[MAXS];
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s)
+      w[s] = (s < S) ? action_weight(p, action, action_dtype, b * (size_t)S + (size_t)s) : 1.0f;
+    sim_step<MAXS>(st, p, L, b, w);
+    if (assign_out != nullptr) {
+#pragma unroll
+      for (int s = 0; s < MAXS; ++s)
+        if (s < S) assign_out[b * (size_t)S + (size_t)s] = L.assigned[s];
+    }
+  }
+  st.episode[b] = L.episode;
+  st.clock[b] = L.clock;
+  st.dropped[b] = L.dropped;
+  st.arr_idx[b] = L.arr_idx;
+  st.next_arr[b] = L.next_arr;
+  st.next_work[b] = L.next_work;
+  st.next_u2[b] = L.u2;
+  st.next_u3[b] = L.u3;
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) {
+    if (s < S) {
+      const size_t sb = b * (size_t)S + (size_t)s;
+      st.hc[sb] = (uint32_t)L.head[s] | ((uint32_t)L.cnt[s] << 16);
+      st.last_tc[sb] = L.last_tc[s];
+      st.res_count[sb] = L.rcnt[s];
+    }
+  }
+}
+
+// ================================================================ wave-level helpers (wave64)
+
+__device__ __forceinline__ uint32_t shfl_xor_u32(uint32_t v, int m) {
+  return (uint32_t)__shfl_xor((int)v, m, 64);
+}
+__device__ __forceinline__ uint32_t shfl_up_u32(uint32_t v, int d) {
+  return (uint32_t)__shfl_up((int)v, (unsigned)d, 64);
+}
+__device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int src) {
+  return (uint32_t)__shfl((int)v, src, 64);
+}
+__device__ __forceinline__ uint32_t readlane_u32(uint32_t v, int lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) {
+    const uint32_t o = shfl_xor_u32(v, m);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+// Bitonic sort of 128 (key, payload) pairs; element i = lane + 64*h lives in (k[h], v[h]).
+// Equal keys never swap, so the network is a deterministic permutation on every backend.
+__device__ __forceinline__ void bitonic128(uint32_t (&k)[2], uint32_t (&v)[2], int lane) {
+#pragma unroll
+  for (int kk = 2; kk <= 128; kk <<= 1) {
+#pragma unroll
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      if (j == 64) {  // only at kk == 128: ascending, partner in the same lane
+        if (k[0] > k[1]) {
+          const uint32_t tk = k[0], tv = v[0];
+          k[0] = k[1]; v[0] = v[1];
+          k[1] = tk; v[1] = tv;
+        }
+      } else {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int i = lane + 64 * h;
+          const uint32_t pk = shfl_xor_u32(k[h], j);
+          const uint32_t pv = shfl_xor_u32(v[h], j);
+          const bool up = (i & kk) == 0;
+          const bool lower = (i & j) == 0;
+          const bool take = (lower == up) ? (pk < k[h]) : (pk > k[h]);
+          if (take) { k[h] = pk; v[h] = pv; }
+        }
+      }
+    }
+  }
+}
+
+// Inclusive wave scan of a u64 held as (hi, lo).
+__device__ __forceinline__ uint64_t wave_scan_u64(uint64_t x, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t lo = shfl_up_u32((uint32_t)x, d);
+    const uint32_t hi = shfl_up_u32((uint32_t)(x >> 32), d);
+    if (lane >= d) x += ((uint64_t)hi << 32) | lo;
+  }
+  return x;
+}
+
+// numpy pairwise summation (numpy/_core/src/umath/loops_utils.h.src, n <= 128): for n < 8 a
+// sequential sum from 0; else 8 strided accumulators, combined ((r0+r1)+(r2+r3))+((r4+r5)+
+// (r6+r7)), then the n % 8 tail added in order.  A group of 8 lanes (j = lane & 7) evaluates one
+// sum; `term(i)` gives element i.  Every lane of the group returns the same bits.
+template <typename T, typename F>
+__device__ __forceinline__ T pairwise_group(int n, int lane, F term) {
+  if (n < 8) {
+    T r = (T)0;
+    for (int i = 0; i < n; ++i) r += term(i);
+    return r;
+  }
+  const int j = lane & 7, g0 = lane & ~7;
+  const int m8 = n - (n % 8);
+  T acc = term(j);
+  for (int i = 8 + j; i < m8; i += 8) acc += term(i);
+  T r[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) r[q] = __shfl(acc, g0 + q, 64);
+  T res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (int i = m8; i < n; ++i) res += term(i);
+  return res;
+}
+
+// ================================================================ features of one server
+
+struct FeatScratch {
+  float v[2][K];    // fct, duration values by slot
+  float w[K];       // decay weight by slot (f32)
+  uint64_t wq[K];   // decay weight in 2^-48 fixed point (exact, order-free sums)
+};
+
+// Features of the two reservoirs (fct, duration) of one server that share their timestamps.
+// n = min(count, K).  out[r][0..4] = {mean, p90, std, mean_decay, p90_decay}  (reservoir.py:105-
+// 196 with numpy 2 float32 semantics; decay weights relative to the newest sample).
+__device__ __forceinline__ void server_features(const float* __restrict__ v0, const float* __restrict__ v1,
+                                const uint32_t* __restrict__ ts, uint32_t count, float decay_c,
+                                FeatScratch& sc, float (&out)[2][5], int lane) {
+  const int n = count < (uint32_t)K ? (int)count : K;
+  if (n == 0) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int f = 0; f < 5; ++f) out[r][f] = 0.0f;
+    return;
+  }
+  float a[2][2];
+  uint32_t t[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int slot = lane + 64 * h;
+    const bool valid = slot < n;
+    a[0][h] = valid ? v0[slot] : 0.0f;
+    a[1][h] = valid ? v1[slot] : 0.0f;
+    t[h] = valid ? ts[slot] : 0u;
+  }
+  const uint32_t newest = wave_max_u32(t[0] > t[1] ? t[0] : t[1]);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int slot = lane + 64 * h;
+    const bool valid = slot < n;
+    const float w = valid ? lb_exp2f((float)(newest - t[h]) * decay_c) : 0.0f;
+    sc.v[0][slot] = a[0][h];
+    sc.v[1][slot] = a[1][h];
+    sc.w[slot] = w;
+    sc.wq[slot] = (uint64_t)(w * 281474976710656.0f);  // * 2^48, exact scaling
+  }
+  __syncthreads();
+
+  // ---- mean (f32 pairwise) of fct (lanes 0-7) and duration (lanes 8-15)
+  const int grp = lane >> 3;
+  const float* arr = sc.v[grp & 1];
+  const float sum32 = pairwise_group<float>(n, lane, [&](int i) { return arr[i]; });
+  const float fn = (float)n;
+  const float mean_g = sum32 / fn;
+  float mean[2];
+  mean[0] = __shfl(mean_g, 0, 64);
+  mean[1] = __shfl(mean_g, 8, 64);
+  // ---- std: sqrt(pairwise((x - mean)^2) / n) in f32 (np.std, ddof 0)
+  const float mg = mean[grp & 1];
+  const float ss32 = pairwise_group<float>(n, lane, [&](int i) {
+    const float d = arr[i] - mg;
+    return d * d;
+  });
+  const float sd_g = sqrtf(ss32 / fn);
+  float sd[2];
+  sd[0] = __shfl(sd_g, 0, 64);
+  sd[1] = __shfl(sd_g, 8, 64);
+  // ---- decay-weighted mean in f64: pairwise(v*w) / pairwise(w) (np.average, weights f64)
+  //      lanes 0-7: sum w; 8-15: sum fct*w; 16-23: sum dur*w
+  const int g3 = grp < 3 ? grp : 2;
+  const float* arr3 = sc.v[g3 == 2 ? 1 : 0];
+  const double sum64 = pairwise_group<double>(n, lane, [&](int i) {
+    const double x = (g3 == 0) ? 1.0 : (double)arr3[i];
+    return x * (double)sc.w[i];
+  });
+  const double sw = __shfl(sum64, 0, 64);
+  float md[2];
+  md[0] = (float)(__shfl(sum64, 8, 64) / sw);
+  md[1] = (float)(__shfl(sum64, 16, 64) / sw);
+
+  // ---- order statistics: sort each reservoir, p90 (linear) and decay-weighted p90
+  const float q = 0.9f;
+  const float hidx = (float)(n - 1) * q;  // numpy 2: (n - 1) * float32(90 / 100)
+  const float fl = floorf(hidx);
+  const int lo = (int)fl;
+  const float g = hidx - fl;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    uint32_t key[2], pay[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int slot = lane + 64 * h;
+      key[h] = slot < n ? as_u32(a[r][h]) : 0xFFFFFFFFu;  // values >= 0: bits are monotone
+      pay[h] = (uint32_t)slot;
+    }
+    bitonic128(key, pay, lane);
+    const float va = as_f32(readlane_u32(lo >= 64 ? key[1] : key[0], lo & 63));
+    const int lo1 = (lo + 1 < n) ? lo + 1 : lo;
+    const float vb = as_f32(readlane_u32(lo1 >= 64 ? key[1] : key[0], lo1 & 63));
+    const float diff = vb - va;
+    const float p90 = (g >= 0.5f) ? (vb - diff * (1.0f - g)) : (va + diff * g);
+
+    // cumulative fixed-point weight in sorted order; first position with cum >= 0.9 * total
+    const uint64_t c0 = wave_scan_u64(sc.wq[pay[0]], lane);
+    const uint64_t t0 = ((uint64_t)readlane_u32((uint32_t)(c0 >> 32), 63) << 32) |
+                        readlane_u32((uint32_t)c0, 63);
+    const uint64_t c1 = wave_scan_u64(sc.wq[pay[1]], lane) + t0;
+    const uint64_t total = ((uint64_t)readlane_u32((uint32_t)(c1 >> 32), 63) << 32) |
+                           readlane_u32((uint32_t)c1, 63);
+    const uint64_t cut9 = total * 9u;
+    const uint64_t m0 = __ballot(c0 * 10u >= cut9);
+    const uint64_t m1 = __ballot(c1 * 10u >= cut9);
+    const int idx = m0 ? __builtin_ctzll(m0) : 64 + __builtin_ctzll(m1);
+    const float p90d = as_f32(readlane_u32(idx >= 64 ? key[1] : key[0], idx & 63));
+
+    out[r][0] = mean[r];
+    out[r][1] = p90;
+    out[r][2] = sd[r];
+    out[r][3] = md[r];
+    out[r][4] = p90d;
+  }
+  __syncthreads();  // scratch is reused by the next server
+}
+
+// ================================================================ reward (rewards.py)
+
+// numpy pairwise sum of a small f64 array (n <= 16) in one thread.
+__device__ __forceinline__ double pw_sum64(const double* x, int n) {
+  if (n < 8) {
+    double r = 0.0;
+    for (int i = 0; i < n; ++i) r += x[i];
+    return r;
+  }
+  double r[8];
+  for (int q = 0; q < 8; ++q) r[q] = x[q];
+  const int m8 = n - (n % 8);
+  for (int i = 8; i < m8; i += 8)
+    for (int q = 0; q < 8; ++q) r[q] += x[i + q];
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (int i = m8; i < n; ++i) res += x[i];
+  return res;
+}
+
+__device__ __forceinline__ double np_var64(const double* x, int n) {
+  const double mean = pw_sum64(x, n) / (double)n;
+  double d[MAX_S];
+  for (int i = 0; i < n; ++i) {
+    const double t = x[i] - mean;
+    d[i] = t * t;
+  }
+  return pw_sum64(d, n) / (double)n;
+}
+
+// RewardFunction.compute on one (S, 11) observation (rewards.py:329-381): values of the active
+// servers (any column > 0, env.py:410-413) at column `field`, metric in float64.
+__device__ double reward_of(const float* obs, int S, int metric, int field) {
+  if (field < 0 || field >= NF) return 0.0;
+  double x[MAX_S];
+  int n = 0;
+  for (int s = 0; s < S; ++s) {
+    bool active = false;
+    for (int f = 0; f < NF; ++f) active |= obs[s * NF + f] > 0.0f;
+    if (active) x[n++] = (double)obs[s * NF + field];
+  }
+  if (n == 0) return 0.0;
+  const double eps = 1e-10;
+  switch (metric) {
+    case 0: {  // jain_fairness 21-67
+      const double sv = pw_sum64(x, n);
+      if (sv < eps) return 1.0;
+      double x2[MAX_S];
+      for (int i = 0; i < n; ++i) x2[i] = x[i] * x[i];
+      const double sq = pw_sum64(x2, n);
+      if (sq < eps) return 1.0;
+      const double j = (sv * sv) / ((double)n * sq);
+      const double lo = 1.0 / (double)n;
+      return j < lo ? lo : (j > 1.0 ? 1.0 : j);
+    }
+    case 1: return -np_var64(x, n);        // variance_fairness 70-94
+    case 2: return -sqrt(np_var64(x, n));  // std_fairness 97-114
+    case 3: {                              // coefficient_of_variation 117-144
+      const double mean = pw_sum64(x, n) / (double)n;
+      if (mean < eps) return 0.0;
+      return -(sqrt(np_var64(x, n)) / (mean + eps));
+    }
+    case 4: {  // max_min_fairness 147-171
+      double m = x[0];
+      for (int i = 1; i < n; ++i) m = x[i] > m ? x[i] : m;
+      return -m;
+    }
+    case 5: {  // min_max_fairness 174-191
+      double m = x[0];
+      for (int i = 1; i < n; ++i) m = x[i] < m ? x[i] : m;
+      return m;
+    }
+    case 6: {  // product_fairness 194-225
+      double l[MAX_S];
+      for (int i = 0; i < n; ++i) l[i] = log(x[i] + eps);
+      return pw_sum64(l, n);
+    }
+    case 7: {  // range_fairness 228-246
+      double mx = x[0], mn = x[0];
+      for (int i = 1; i < n; ++i) { mx = x[i] > mx ? x[i] : mx; mn = x[i] < mn ? x[i] : mn; }
+      return -(mx - mn);
+    }
+    case 8: {  // gini_coefficient 249-287
+      const double mean = pw_sum64(x, n) / (double)n;
+      if (mean == 0.0) return 0.0;
+      double ds = 0.0;
+      for (int i = 0; i < n; ++i)
+        for (int k = 0; k < n; ++k) ds += fabs(x[i] - x[k]);
+      return -(ds / ((double)(2 * n * n) * mean));
+    }
+    default: return 0.0;
+  }
+}
+
+// ================================================================ observe (one wave = one env)
+
+struct ObsOutputs {
+  float* obs;
+  float* reward;
+  uint8_t* done;
+  float* raw_obs;
+  int32_t* ep_len;
+  double* ep_ret;
+};
+
+__global__ void __launch_bounds__(64)
+    observe_kernel(DevState st, SimParams p, ObsOutputs out, const uint8_t* reset_mask, int mode) {
+  const size_t b = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (mode == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
+  __shared__ FeatScratch sc;
+  __shared__ float s_obs[MAX_S * NF];
+  const int S = p.S;
+  for (int s = 0; s < S; ++s) {
+    const size_t sb = b * (size_t)S + (size_t)s;
+    const uint32_t cnt = st.hc[sb] >> 16;
+    const uint32_t rc = st.res_count[sb];
+    float f[2][5];
+    server_features(st.res_fct + sb * K, st.res_dur + sb * K, st.res_ts + sb * K, rc, p.decay_c,
+                    sc, f, lane);
+    if (lane == 0) {
+      s_obs[s * NF + 0] = (float)cnt;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        s_obs[s * NF + 1 + q] = f[0][q];
+        s_obs[s * NF + 6 + q] = f[1][q];
+      }
+    }
+  }
+  __syncthreads();
+
+  if (mode == kModeStep && lane == 0) {
+    const double r = reward_of(s_obs, S, p.reward_metric, p.reward_field);
+    out.reward[b] = (float)r;
+    const int32_t es = st.ep_step[b] + 1;
+    const double er = st.ep_return[b] + r;
+    st.ep_step[b] = es;
+    st.ep_return[b] = er;
+    out.done[b] = (uint8_t)(es >= p.max_steps ? 1 : 0);
+    if (out.ep_len != nullptr) out.ep_len[b] = es;
+    if (out.ep_ret != nullptr) out.ep_ret[b] = er;
+  }
+
+  const int nobs = S * NF;
+  float* orow = out.obs + b * (size_t)nobs;
+  if (out.raw_obs != nullptr)
+    for (int e = lane; e < nobs; e += 64) out.raw_obs[b * (size_t)nobs + e] = s_obs[e];
+  if (p.normalize) {  // env.py:460-468, float64 running statistics
+    const int32_t cnt = st.norm_count[b] + 1;
+    for (int e = lane; e < nobs; e += 64) {
+      const size_t gi = b * (size_t)nobs + (size_t)e;
+      const double o = (double)s_obs[e];
+      double m = st.norm_mean[gi];
+      const double sdv = st.norm_std[gi];
+      const double delta = o - m;
+      m = m + delta / (double)cnt;
+      const double delta2 = o - m;
+      double v = (sdv * sdv * (double)(cnt - 1) + delta * delta2) / (double)cnt;
+      v = v > 1e-8 ? v : 1e-8;
+      const double ns = sqrt(v);
+      st.norm_mean[gi] = m;
+      st.norm_std[gi] = ns;
+      orow[e] = (float)((o - m) / (ns + 1e-8));
+    }
+    if (lane == 0) st.norm_count[b] = cnt;
+  } else {
+    for (int e = lane; e < nobs; e += 64) orow[e] = s_obs[e];
+  }
+}
+
+// ================================================================ stateless entry points
+
+__global__ void __launch_bounds__(64)
+    features_kernel(const float* values, const uint32_t* ts, const uint32_t* counts,
+                    float decay_c, float* out) {
+  const size_t r = blockIdx.x;
+  const int lane = threadIdx.x;
+  __shared__ FeatScratch sc;
+  float f[2][5];
+  server_features(values + r * K, values + r * K, ts + r * K, counts[r], decay_c, sc, f, lane);
+  if (lane == 0) {
+#pragma unroll
+    for (int q = 0; q < 5; ++q) out[r * 5 + q] = f[0][q];
+  }
+}
+
+__global__ void __launch_bounds__(256)
+    reward_kernel(const float* obs, int64_t n, int S, int metric, int field, float* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = (float)reward_of(obs + i * (int64_t)S * NF, S, metric, field);
+}
+
+}  // namespace lbk

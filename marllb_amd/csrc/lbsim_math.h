@@ -1,0 +1,93 @@
+// lbsim_math.h — bit-reproducible scalar math for the gfx950 kernels.
+//
+// Every function here is written with plain IEEE-754 binary32/binary64 +,-,*,/ and integer ops
+// only, and the whole library is compiled with -ffp-contract=off, so a kernel lane produces the
+// same bits as oracle/lbsim_oracle.c (gcc, -ffp-contract=off) for the same inputs.  That is what
+// makes the server-assignment indices and every integer state word bit-exact against the oracle
+// (DESIGN.md §3.1).  No hardware transcendental (v_exp_f32/v_log_f32) is used on the state path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lbk {
+
+// ---------------------------------------------------------------- Philox4x32-10 (Salmon et al.
+// SC'11, "Parallel random numbers: as easy as 1, 2, 3").  Counter-based: the draw for
+// (env, episode, stream, index) is a pure function, so no RNG state is stored per env.
+struct u32x4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+    const uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += W0;
+    k1 += W1;
+  }
+  return c;
+}
+
+// RNG streams (counter word w bits 24..31); see DESIGN.md §3.2.
+constexpr uint32_t kStreamArrival = 1u;
+constexpr uint32_t kStreamReservoir = 2u;
+
+// Uniform in (0, 1]: 24 high bits + 1, scaled by 2^-24 (exact in binary32).
+__device__ __forceinline__ float u01_open0(uint32_t r) {
+  return (float)((r >> 8) + 1u) * 5.9604644775390625e-8f;
+}
+
+__device__ __forceinline__ float as_f32(uint32_t u) { return __uint_as_float(u); }
+__device__ __forceinline__ uint32_t as_u32(float f) { return __float_as_uint(f); }
+
+// Natural log for x in [2^-24, 1]: m*2^e with m folded into [sqrt(1/2), sqrt(2)], then
+// ln m = 2 atanh(t), t = (m-1)/(m+1), odd series to t^9 (|t| <= 0.1716).
+__device__ __forceinline__ float lb_logf(float x) {
+  const uint32_t b = as_u32(x);
+  int e = (int)(b >> 23) - 127;
+  float m = as_f32((b & 0x007fffffu) | 0x3f800000u);
+  if (m > 1.41421354f) {
+    m = m * 0.5f;
+    e = e + 1;
+  }
+  const float t = (m - 1.0f) / (m + 1.0f);
+  const float t2 = t * t;
+  float p = 0.222222224f;
+  p = p * t2 + 0.285714298f;
+  p = p * t2 + 0.400000006f;
+  p = p * t2 + 0.666666687f;
+  p = p * t2 + 2.0f;
+  return t * p + (float)e * 0.693147182f;
+}
+
+// 2^x for x <= 0 (x < -60 -> 0): x = n + f, n = floor(x + 1/2), f in [-1/2, 1/2), degree-7
+// Taylor of e^(f ln2) (truncation error < 6e-9), times 2^n.
+__device__ __forceinline__ float lb_exp2f(float x) {
+  if (x < -60.0f) return 0.0f;
+  const float fl = floorf(x + 0.5f);  /* exact for |x| <= 60 */
+  const int n = (int)fl;
+  const float f = x - fl;             /* exact, in [-0.5, 0.5) */
+  float p = 1.52527336e-5f;
+  p = p * f + 1.54035297e-4f;
+  p = p * f + 1.33335581e-3f;
+  p = p * f + 9.61812911e-3f;
+  p = p * f + 5.55041086e-2f;
+  p = p * f + 0.240226507f;
+  p = p * f + 0.693147182f;
+  p = p * f + 1.0f;
+  return p * as_f32((uint32_t)(n + 127) << 23);
+}
+
+// floor(r64 * n / 2^64) for n <= 2^32: uniform integer in [0, n) (Lemire multiply-shift, 64-bit
+// source, bias <= n / 2^64).  Used for Algorithm R's j = randint(0, count + 1).
+__device__ __forceinline__ uint64_t mulhi64_by_u33(uint32_t r_hi, uint32_t r_lo, uint64_t n) {
+  const uint64_t a = (uint64_t)r_hi * n;
+  const uint64_t b = ((uint64_t)r_lo * n) >> 32;
+  return (a + b) >> 32;
+}
+
+}  // namespace lbk

@@ -1,0 +1,446 @@
+"""Gym-style facades over liblbsim.
+
+VecLoadBalanceEnv   B independent LB environments resident on one GPU; torch tensors in/out,
+                    no host synchronisation on the step path (the batched hot path).
+LoadBalanceEnv      the reference's single-environment API, call for call
+                    (simulation-mode/problem-03-rl-environment/src/env.py:41-470): numpy in/out,
+                    same kwargs, spaces, info dict, done rule, seed/render/close and ValueErrors,
+                    so problem-04's Trainer and problem-05's wrapper drop in unchanged.
+
+Both run every step through the gfx950 kernels (marllb_amd/csrc).  What differs from the
+reference by design: observations come from a real flow simulator (arrivals ->
+server assignment -> FIFO service -> reservoir features) instead of np.random draws, and there is
+no wall-clock sleep (step_interval is SIMULATED seconds).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Any, Dict, List, Optional, Tuple
+
+import numpy as np
+
+from . import _lib
+from .spaces import Box, MultiDiscrete
+
+# env.py:377-381 — observation column order (column 10 is named flow_duration_avg_decay there)
+FEATURE_NAMES = [
+    "n_flow_on", "fct_mean", "fct_p90", "fct_std", "fct_mean_decay", "fct_p90_decay",
+    "flow_duration_mean", "flow_duration_p90", "flow_duration_std",
+    "flow_duration_mean_decay", "flow_duration_avg_decay",
+]
+DEFAULT_DISCRETE_WEIGHTS = [1.0, 1.5, 2.0]  # env.py:69
+
+
+def action_to_weights(action, action_type: str, discrete_weights, min_weight: float,
+                      max_weight: float) -> np.ndarray:
+    """env.py:334-353: discrete index -> discrete_weights[int(a)]; continuous -> clip (f32)."""
+    if action_type == "discrete":
+        return np.array([discrete_weights[int(a)] for a in action], dtype=np.float32)
+    return np.clip(np.asarray(action, dtype=np.float32), min_weight, max_weight)
+
+
+def array_to_dict(obs: np.ndarray, sequence_id: int = 0) -> dict:
+    """env.py:391-423: active = any(obs[s] > 0); per-server dict of the 11 named features."""
+    stats, active = {}, []
+    for sid in range(obs.shape[0]):
+        if np.any(obs[sid] > 0):
+            active.append(sid)
+            stats[sid] = {name: float(obs[sid, i]) for i, name in enumerate(FEATURE_NAMES)}
+    return {"active_servers": active, "server_stats": stats, "sequence_id": sequence_id}
+
+
+def dict_to_array(obs_dict: dict, num_servers: int) -> np.ndarray:
+    """env.py:355-389."""
+    obs = np.zeros((num_servers, 11), dtype=np.float32)
+    stats = obs_dict.get("server_stats", {})
+    for sid in obs_dict.get("active_servers", []):
+        if sid < num_servers and sid in stats:
+            for i, name in enumerate(FEATURE_NAMES):
+                obs[sid, i] = stats[sid].get(name, 0.0)
+    return obs
+
+
+def make_spaces(num_servers: int, action_type: str, discrete_weights, min_weight: float,
+                max_weight: float, use_ground_truth: bool = False):
+    """env.py:156-184 (observation space is (S, 11 [+3]) even though arrays are (S, 11))."""
+    num_features = 11 + (3 if use_ground_truth else 0)
+    obs_space = Box(low=0, high=np.inf, shape=(num_servers, num_features), dtype=np.float32)
+    if action_type == "discrete":
+        act_space = MultiDiscrete([len(discrete_weights)] * num_servers)
+    elif action_type == "continuous":
+        act_space = Box(low=min_weight, high=max_weight, shape=(num_servers,), dtype=np.float32)
+    else:
+        raise ValueError(f"Unknown action_type: {action_type}")
+    return obs_space, act_space
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _device_index(device) -> int:
+    torch = _torch()
+    if device is None:
+        return torch.cuda.current_device()
+    d = torch.device(device)
+    if d.type != "cuda":
+        raise ValueError(f"lbsim runs on a HIP device (cuda:N), got {device!r}")
+    return torch.cuda.current_device() if d.index is None else d.index
+
+
+def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discrete",
+                discrete_weights: Optional[List[float]] = None, max_weight: float = 10.0,
+                min_weight: float = 0.1, reward_metric: str = "jain",
+                reward_field: str = "flow_duration_avg_decay", step_interval: float = 0.25,
+                max_steps: int = 10000, normalize_obs: bool = False, seed: Optional[int] = None,
+                env_id_offset: int = 0, arrival_rate: float = 400.0,
+                server_rates: Optional[List[float]] = None, load: float = 0.8,
+                queue_capacity: int = 32, warmup_steps: int = 8, decay_factor: float = 0.9,
+                assign_policy: str = "sed") -> _lib.LbsimConfig:
+    """Build and validate an lbsim_config_t from reference-style kwargs.
+
+    server_rates defaults to identical servers at utilisation `load`: mu = rate / (load * S).
+    """
+    if reward_metric not in _lib.METRICS:  # rewards.py:321-323
+        raise ValueError(f"Unsupported metric: {reward_metric}. Supported: {_lib.METRICS}")
+    if action_type not in ("discrete", "continuous"):  # env.py:183-184
+        raise ValueError(f"Unknown action_type: {action_type}")
+    if assign_policy not in _lib.POLICIES:
+        raise ValueError(f"Unknown assign_policy: {assign_policy}. Supported: {_lib.POLICIES}")
+    cfg = _lib.default_config()
+    cfg.num_envs = int(num_envs)
+    cfg.num_servers = int(num_servers)
+    cfg.env_id_offset = int(env_id_offset)
+    if seed is None:
+        seed = int.from_bytes(os.urandom(8), "little")
+    cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    cfg.action_type = _lib.ACTION_DISCRETE if action_type == "discrete" else _lib.ACTION_CONTINUOUS
+    dw = list(discrete_weights or DEFAULT_DISCRETE_WEIGHTS)
+    if len(dw) > _lib.MAX_DISCRETE:
+        raise ValueError(f"at most {_lib.MAX_DISCRETE} discrete weight levels")
+    cfg.num_discrete = len(dw)
+    for i in range(_lib.MAX_DISCRETE):
+        cfg.discrete_weights[i] = float(dw[i]) if i < len(dw) else 0.0
+    cfg.min_weight = float(min_weight)
+    cfg.max_weight = float(max_weight)
+    cfg.reward_metric = _lib.METRICS.index(reward_metric)
+    cfg.reward_field = FEATURE_NAMES.index(reward_field) if reward_field in FEATURE_NAMES else -1
+    cfg.step_interval = float(step_interval)
+    cfg.max_steps = int(max_steps)
+    cfg.normalize_obs = 1 if normalize_obs else 0
+    cfg.assign_policy = _lib.POLICIES.index(assign_policy)
+    cfg.arrival_rate = float(arrival_rate)
+    if server_rates is None:
+        server_rates = [float(arrival_rate) / (float(load) * num_servers)] * num_servers
+    if len(server_rates) != num_servers:
+        raise ValueError("server_rates must have num_servers entries")
+    for s in range(_lib.MAX_SERVERS):
+        cfg.server_rate[s] = float(server_rates[s]) if s < num_servers else 0.0
+    cfg.decay_factor = float(decay_factor)
+    cfg.queue_capacity = int(queue_capacity)
+    cfg.warmup_steps = int(warmup_steps)
+    _lib.validate(cfg)
+    return cfg
+
+
+class Handle:
+    """Owns one lbsim_t (device state of B envs on one GPU)."""
+
+    def __init__(self, cfg: _lib.LbsimConfig, device_index: int):
+        self.lib = _lib.load()
+        self.cfg = cfg
+        self.device_index = device_index
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.lbsim_create(ctypes.byref(cfg), device_index, ctypes.byref(h)))
+        self.h = h
+
+    def check(self, rc: int) -> None:
+        _lib.check(rc, self.h)
+
+    def close(self) -> None:
+        if getattr(self, "h", None) is not None and self.h.value is not None:
+            self.lib.lbsim_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def state_bytes(self) -> bytes:
+        n = ctypes.c_size_t()
+        self.check(self.lib.lbsim_state_size(self.h, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(n.value)
+        self.check(self.lib.lbsim_get_state(self.h, buf, n.value))
+        return buf.raw
+
+    def load_state(self, data: bytes) -> None:
+        self.check(self.lib.lbsim_set_state(self.h, data, len(data)))
+
+
+class VecLoadBalanceEnv:
+    """num_envs independent LoadBalanceEnv instances stepped together on one GPU.
+
+    reset(mask=None) -> obs (B, S, 11) f32 cuda tensor
+    step(actions)    -> obs, reward (B,) f32, done (B,) bool, info dict of tensors
+    Actions: (B, S) int32/int64 indices (discrete) or float32 weights (continuous), any device.
+    With autoreset=True, envs whose episode ended are reset inside step(); their returned obs is
+    the first obs of the new episode and info['terminal_obs'] (if keep_terminal_obs) holds the
+    last one, as gym/SB3 vector envs do.
+    """
+
+    def __init__(self, num_envs: int, num_servers: int = 4, *, device=None,
+                 autoreset: bool = True, keep_terminal_obs: bool = False, **kwargs):
+        torch = _torch()
+        self.device_index = _device_index(device)
+        self.device = torch.device("cuda", self.device_index)
+        self.cfg = make_config(num_envs, num_servers, **kwargs)
+        self.num_envs = int(num_envs)
+        self.num_servers = int(num_servers)
+        self.action_type = "discrete" if self.cfg.action_type == _lib.ACTION_DISCRETE else "continuous"
+        self.autoreset = autoreset
+        self.keep_terminal_obs = keep_terminal_obs
+        self.handle = Handle(self.cfg, self.device_index)
+        self._ep_len = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
+        self._ep_ret = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
+        self._reset_done = False
+
+    # -- helpers
+    def _stream(self) -> int:
+        return _torch().cuda.current_stream(self.device).cuda_stream
+
+    def _obs_buffer(self):
+        torch = _torch()
+        return torch.empty((self.num_envs, self.num_servers, 11), dtype=torch.float32,
+                           device=self.device)
+
+    def _action(self, actions):
+        torch = _torch()
+        a = torch.as_tensor(actions)
+        if self.action_type == "discrete":
+            if a.dtype not in (torch.int32, torch.int64):
+                a = a.to(torch.int64)
+            dt = _lib.DTYPE_I64 if a.dtype == torch.int64 else _lib.DTYPE_I32
+        else:
+            if a.dtype != torch.float32:
+                a = a.to(torch.float32)
+            dt = _lib.DTYPE_F32
+        a = a.to(self.device).reshape(self.num_envs, self.num_servers).contiguous()
+        return a, dt
+
+    # -- API
+    def reset(self, mask=None):
+        """Reset all envs (mask None) or those with mask[b] true; returns obs for all envs.
+
+        With a mask, rows of envs that are not reset hold the obs of their last step() (or of
+        the previous reset), so the returned tensor is always a complete batch.
+        """
+        torch = _torch()
+        if mask is None:
+            obs = self._obs_buffer()
+            self.handle.check(self.handle.lib.lbsim_reset(self.handle.h, None, obs.data_ptr(),
+                                                          self._stream()))
+            self._reset_done = True
+            self._last_obs = obs
+            return obs
+        if not self._reset_done:
+            raise RuntimeError("call reset() without a mask first")
+        m = torch.as_tensor(mask).to(self.device).to(torch.uint8).contiguous()
+        obs = self._last_obs.clone()
+        self.handle.check(self.handle.lib.lbsim_reset(self.handle.h, m.data_ptr(),
+                                                      obs.data_ptr(), self._stream()))
+        self._last_obs = obs
+        return obs
+
+    def step(self, actions, *, assign_counts: bool = False, raw_obs: bool = False
+             ) -> Tuple[Any, Any, Any, Dict[str, Any]]:
+        torch = _torch()
+        if not self._reset_done:
+            raise RuntimeError("call reset() before step()")
+        a, dt = self._action(actions)
+        B, S = self.num_envs, self.num_servers
+        obs = self._obs_buffer()
+        reward = torch.empty(B, dtype=torch.float32, device=self.device)
+        done = torch.empty(B, dtype=torch.uint8, device=self.device)
+        out = _lib.StepOutputs()
+        out.obs, out.reward, out.done = obs.data_ptr(), reward.data_ptr(), done.data_ptr()
+        assign = raw = None
+        if assign_counts:
+            assign = torch.empty((B, S), dtype=torch.int32, device=self.device)
+            out.assign_count = assign.data_ptr()
+        if raw_obs:
+            raw = self._obs_buffer()
+            out.raw_obs = raw.data_ptr()
+        out.episode_length = self._ep_len.data_ptr()
+        out.episode_return = self._ep_ret.data_ptr()
+        self.handle.check(self.handle.lib.lbsim_step_ex(self.handle.h, a.data_ptr(), dt,
+                                                        ctypes.byref(out), self._stream()))
+        info: Dict[str, Any] = {"episode_length": self._ep_len.clone(),
+                                "episode_return": self._ep_ret.clone()}
+        if assign is not None:
+            info["assign_counts"] = assign
+        if raw is not None:
+            info["raw_obs"] = raw
+        if self.autoreset:
+            if self.keep_terminal_obs:
+                info["terminal_obs"] = obs.clone()
+            # envs with done == 0 are untouched by the masked reset (no host sync needed)
+            self.handle.check(self.handle.lib.lbsim_reset(self.handle.h, done.data_ptr(),
+                                                          obs.data_ptr(), self._stream()))
+        self._last_obs = obs
+        return obs, reward, done.bool(), info
+
+    def seed(self, seed: Optional[int] = None):
+        if seed is None:
+            seed = int.from_bytes(os.urandom(8), "little")
+        self.handle.check(self.handle.lib.lbsim_seed(self.handle.h, int(seed) & (2**64 - 1)))
+        return [seed]
+
+    def get_state(self) -> bytes:
+        return self.handle.state_bytes()
+
+    def set_state(self, data: bytes) -> None:
+        self.handle.load_state(data)
+        self._reset_done = True
+
+    def close(self) -> None:
+        self.handle.close()
+
+
+class LoadBalanceEnv:
+    """Drop-in for the reference LoadBalanceEnv (env.py:41-470), one env, numpy I/O."""
+
+    DEFAULT_DISCRETE_WEIGHTS = DEFAULT_DISCRETE_WEIGHTS
+
+    def __init__(self, num_servers: int = 4, action_type: str = "discrete",
+                 discrete_weights: Optional[List[float]] = None, max_weight: float = 10.0,
+                 min_weight: float = 0.1, reward_metric: str = "jain",
+                 reward_field: str = "flow_duration_avg_decay", step_interval: float = 0.25,
+                 max_steps: int = 10000, use_shm: bool = False, shm_name: Optional[str] = None,
+                 use_ground_truth: bool = False, normalize_obs: bool = False,
+                 seed: Optional[int] = None, *, device=None, **sim_kwargs):
+        self.num_servers = num_servers
+        self.action_type = action_type
+        self.discrete_weights = discrete_weights or self.DEFAULT_DISCRETE_WEIGHTS
+        self.max_weight = max_weight
+        self.min_weight = min_weight
+        self.step_interval = step_interval
+        self.max_steps = max_steps
+        self.use_shm = use_shm
+        self.shm_name = shm_name
+        self.use_ground_truth = use_ground_truth
+        self.normalize_obs = normalize_obs
+        self.reward_metric = reward_metric
+        self.reward_field = reward_field
+        if reward_metric not in _lib.METRICS:  # RewardFunction.__init__ (rewards.py:321-323)
+            raise ValueError(f"Unsupported metric: {reward_metric}. Supported: {_lib.METRICS}")
+        self._setup_spaces()
+        if self.use_shm:  # env.py:134-143: no SHM bridge in this build -> simulation fallback
+            if self.shm_name is None:
+                raise ValueError("shm_name required when use_shm=True")
+            print(f"Warning: SHM bridge not built; falling back to the GPU simulator "
+                  f"(requested {self.shm_name})")
+            self.use_shm = False
+        self._vec = VecLoadBalanceEnv(
+            1, num_servers, device=device, autoreset=False, action_type=action_type,
+            discrete_weights=self.discrete_weights, max_weight=max_weight, min_weight=min_weight,
+            reward_metric=reward_metric, reward_field=reward_field, step_interval=step_interval,
+            max_steps=max_steps, normalize_obs=normalize_obs, seed=seed, **sim_kwargs)
+        self.shm = None
+        self.current_step = 0
+        self.last_observation = None
+        self.episode_rewards: List[float] = []
+        self.episode_return = 0.0
+
+    # ---- spaces (env.py:156-184)
+    def _setup_spaces(self):
+        self.observation_space, self.action_space = make_spaces(
+            self.num_servers, self.action_type, self.discrete_weights, self.min_weight,
+            self.max_weight, self.use_ground_truth)
+
+    # ---- gym API
+    def reset(self) -> np.ndarray:
+        self.current_step = 0
+        self.episode_rewards = []
+        self.episode_return = 0.0
+        obs = self._vec.reset()[0].cpu().numpy()
+        return obs
+
+    def step(self, action) -> Tuple[np.ndarray, float, bool, Dict[str, Any]]:
+        torch = _torch()
+        self.current_step += 1
+        weights = self._action_to_weights(action)
+        a = np.asarray(action)
+        if self.action_type == "discrete":
+            idx = np.array([int(x) for x in a.reshape(-1)], dtype=np.int64)
+            n = len(self.discrete_weights)
+            if np.any(idx >= n) or np.any(idx < -n):  # python list indexing (env.py:346)
+                raise IndexError("list index out of range")
+            act = torch.from_numpy(idx.reshape(1, -1))
+        else:
+            act = torch.from_numpy(np.asarray(a, dtype=np.float32).reshape(1, -1))
+        obs_t, rew_t, _, info_t = self._vec.step(act, raw_obs=True)
+        next_obs = obs_t[0].cpu().numpy()
+        raw = info_t["raw_obs"][0].cpu().numpy()
+        reward = float(rew_t[0].item())
+        obs_dict = self._array_to_dict(raw)
+        self.last_observation = obs_dict
+        self.episode_rewards.append(reward)
+        self.episode_return += reward
+        done = self.current_step >= self.max_steps
+        info = {
+            "step": self.current_step,
+            "weights": weights.tolist(),
+            "active_servers": obs_dict.get("active_servers", list(range(self.num_servers))),
+            "episode_return": self.episode_return,
+        }
+        if done:
+            info["episode"] = {"r": self.episode_return, "l": self.current_step}
+        return next_obs, reward, done, info
+
+    def render(self, mode: str = "human"):
+        if mode == "human":
+            print(f"\n{'=' * 60}")
+            print(f"Step: {self.current_step}/{self.max_steps}")
+            print(f"Episode Return: {self.episode_return:.4f}")
+            if self.last_observation:
+                obs_dict = self.last_observation
+                active = obs_dict.get("active_servers", [])
+                stats = obs_dict.get("server_stats", {})
+                print(f"Active Servers: {active}")
+                print(f"\n{'Server':<10} {'n_flows':<10} {'fct_mean':<12} {'fct_p90':<12} "
+                      f"{'dur_decay':<12}")
+                print("-" * 60)
+                for sid in active:
+                    st = stats.get(sid, {})
+                    print(f"{sid:<10} {st.get('n_flow_on', 0):<10.0f} "
+                          f"{st.get('fct_mean', 0):<12.4f} {st.get('fct_p90', 0):<12.4f} "
+                          f"{st.get('flow_duration_avg_decay', 0):<12.4f}")
+            print("=" * 60)
+
+    def close(self):
+        self._vec.close()
+
+    def seed(self, seed: Optional[int] = None):
+        self._vec.seed(seed)
+        return [seed]
+
+    # ---- reference helpers (host plumbing, env.py:334-423)
+    def _action_to_weights(self, action) -> np.ndarray:
+        return action_to_weights(action, self.action_type, self.discrete_weights,
+                                 self.min_weight, self.max_weight)
+
+    def _dict_to_array(self, obs_dict: dict) -> np.ndarray:
+        return dict_to_array(obs_dict, self.num_servers)
+
+    def _array_to_dict(self, obs: np.ndarray) -> dict:
+        return array_to_dict(obs, self.current_step)
+
+
+class LoadBalanceEnvGym(LoadBalanceEnv):
+    """env.py:474-481 alias (gym.Env mixin not needed: no gym dependency)."""
+
+    metadata = {"render.modes": ["human"]}

@@ -1,0 +1,680 @@
+/*
+ * lbsim_oracle.c — CPU ORACLE for the lbsim GPU path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library, and
+ * only as the checker / the timed CPU baseline.  The product path (marllb_amd/, liblbsim.so)
+ * never links, loads or calls it.
+ *
+ * What it restates (one env at a time, scalar C99, no wave-level tricks):
+ *   - ReservoirSampler.add (Algorithm R)              reservoir.py:50-85, reservoir.h:118-143
+ *   - ReservoirSampler.get_features (numpy 2 f32)     reservoir.py:105-196
+ *   - MultiMetricReservoir shared replacement stream  reservoir.py:236-265
+ *   - PerServerFeatures.get_state_vector (S, 11)      features.py:256-286
+ *   - RewardFunction.compute + 9 metrics (float64)    rewards.py:21-381
+ *   - active-server rule any(obs[s] > 0)              env.py:410-413
+ *   - _action_to_weights                              env.py:334-353
+ *   - _normalize_observation (float64)                env.py:450-470
+ *   - step/reset bookkeeping (done, return)           env.py:186-286
+ *   - SED/SED2/LSQ/LSQ2 server choice                 src/vpp/lb/node.c:388-441
+ *   - completion samples fct / duration               src/vpp/lb/lbhash.h:116-135
+ * plus the flow dynamics the reference does not have (Poisson arrivals, per-server
+ * FIFO service, Philox4x32-10 counter RNG).  Those are "parity unpinned" against the reference:
+ * this file is their executable specification.
+ *
+ * Pinning: tests/test_oracle_golden.py checks the features, rewards and plumbing against golden
+ * vectors produced by the reference Python itself (tests/golden/gen_golden.py), and Philox against
+ * the Random123 known-answer vectors.
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off -fopenmp).  -ffp-contract=off is required:
+ * the GPU kernels are compiled the same way and integer state must match bit for bit.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "../include/lbsim.h"
+
+#define K LBSIM_RESERVOIR_K
+#define NF LBSIM_NUM_FEATURES
+#define LAST_NONE (-(1 << 30))
+
+/* ------------------------------------------------------------------ Philox4x32-10 */
+void oracle_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+  uint32_t k0 = key[0], k1 = key[1];
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n1 = (uint32_t)p1;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    const uint32_t n3 = (uint32_t)p0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+static float bits_f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+static uint32_t f_bits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+
+static float u01(uint32_t r) { return (float)((r >> 8) + 1u) * 5.9604644775390625e-8f; }
+
+/* ln x for x in [2^-24, 1] — DESIGN.md §3.2 (same operation sequence as the GPU). */
+float oracle_logf(float x) {
+  const uint32_t b = f_bits(x);
+  int e = (int)(b >> 23) - 127;
+  float m = bits_f((b & 0x007fffffu) | 0x3f800000u);
+  if (m > 1.41421354f) { m = m * 0.5f; e = e + 1; }
+  const float t = (m - 1.0f) / (m + 1.0f);
+  const float t2 = t * t;
+  float p = 0.222222224f;
+  p = p * t2 + 0.285714298f;
+  p = p * t2 + 0.400000006f;
+  p = p * t2 + 0.666666687f;
+  p = p * t2 + 2.0f;
+  return t * p + (float)e * 0.693147182f;
+}
+
+/* 2^x for x <= 0 — DESIGN.md §3.4. */
+float oracle_exp2f(float x) {
+  if (x < -60.0f) return 0.0f;
+  const float fl = floorf(x + 0.5f);  /* exact for |x| <= 60 */
+  const int n = (int)fl;
+  const float f = x - fl;             /* exact, in [-0.5, 0.5) */
+  float p = 1.52527336e-5f;
+  p = p * f + 1.54035297e-4f;
+  p = p * f + 1.33335581e-3f;
+  p = p * f + 9.61812911e-3f;
+  p = p * f + 5.55041086e-2f;
+  p = p * f + 0.240226507f;
+  p = p * f + 0.693147182f;
+  p = p * f + 1.0f;
+  return p * bits_f((uint32_t)(n + 127) << 23);
+}
+
+/* ------------------------------------------------------------------ numpy pairwise sums */
+/* numpy/_core/src/umath/loops_utils.h.src pairwise_sum, n <= 128 (PW_BLOCKSIZE). */
+static float pw32(const float* a, int n) {
+  if (n < 8) {
+    float r = 0.0f;
+    for (int i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  float r[8];
+  for (int j = 0; j < 8; ++j) r[j] = a[j];
+  const int m8 = n - (n % 8);
+  for (int i = 8; i < m8; i += 8)
+    for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (int i = m8; i < n; ++i) res += a[i];
+  return res;
+}
+
+static double pw64(const double* a, int n) {
+  if (n < 8) {
+    double r = 0.0;
+    for (int i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  double r[8];
+  for (int j = 0; j < 8; ++j) r[j] = a[j];
+  const int m8 = n - (n % 8);
+  for (int i = 8; i < m8; i += 8)
+    for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (int i = m8; i < n; ++i) res += a[i];
+  return res;
+}
+
+/* ------------------------------------------------------------------ reservoir features */
+typedef struct { float v; int slot; } vs_t;
+static int cmp_vs(const void* a, const void* b) {
+  const vs_t* x = (const vs_t*)a;
+  const vs_t* y = (const vs_t*)b;
+  if (x->v < y->v) return -1;
+  if (x->v > y->v) return 1;
+  return (x->slot > y->slot) - (x->slot < y->slot);
+}
+
+/* get_features(decay, now) of one reservoir; w[]/wq[] are the slot weights (see below). */
+static void features_one(const float* vals, const float* w, const uint64_t* wq, int n,
+                         float out[5]) {
+  if (n == 0) { for (int f = 0; f < 5; ++f) out[f] = 0.0f; return; }
+  /* mean, std: numpy float32 pairwise (np.mean / np.std ddof 0) */
+  const float fn = (float)n;
+  const float mean = pw32(vals, n) / fn;
+  float d2[K];
+  for (int i = 0; i < n; ++i) { const float d = vals[i] - mean; d2[i] = d * d; }
+  const float sd = sqrtf(pw32(d2, n) / fn);
+  /* mean_decay = np.average(values, weights=w) in float64 */
+  double vw[K], ww[K];
+  for (int i = 0; i < n; ++i) { ww[i] = (double)w[i]; vw[i] = (double)vals[i] * (double)w[i]; }
+  const float md = (float)(pw64(vw, n) / pw64(ww, n));
+  /* sorted order by (value, slot) */
+  vs_t srt[K];
+  for (int i = 0; i < n; ++i) { srt[i].v = vals[i]; srt[i].slot = i; }
+  qsort(srt, (size_t)n, sizeof(vs_t), cmp_vs);
+  /* p90: numpy 2 'linear' with float32 q = 90 / float32(100) (virtual index (n-1)*q) */
+  const float q = 0.9f;
+  const float h = (float)(n - 1) * q;
+  const float fl = floorf(h);
+  const int lo = (int)fl;
+  const float g = h - fl;
+  const float a = srt[lo].v;
+  const float b = srt[lo + 1 < n ? lo + 1 : lo].v;
+  const float diff = b - a;
+  const float p90 = (g >= 0.5f) ? (b - diff * (1.0f - g)) : (a + diff * g);
+  /* p90_decay: first sorted index with cumsum >= 0.9 * total (searchsorted 'left'), with the
+   * weights in exact 2^-48 fixed point so the comparison does not depend on summation order. */
+  uint64_t total = 0;
+  for (int i = 0; i < n; ++i) total += wq[i];
+  uint64_t cum = 0;
+  int idx = n - 1;
+  for (int i = 0; i < n; ++i) {
+    cum += wq[srt[i].slot];
+    if (cum * 10u >= total * 9u) { idx = i; break; }
+  }
+  out[0] = mean; out[1] = p90; out[2] = sd; out[3] = md; out[4] = srt[idx].v;
+}
+
+/* Decay weights relative to the newest sample: w = 2^(log2(decay)/1000 * age_ms). */
+static void slot_weights(const uint32_t* ts, int n, float decay_c, float* w, uint64_t* wq) {
+  uint32_t newest = 0;
+  for (int i = 0; i < n; ++i) newest = ts[i] > newest ? ts[i] : newest;
+  for (int i = 0; i < n; ++i) {
+    w[i] = oracle_exp2f((float)(newest - ts[i]) * decay_c);
+    wq[i] = (uint64_t)(w[i] * 281474976710656.0f);
+  }
+}
+
+float oracle_decay_c(float decay_factor) {
+  return (float)(log2((double)decay_factor) / 1000.0);
+}
+
+void oracle_reservoir_features(const float* values, const uint32_t* ts_ms, uint32_t count,
+                               float decay_factor, float out[5]) {
+  const int n = count < (uint32_t)K ? (int)count : K;
+  float w[K];
+  uint64_t wq[K];
+  slot_weights(ts_ms, n, oracle_decay_c(decay_factor), w, wq);
+  features_one(values, w, wq, n, out);
+}
+
+/* ------------------------------------------------------------------ reward (float64) */
+static double np_var(const double* x, int n) {
+  const double mean = pw64(x, n) / (double)n;
+  double d[LBSIM_MAX_SERVERS];
+  for (int i = 0; i < n; ++i) { const double t = x[i] - mean; d[i] = t * t; }
+  return pw64(d, n) / (double)n;
+}
+
+double oracle_reward(const float* obs, int S, int metric, int field) {
+  if (field < 0 || field >= NF) return 0.0;
+  double x[LBSIM_MAX_SERVERS];
+  int n = 0;
+  for (int s = 0; s < S; ++s) {
+    int active = 0;
+    for (int f = 0; f < NF; ++f) active |= obs[s * NF + f] > 0.0f;
+    if (active) x[n++] = (double)obs[s * NF + field];
+  }
+  if (n == 0) return 0.0;
+  const double eps = 1e-10;
+  switch (metric) {
+    case LBSIM_METRIC_JAIN: {
+      const double sv = pw64(x, n);
+      if (sv < eps) return 1.0;
+      double x2[LBSIM_MAX_SERVERS];
+      for (int i = 0; i < n; ++i) x2[i] = x[i] * x[i];
+      const double sq = pw64(x2, n);
+      if (sq < eps) return 1.0;
+      const double j = (sv * sv) / ((double)n * sq);
+      const double lo = 1.0 / (double)n;
+      return j < lo ? lo : (j > 1.0 ? 1.0 : j);
+    }
+    case LBSIM_METRIC_VARIANCE: return -np_var(x, n);
+    case LBSIM_METRIC_STD: return -sqrt(np_var(x, n));
+    case LBSIM_METRIC_CV: {
+      const double mean = pw64(x, n) / (double)n;
+      if (mean < eps) return 0.0;
+      return -(sqrt(np_var(x, n)) / (mean + eps));
+    }
+    case LBSIM_METRIC_MAX: {
+      double m = x[0];
+      for (int i = 1; i < n; ++i) m = x[i] > m ? x[i] : m;
+      return -m;
+    }
+    case LBSIM_METRIC_MIN: {
+      double m = x[0];
+      for (int i = 1; i < n; ++i) m = x[i] < m ? x[i] : m;
+      return m;
+    }
+    case LBSIM_METRIC_PRODUCT: {
+      double l[LBSIM_MAX_SERVERS];
+      for (int i = 0; i < n; ++i) l[i] = log(x[i] + eps);
+      return pw64(l, n);
+    }
+    case LBSIM_METRIC_RANGE: {
+      double mx = x[0], mn = x[0];
+      for (int i = 1; i < n; ++i) { if (x[i] > mx) mx = x[i]; if (x[i] < mn) mn = x[i]; }
+      return -(mx - mn);
+    }
+    case LBSIM_METRIC_GINI: {
+      const double mean = pw64(x, n) / (double)n;
+      if (mean == 0.0) return 0.0;
+      double ds = 0.0;
+      for (int i = 0; i < n; ++i)
+        for (int k = 0; k < n; ++k) ds += fabs(x[i] - x[k]);
+      return -(ds / ((double)(2 * n * n) * mean));
+    }
+    default: return 0.0;
+  }
+}
+
+/* ------------------------------------------------------------------ simulator state */
+typedef struct oracle {
+  lbsim_config_t cfg;
+  int B, S, Q;
+  int32_t dt_us;
+  float mean_gap_us, svc_scale[LBSIM_MAX_SERVERS], decay_c;
+  uint32_t key[2];
+  int threads;
+  int initialised;
+  char* buf;
+  size_t bytes;
+  /* sections, snapshot order == liblbsim */
+  int32_t* next_arr; float* next_work; uint32_t* next_u2; uint32_t* next_u3; uint32_t* arr_idx;
+  uint32_t* episode; uint32_t* clock; int32_t* ep_step; uint32_t* dropped; int32_t* norm_count;
+  double* ep_return;
+  uint32_t* hc; int32_t* last_tc; uint32_t* res_count;
+  int32_t* ring; /* [B*S*Q][2] = {t_complete, t_arrival} */
+  float* res_fct; float* res_dur; uint32_t* res_ts;
+  double* norm_mean; double* norm_std;
+} oracle_t;
+
+static void derive(oracle_t* o) {
+  const lbsim_config_t* c = &o->cfg;
+  o->B = c->num_envs; o->S = c->num_servers; o->Q = c->queue_capacity;
+  o->dt_us = (int32_t)llround((double)c->step_interval * 1e6);
+  o->mean_gap_us = (float)(1e6 / (double)c->arrival_rate);
+  for (int s = 0; s < LBSIM_MAX_SERVERS; ++s)
+    o->svc_scale[s] = s < c->num_servers ? (float)(1e6 / (double)c->server_rate[s]) : 0.0f;
+  o->decay_c = oracle_decay_c(c->decay_factor);
+  o->key[0] = (uint32_t)(c->seed & 0xFFFFFFFFull);
+  o->key[1] = (uint32_t)(c->seed >> 32);
+}
+
+oracle_t* oracle_create(const lbsim_config_t* cfg) {
+  oracle_t* o = (oracle_t*)calloc(1, sizeof(oracle_t));
+  if (!o) return NULL;
+  o->cfg = *cfg;
+  derive(o);
+  o->threads = 1;
+  const size_t B = o->B, BS = (size_t)o->B * o->S, BSQ = BS * o->Q, BSK = BS * K;
+  const size_t sz[] = {B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4,
+                       B * 8, BS * 4, BS * 4, BS * 4, BSQ * 8, BSK * 4, BSK * 4, BSK * 4,
+                       cfg->normalize_obs ? BS * NF * 8 : 0, cfg->normalize_obs ? BS * NF * 8 : 0};
+  size_t total = 0;
+  for (size_t i = 0; i < sizeof(sz) / sizeof(sz[0]); ++i) total += sz[i];
+  o->bytes = total;
+  o->buf = (char*)calloc(1, total ? total : 1);
+  if (!o->buf) { free(o); return NULL; }
+  char* p = o->buf;
+  void** ptrs[] = {(void**)&o->next_arr, (void**)&o->next_work, (void**)&o->next_u2,
+                   (void**)&o->next_u3, (void**)&o->arr_idx, (void**)&o->episode,
+                   (void**)&o->clock, (void**)&o->ep_step, (void**)&o->dropped,
+                   (void**)&o->norm_count, (void**)&o->ep_return, (void**)&o->hc,
+                   (void**)&o->last_tc, (void**)&o->res_count, (void**)&o->ring,
+                   (void**)&o->res_fct, (void**)&o->res_dur, (void**)&o->res_ts,
+                   (void**)&o->norm_mean, (void**)&o->norm_std};
+  for (size_t i = 0; i < sizeof(sz) / sizeof(sz[0]); ++i) {
+    *ptrs[i] = sz[i] ? (void*)p : NULL;
+    p += sz[i];
+  }
+  if (cfg->normalize_obs)
+    for (size_t i = 0; i < BS * NF; ++i) o->norm_std[i] = 1.0; /* env.py:153 */
+  return o;
+}
+
+void oracle_destroy(oracle_t* o) {
+  if (!o) return;
+  free(o->buf);
+  free(o);
+}
+
+void oracle_set_threads(oracle_t* o, int n) { o->threads = n < 1 ? 1 : n; }
+size_t oracle_state_size(const oracle_t* o) { return o->bytes; }
+void oracle_get_state(const oracle_t* o, void* dst) { memcpy(dst, o->buf, o->bytes); }
+void oracle_set_state(oracle_t* o, const void* src) { memcpy(o->buf, src, o->bytes); o->initialised = 1; }
+
+void oracle_seed(oracle_t* o, uint64_t seed) {
+  o->cfg.seed = seed;
+  o->key[0] = (uint32_t)(seed & 0xFFFFFFFFull);
+  o->key[1] = (uint32_t)(seed >> 32);
+  memset(o->episode, 0, (size_t)o->B * 4);
+}
+
+/* ------------------------------------------------------------------ one env, scalar */
+typedef struct {
+  oracle_t* o;
+  size_t b;
+  uint32_t gid;
+  int assigned[LBSIM_MAX_SERVERS];
+} env_ctx;
+
+static float score_of(int policy, int32_t cnt, double den) {
+  if (policy == LBSIM_POLICY_LSQ || policy == LBSIM_POLICY_LSQ2) return (float)cnt;
+  return (float)((double)(cnt + 1) / den);
+}
+
+static int ring_head(const oracle_t* o, size_t sb) { return (int)(o->hc[sb] & 0xFFFFu); }
+static int ring_count(const oracle_t* o, size_t sb) { return (int)(o->hc[sb] >> 16); }
+static void ring_set(oracle_t* o, size_t sb, int head, int cnt) {
+  o->hc[sb] = (uint32_t)head | ((uint32_t)cnt << 16);
+}
+
+/* Algorithm R insert of one completion into both reservoirs of server s (shared decision). */
+static void reservoir_add(env_ctx* e, int s, float fct, float dur, uint32_t ts_ms) {
+  oracle_t* o = e->o;
+  const size_t sb = e->b * (size_t)o->S + (size_t)s;
+  const uint32_t c = o->res_count[sb];
+  long slot;
+  if (c < (uint32_t)K) {
+    slot = (long)c;
+  } else {
+    const uint32_t ctr[4] = {c >> 1, e->gid, o->episode[e->b], (2u << 24) | (uint32_t)s};
+    uint32_t d[4];
+    oracle_philox(ctr, o->key, d);
+    const uint32_t hi = (c & 1u) ? d[3] : d[1];
+    const uint32_t lo = (c & 1u) ? d[2] : d[0];
+    /* j = floor(r64 * (c + 1) / 2^64): randint(0, count + 1) (reservoir.py:76) */
+    const unsigned __int128 prod = (unsigned __int128)(((uint64_t)hi << 32) | lo) * ((uint64_t)c + 1u);
+    const uint64_t j = (uint64_t)(prod >> 64);
+    slot = j < (uint64_t)K ? (long)j : -1;
+  }
+  if (slot >= 0) {
+    const size_t r = sb * K + (size_t)slot;
+    o->res_fct[r] = fct;
+    o->res_dur[r] = dur;
+    o->res_ts[r] = ts_ms;
+  }
+  if (c != 0xFFFFFFFFu) o->res_count[sb] = c + 1u;
+}
+
+static void pop_until(env_ctx* e, int s, int32_t t, uint64_t base_us, double den) {
+  oracle_t* o = e->o;
+  const size_t sb = e->b * (size_t)o->S + (size_t)s;
+  int head = ring_head(o, sb), cnt = ring_count(o, sb);
+  while (cnt > 0) {
+    const int32_t* ent = &o->ring[(sb * o->Q + (size_t)head) * 2];
+    const int32_t tc = ent[0], ta = ent[1];
+    if (tc > t) break;
+    const int32_t start = ta > o->last_tc[sb] ? ta : o->last_tc[sb];
+    const float fct = (float)(tc - ta) * 1.0e-6f;
+    const float dur = (float)(tc - start) * 1.0e-6f;
+    o->last_tc[sb] = tc;
+    const uint32_t ts_ms = (uint32_t)((base_us + (uint64_t)(int64_t)tc) / 1000u);
+    reservoir_add(e, s, fct, dur, ts_ms);
+    head = head + 1 == o->Q ? 0 : head + 1;
+    cnt -= 1;
+  }
+  ring_set(o, sb, head, cnt);
+  (void)den;
+}
+
+static void draw_arrival(env_ctx* e, int32_t t_prev) {
+  oracle_t* o = e->o;
+  const size_t b = e->b;
+  const uint32_t ctr[4] = {o->arr_idx[b], e->gid, o->episode[b], 1u << 24};
+  uint32_t d[4];
+  oracle_philox(ctr, o->key, d);
+  const int32_t gap = (int32_t)(-oracle_logf(u01(d[0])) * o->mean_gap_us);
+  o->next_arr[b] = t_prev + gap;
+  o->next_work[b] = -oracle_logf(u01(d[1]));
+  o->next_u2[b] = d[2];
+  o->next_u3[b] = d[3];
+}
+
+static void sim_step(env_ctx* e, const float* w) {
+  oracle_t* o = e->o;
+  const size_t b = e->b;
+  const int S = o->S, Q = o->Q;
+  const int policy = o->cfg.assign_policy;
+  const uint64_t base_us = (uint64_t)o->clock[b] * (uint64_t)o->dt_us;
+  double den[LBSIM_MAX_SERVERS];
+  for (int s = 0; s < S; ++s) den[s] = (double)w[s] + 1e-9;
+
+  while (o->next_arr[b] < o->dt_us) {
+    const int32_t ta = o->next_arr[b];
+    for (int s = 0; s < S; ++s) pop_until(e, s, ta, base_us, den[s]);
+    int cnt[LBSIM_MAX_SERVERS];
+    float sc[LBSIM_MAX_SERVERS];
+    for (int s = 0; s < S; ++s) {
+      cnt[s] = ring_count(o, b * (size_t)S + (size_t)s);
+      sc[s] = score_of(policy, cnt[s], den[s]);
+    }
+    int chosen = -1;
+    if (policy == LBSIM_POLICY_SED2 || policy == LBSIM_POLICY_LSQ2) {
+      /* node.c:409-417 / 433-441: two candidates, keep the second only if strictly better */
+      const int h1 = (int)(((uint64_t)o->next_u2[b] * (uint64_t)S) >> 32);
+      const int h2 = (int)(((uint64_t)o->next_u3[b] * (uint64_t)S) >> 32);
+      const int ok1 = cnt[h1] < Q, ok2 = cnt[h2] < Q;
+      if (ok1 && ok2) chosen = sc[h2] < sc[h1] ? h2 : h1;
+      else if (ok1) chosen = h1;
+      else if (ok2) chosen = h2;
+    } else {
+      /* node.c:393-404: start at the hashed (Maglev) server, replace on strictly lower score */
+      const int h = (int)(((uint64_t)o->next_u2[b] * (uint64_t)S) >> 32);
+      float best = 0.0f;
+      if (cnt[h] < Q) { chosen = h; best = sc[h]; }
+      for (int s = 0; s < S; ++s)
+        if (cnt[s] < Q && (chosen < 0 || sc[s] < best)) { chosen = s; best = sc[s]; }
+    }
+    if (chosen < 0) {
+      o->dropped[b] += 1u;
+    } else {
+      const int s = chosen;
+      const size_t sb = b * (size_t)S + (size_t)s;
+      const int head = ring_head(o, sb), c = ring_count(o, sb);
+      int32_t start = ta;
+      if (c > 0) {
+        int tp = head + c - 1;
+        if (tp >= Q) tp -= Q;
+        const int32_t tail_tc = o->ring[(sb * Q + (size_t)tp) * 2];
+        start = tail_tc > ta ? tail_tc : ta;
+      }
+      int32_t svc = (int32_t)(o->next_work[b] * o->svc_scale[s]);
+      if (svc < 1) svc = 1;
+      int pos = head + c;
+      if (pos >= Q) pos -= Q;
+      o->ring[(sb * Q + (size_t)pos) * 2] = start + svc;
+      o->ring[(sb * Q + (size_t)pos) * 2 + 1] = ta;
+      ring_set(o, sb, head, c + 1);
+      e->assigned[s] += 1;
+    }
+    o->arr_idx[b] += 1u;
+    draw_arrival(e, ta);
+  }
+  for (int s = 0; s < S; ++s) pop_until(e, s, o->dt_us, base_us, den[s]);
+  /* rebase to the next step */
+  const int32_t dt = o->dt_us;
+  o->next_arr[b] -= dt;
+  for (int s = 0; s < S; ++s) {
+    const size_t sb = b * (size_t)S + (size_t)s;
+    int pos = ring_head(o, sb);
+    const int c = ring_count(o, sb);
+    for (int i = 0; i < c; ++i) {
+      o->ring[(sb * Q + (size_t)pos) * 2] -= dt;
+      o->ring[(sb * Q + (size_t)pos) * 2 + 1] -= dt;
+      pos = pos + 1 == Q ? 0 : pos + 1;
+    }
+    o->last_tc[sb] = o->last_tc[sb] < LAST_NONE + dt ? LAST_NONE : o->last_tc[sb] - dt;
+  }
+  o->clock[b] += 1u;
+}
+
+static float action_weight(const oracle_t* o, const void* action, int dtype, size_t idx) {
+  const lbsim_config_t* c = &o->cfg;
+  if (c->action_type == LBSIM_ACTION_DISCRETE) {
+    int64_t a = dtype == LBSIM_DTYPE_I64 ? ((const int64_t*)action)[idx]
+                                         : (int64_t)((const int32_t*)action)[idx];
+    if (a < 0) a += c->num_discrete;
+    if (a < 0) a = 0;
+    if (a >= c->num_discrete) a = c->num_discrete - 1;
+    return c->discrete_weights[a];
+  }
+  const float a = ((const float*)action)[idx];
+  return a < c->min_weight ? c->min_weight : (a > c->max_weight ? c->max_weight : a);
+}
+
+/* env.py:460-468: running mean/std in float64; count is incremented first; out = float32 cast. */
+void oracle_normalize(const float* raw, int n, int32_t* count, double* mean, double* std,
+                      float* out) {
+  const int32_t cnt = *count + 1;
+  for (int e = 0; e < n; ++e) {
+    const double ob = (double)raw[e];
+    double m = mean[e];
+    const double sd = std[e];
+    const double delta = ob - m;
+    m = m + delta / (double)cnt;
+    const double delta2 = ob - m;
+    double v = (sd * sd * (double)(cnt - 1) + delta * delta2) / (double)cnt;
+    v = v > 1e-8 ? v : 1e-8;
+    const double ns = sqrt(v);
+    mean[e] = m;
+    std[e] = ns;
+    out[e] = (float)((ob - m) / (ns + 1e-8));
+  }
+  *count = cnt;
+}
+
+/* Observation (S, 11), reward, bookkeeping and normalisation of env b. */
+static void observe(oracle_t* o, size_t b, float* obs_out, float* reward_out, uint8_t* done_out,
+                    int step_mode) {
+  const int S = o->S;
+  float raw[LBSIM_MAX_SERVERS * NF];
+  for (int s = 0; s < S; ++s) {
+    const size_t sb = b * (size_t)S + (size_t)s;
+    const uint32_t rc = o->res_count[sb];
+    const int n = rc < (uint32_t)K ? (int)rc : K;
+    float w[K];
+    uint64_t wq[K];
+    slot_weights(o->res_ts + sb * K, n, o->decay_c, w, wq);
+    float ff[5], fd[5];
+    features_one(o->res_fct + sb * K, w, wq, n, ff);
+    features_one(o->res_dur + sb * K, w, wq, n, fd);
+    raw[s * NF + 0] = (float)ring_count(o, sb);
+    for (int f = 0; f < 5; ++f) { raw[s * NF + 1 + f] = ff[f]; raw[s * NF + 6 + f] = fd[f]; }
+  }
+  if (step_mode) {
+    const double r = oracle_reward(raw, S, o->cfg.reward_metric, o->cfg.reward_field);
+    reward_out[b] = (float)r;
+    o->ep_step[b] += 1;
+    o->ep_return[b] += r;
+    done_out[b] = (uint8_t)(o->ep_step[b] >= o->cfg.max_steps);
+  }
+  float* row = obs_out + b * (size_t)S * NF;
+  if (o->cfg.normalize_obs) {
+    const size_t off = b * (size_t)S * NF;
+    oracle_normalize(raw, S * NF, &o->norm_count[b], o->norm_mean + off, o->norm_std + off, row);
+  } else {
+    memcpy(row, raw, sizeof(float) * (size_t)S * NF);
+  }
+}
+
+static void reset_env(oracle_t* o, size_t b) {
+  env_ctx e;
+  memset(&e, 0, sizeof(e));
+  e.o = o; e.b = b; e.gid = (uint32_t)(o->cfg.env_id_offset + (int64_t)b);
+  const int S = o->S;
+  o->episode[b] += 1u;
+  o->clock[b] = 0u;
+  o->dropped[b] = 0u;
+  o->arr_idx[b] = 0u;
+  draw_arrival(&e, 0);
+  for (int s = 0; s < S; ++s) {
+    const size_t sb = b * (size_t)S + (size_t)s;
+    o->hc[sb] = 0u;
+    o->last_tc[sb] = LAST_NONE;
+    o->res_count[sb] = 0u;
+  }
+  float w1[LBSIM_MAX_SERVERS];
+  for (int s = 0; s < LBSIM_MAX_SERVERS; ++s) w1[s] = 1.0f;
+  for (int k = 0; k < o->cfg.warmup_steps; ++k) sim_step(&e, w1);
+  o->ep_step[b] = 0;
+  o->ep_return[b] = 0.0;
+}
+
+int oracle_reset(oracle_t* o, const uint8_t* mask, float* obs_out) {
+  const long B = o->B;
+#pragma omp parallel for schedule(dynamic, 16) num_threads(o->threads)
+  for (long b = 0; b < B; ++b) {
+    if (mask && !mask[b]) continue;
+    reset_env(o, (size_t)b);
+    observe(o, (size_t)b, obs_out, NULL, NULL, 0);
+  }
+  if (!mask) o->initialised = 1;
+  return 0;
+}
+
+int oracle_step(oracle_t* o, const void* action, int dtype, float* obs_out, float* reward_out,
+                uint8_t* done_out, int32_t* assign_out) {
+  if (!o->initialised) return LBSIM_EINVAL;
+  const long B = o->B;
+  const int S = o->S;
+#pragma omp parallel for schedule(dynamic, 16) num_threads(o->threads)
+  for (long b = 0; b < B; ++b) {
+    env_ctx e;
+    memset(&e, 0, sizeof(e));
+    e.o = o; e.b = (size_t)b; e.gid = (uint32_t)(o->cfg.env_id_offset + (int64_t)b);
+    float w[LBSIM_MAX_SERVERS];
+    for (int s = 0; s < S; ++s) w[s] = action_weight(o, action, dtype, (size_t)b * S + (size_t)s);
+    sim_step(&e, w);
+    if (assign_out)
+      for (int s = 0; s < S; ++s) assign_out[(size_t)b * S + (size_t)s] = e.assigned[s];
+    observe(o, (size_t)b, obs_out, reward_out, done_out, 1);
+  }
+  return 0;
+}
+
+void oracle_episode_stats(const oracle_t* o, int32_t* len_out, double* ret_out) {
+  for (int b = 0; b < o->B; ++b) {
+    if (len_out) len_out[b] = o->ep_step[b];
+    if (ret_out) ret_out[b] = o->ep_return[b];
+  }
+}
+
+/* Stateless batch helpers used by the golden tests. */
+void oracle_reward_batch(const float* obs, long n, int S, int metric, int field, float* out) {
+  for (long i = 0; i < n; ++i) out[i] = (float)oracle_reward(obs + i * (long)S * NF, S, metric, field);
+}
+
+void oracle_reward_batch64(const float* obs, long n, int S, int metric, int field, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = oracle_reward(obs + i * (long)S * NF, S, metric, field);
+}
+
+void oracle_features_batch(const float* values, const uint32_t* ts, const uint32_t* counts, long n,
+                           float decay_factor, float* out) {
+  for (long r = 0; r < n; ++r)
+    oracle_reservoir_features(values + r * K, ts + r * K, counts[r], decay_factor, out + r * 5);
+}
+
+/* Algorithm R slot for the insert that sees `count` earlier samples (-1 = rejected); exposes the
+ * decision rule alone for the uniformity test (test_reservoir.py:243-287 analogue). */
+long oracle_algr_slot(uint32_t count, uint32_t gid, uint32_t episode, uint32_t server,
+                      const uint32_t key[2]) {
+  if (count < (uint32_t)K) return (long)count;
+  const uint32_t ctr[4] = {count >> 1, gid, episode, (2u << 24) | server};
+  uint32_t d[4];
+  oracle_philox(ctr, key, d);
+  const uint32_t hi = (count & 1u) ? d[3] : d[1];
+  const uint32_t lo = (count & 1u) ? d[2] : d[0];
+  const unsigned __int128 prod = (unsigned __int128)(((uint64_t)hi << 32) | lo) * ((uint64_t)count + 1u);
+  const uint64_t j = (uint64_t)(prod >> 64);
+  return j < (uint64_t)K ? (long)j : -1;
+}

@@ -1,0 +1,26 @@
+"""Shared pytest setup: `gpu` marker, repo root on sys.path, one-time oracle build."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+
+
+@pytest.fixture(scope="session")
+def oracle_mod():
+    import oracle
+    oracle.load()
+    return oracle
+
+
+@pytest.fixture(scope="session")
+def golden_dir():
+    return GOLDEN

@@ -1,0 +1,41 @@
+"""Snapshot layout of lbsim device state — shared by liblbsim and the oracle."""
+import numpy as np
+
+K, NF = 128, 11
+
+
+def sections(B, S, Q, normalize):
+    BS = B * S
+    out = [("next_arr", np.int32, B), ("next_work", np.float32, B), ("next_u2", np.uint32, B),
+           ("next_u3", np.uint32, B), ("arr_idx", np.uint32, B), ("episode", np.uint32, B),
+           ("clock", np.uint32, B), ("ep_step", np.int32, B), ("dropped", np.uint32, B),
+           ("norm_count", np.int32, B), ("ep_return", np.float64, B), ("hc", np.uint32, BS),
+           ("last_tc", np.int32, BS), ("res_count", np.uint32, BS), ("ring", np.int32, BS * Q * 2),
+           ("res_fct", np.float32, BS * K), ("res_dur", np.float32, BS * K),
+           ("res_ts", np.uint32, BS * K)]
+    if normalize:
+        out += [("norm_mean", np.float64, BS * NF), ("norm_std", np.float64, BS * NF)]
+    return out
+
+
+def parse(buf: bytes, B, S, Q, normalize):
+    d, off = {}, 0
+    for name, dt, n in sections(B, S, Q, normalize):
+        nb = np.dtype(dt).itemsize * n
+        d[name] = np.frombuffer(buf[off:off + nb], dtype=dt)
+        off += nb
+    assert off == len(buf), (off, len(buf))
+    return d
+
+
+def live_ring(d, B, S, Q):
+    """Ring entries that are in flight (stale slots beyond the count are not state)."""
+    hc = d["hc"].reshape(B, S)
+    ring = d["ring"].reshape(B, S, Q, 2)
+    live = np.zeros((B, S, Q), bool)
+    for b in range(B):
+        for s in range(S):
+            h, c = int(hc[b, s] & 0xFFFF), int(hc[b, s] >> 16)
+            for i in range(c):
+                live[b, s, (h + i) % Q] = True
+    return np.where(live[..., None], ring, 0)

@@ -1,0 +1,124 @@
+"""The CPU oracle against the reference's own outputs (tests/golden/, made by gen_golden.py).
+
+Pins oracle/lbsim_oracle.c to the reference Python before the oracle is trusted as the GPU
+checker:
+  reservoir.py:105-196 features   -> bit-exact mean/p90/std/p90_decay, mean_decay <= 2e-6 rel
+  rewards.py:21-381 (9 metrics)   -> <= 1e-12 rel in float64 (numpy's x**2 goes through libm pow)
+  env.py:450-470 normalisation    -> float32 cast of the float64 reference
+  Philox4x32-10                   -> Random123 known-answer vectors
+  Algorithm R                     -> uniformity chi^2 as test_reservoir.py:243-287
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+FIELD_COL = {"flow_duration_avg_decay": 10, "n_flow_on": 0, "fct_mean": 1, "no_such_field": -1}
+
+
+def test_philox_known_answers(oracle_mod):
+    kat = [((0, 0, 0, 0), (0, 0), (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)),
+           ((0xFFFFFFFF,) * 4, (0xFFFFFFFF,) * 2, (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)),
+           ((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0),
+            (0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1))]
+    for ctr, key, exp in kat:
+        assert list(oracle_mod.philox(ctr, key)) == list(exp)
+
+
+def test_log_exp2_accuracy(oracle_mod):
+    lib = oracle_mod.load()
+    xs = np.linspace(-59.9, 0.0, 20001, dtype=np.float32)
+    rel = max(abs(lib.oracle_exp2f(float(x)) / 2.0 ** float(x) - 1.0) for x in xs)
+    assert rel < 2e-7
+    us = (np.arange(1, 2 ** 24, 997) * 2.0 ** -24).astype(np.float32)
+    err = max(abs(lib.oracle_logf(float(u)) - math.log(float(u))) for u in us)
+    assert err < 1e-6
+
+
+def test_reservoir_features_match_reference(oracle_mod, golden_dir):
+    g = np.load(os.path.join(golden_dir, "reservoir_features.npz"))
+    out = oracle_mod.features(g["values"], g["ts_ms"], g["counts"], float(g["decay"]))
+    exp = g["expected"]
+    for f in (0, 1, 2, 4):  # mean, p90, std, p90_decay: bit-exact float32
+        np.testing.assert_array_equal(out[:, f], exp[:, f].astype(np.float32), err_msg=f"col {f}")
+    rel = np.abs(out[:, 3] - exp[:, 3]) / np.maximum(np.abs(exp[:, 3]), 1e-30)
+    assert rel.max() < 2e-6, rel.max()
+    # known answers of test_reservoir.py:80-131
+    assert out[0].tolist() == [0.0] * 5
+    assert abs(out[1, 0] - 3.0) < 1e-6 and abs(out[1, 2] - np.std([1, 2, 3, 4, 5])) < 1e-6
+    assert 85 < out[2, 1] < 95
+    assert abs(out[3, 0] - 5.5) < 0.5 and 7.0 < out[3, 3] < 10.0
+
+
+@pytest.mark.parametrize("S", [1, 2, 3, 4, 8, 16])
+def test_rewards_match_reference(oracle_mod, golden_dir, S):
+    g = np.load(os.path.join(golden_dir, "rewards.npz"))
+    metrics, fields = list(g["metrics"]), list(g["fields"])
+    obs, exp = g[f"obs_S{S}"], g[f"expected_S{S}"]
+    for m in range(len(metrics)):
+        for fi, fname in enumerate(fields):
+            got = oracle_mod.rewards(obs, m, FIELD_COL[str(fname)], f64=True)
+            want = exp[:, m, fi]
+            np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-300,
+                                       err_msg=f"{metrics[m]} {fname}")
+
+
+def test_metric_known_answers(oracle_mod, golden_dir):
+    """rewards.py docstring / test_rewards.py values through the obs path (all servers active)."""
+    plumb = json.load(open(os.path.join(golden_dir, "env_plumbing.json")))
+    names = ["jain", "variance", "std", "cv", "max", "min", "product", "range", "gini"]
+    for case in plumb["metric_kat"]:
+        vals = case["values"]
+        obs = np.ones((1, len(vals), 11), np.float32)
+        obs[0, :, 10] = vals
+        for m, name in enumerate(names):
+            got = oracle_mod.rewards(obs, m, 10, f64=True)[0]
+            assert got == pytest.approx(case[name], rel=1e-12, abs=1e-15), name
+
+
+def test_normalisation_matches_reference(oracle_mod, golden_dir):
+    """env.py:450-470 through a 1-env oracle whose raw obs are injected via the state snapshot."""
+    plumb = json.load(open(os.path.join(golden_dir, "env_plumbing.json")))
+    seq = [np.array(x, np.float32) for x in plumb["normalize"]["inputs"]]
+    want = [np.array(x) for x in plumb["normalize"]["outputs"]]
+    lib = oracle_mod.load()
+    mean = np.zeros(44, np.float64)
+    std = np.ones(44, np.float64)
+    count = np.zeros(1, np.int32)
+    for raw, w in zip(seq, want):
+        out = np.zeros(44, np.float32)
+        lib.oracle_normalize(oracle_mod.ptr(np.ascontiguousarray(raw.reshape(-1))), 44,
+                             oracle_mod.ptr(count), oracle_mod.ptr(mean), oracle_mod.ptr(std),
+                             oracle_mod.ptr(out))
+        np.testing.assert_array_equal(out, w.reshape(-1).astype(np.float32))
+
+
+def test_algorithm_r_uniformity(oracle_mod):
+    """Every stream element is kept with probability K/N (chi^2 as test_reservoir.py:243-287)."""
+    import ctypes
+    lib = oracle_mod.load()
+    K, N, trials = 128, 1000, 500
+    counts = np.zeros(N)
+    key = np.array([12345, 678], np.uint32)
+    for t in range(trials):
+        slots = np.arange(K)  # slot -> stream index
+        for c in range(K, N):
+            j = lib.oracle_algr_slot(c, t, 1, 0, oracle_mod.ptr(key))
+            if j >= 0:
+                slots[j] = c
+        counts[slots] += 1
+    expected = trials * K / N
+    chi2 = np.sum((counts - expected) ** 2 / expected)
+    assert chi2 < 1100, chi2
+
+
+def test_algorithm_r_acceptance_rate(oracle_mod):
+    lib = oracle_mod.load()
+    key = np.array([1, 2], np.uint32)
+    for count in (128, 1000, 100000, 2 ** 31 - 5):
+        acc = sum(lib.oracle_algr_slot(count, e, 7, 3, oracle_mod.ptr(key)) >= 0
+                  for e in range(20000))
+        p = 128 / (count + 1)
+        assert abs(acc / 20000 - p) < 5 * math.sqrt(p * (1 - p) / 20000) + 1e-4
