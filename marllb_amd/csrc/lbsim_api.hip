@@ -204,27 +204,37 @@ struct ProfScope {
   }
 };
 
+template <int MODE>
+void launch_dynamics_t(lbsim_t* h, const void* action, int dtype, int32_t* assign,
+                       const uint8_t* mask, hipStream_t stream) {
+  const dim3 block(64), grid((unsigned)((h->B + 63) / 64));
+  if (h->S <= 4)
+    hipLaunchKernelGGL((dynamics_kernel<4, MODE>), grid, block, 0, stream, h->st, h->prm, action,
+                       dtype, assign, mask);
+  else if (h->S <= 8)
+    hipLaunchKernelGGL((dynamics_kernel<8, MODE>), grid, block, 0, stream, h->st, h->prm, action,
+                       dtype, assign, mask);
+  else
+    hipLaunchKernelGGL((dynamics_kernel<16, MODE>), grid, block, 0, stream, h->st, h->prm, action,
+                       dtype, assign, mask);
+}
+
 int launch_dynamics(lbsim_t* h, const void* action, int dtype, int32_t* assign,
                     const uint8_t* mask, int mode, hipStream_t stream) {
-  const dim3 block(64), grid((unsigned)((h->B + 63) / 64));
   ProfScope ps(h, stream, mode == kModeStep ? 0 : 2);
-  if (h->S <= 4)
-    hipLaunchKernelGGL(dynamics_kernel<4>, grid, block, 0, stream, h->st, h->prm, action, dtype,
-                       assign, mask, mode);
-  else if (h->S <= 8)
-    hipLaunchKernelGGL(dynamics_kernel<8>, grid, block, 0, stream, h->st, h->prm, action, dtype,
-                       assign, mask, mode);
-  else
-    hipLaunchKernelGGL(dynamics_kernel<16>, grid, block, 0, stream, h->st, h->prm, action, dtype,
-                       assign, mask, mode);
+  if (mode == kModeStep) launch_dynamics_t<kModeStep>(h, action, dtype, assign, mask, stream);
+  else launch_dynamics_t<kModeReset>(h, action, dtype, assign, mask, stream);
   return launch_check(h, "dynamics_kernel");
 }
 
 int launch_observe(lbsim_t* h, const ObsOutputs& o, const uint8_t* mask, int mode,
                    hipStream_t stream) {
   ProfScope ps(h, stream, mode == kModeStep ? 1 : 3);
-  hipLaunchKernelGGL(observe_kernel, dim3((unsigned)h->B), dim3(64), 0, stream, h->st, h->prm, o,
-                     mask, mode);
+  const dim3 grid((unsigned)h->B), block(64);
+  if (mode == kModeStep)
+    hipLaunchKernelGGL(observe_kernel<kModeStep>, grid, block, 0, stream, h->st, h->prm, o, mask);
+  else
+    hipLaunchKernelGGL(observe_kernel<kModeReset>, grid, block, 0, stream, h->st, h->prm, o, mask);
   return launch_check(h, "observe_kernel");
 }
 

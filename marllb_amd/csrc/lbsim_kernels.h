@@ -83,7 +83,9 @@ struct SimParams {
 template <int MAXS>
 struct LaneState {
   int32_t cnt[MAXS], head[MAXS];
-  int32_t head_tc[MAXS], head_ta[MAXS], tail_tc[MAXS], last_tc[MAXS];
+  int32_t head_tc[MAXS], head_ta[MAXS];  // entry at the ring head (valid if cnt >= 1)
+  int32_t nxt_tc[MAXS], nxt_ta[MAXS];    // entry after the head, prefetched (valid if cnt >= 2)
+  int32_t tail_tc[MAXS], last_tc[MAXS];
   uint32_t rcnt[MAXS];
   int32_t assigned[MAXS];
   float score[MAXS];
@@ -100,58 +102,15 @@ __device__ __forceinline__ float policy_score(int policy, int32_t cnt, double de
   return (float)((double)(cnt + 1) / den);
 }
 
-template <int MAXS>
-__device__ __forceinline__ void res_insert(const DevState& st, const SimParams& p,
-                                           LaneState<MAXS>& L, int s, size_t sbase, float fct,
-                                           float dur, uint32_t ts_ms) {
-  const uint32_t c = L.rcnt[s];
-  int slot;
-  if (c < (uint32_t)K) {
-    slot = (int)c;
-  } else {
-    const u32x4 d = philox4x32_10(
-        u32x4{c >> 1, L.gid, L.episode, (kStreamReservoir << 24) | (uint32_t)s}, p.key0, p.key1);
-    const uint32_t hi = (c & 1u) ? d.w : d.y;
-    const uint32_t lo = (c & 1u) ? d.z : d.x;
-    const uint64_t j = mulhi64_by_u33(hi, lo, (uint64_t)c + 1u);
-    slot = j < (uint64_t)K ? (int)j : -1;
-  }
-  if (slot >= 0) {
-    const size_t r = sbase * K + (size_t)slot;
-    st.res_fct[r] = fct;
-    st.res_dur[r] = dur;
-    st.res_ts[r] = ts_ms;
-  }
-  if (c != 0xFFFFFFFFu) L.rcnt[s] = c + 1u;
-}
-
-// Pop every flow of server s completed at or before time t (relative us); each completion
-// yields one fct sample (t_complete - t_arrival, lbhash.h:116-124) and one duration sample
-// (t_complete - t_service_start) that share one Algorithm R decision (reservoir.py:261-265).
-template <int MAXS>
-__device__ __forceinline__ void pop_until(const DevState& st, const SimParams& p,
-                                          LaneState<MAXS>& L, int s, size_t b, int32_t t,
-                                          uint64_t base_us) {
-  const size_t sbase = b * (size_t)p.S + (size_t)s;
-  while (L.cnt[s] > 0 && L.head_tc[s] <= t) {
-    const int32_t tc = L.head_tc[s], ta = L.head_ta[s];
-    const int32_t start = ta > L.last_tc[s] ? ta : L.last_tc[s];
-    const float fct = (float)(tc - ta) * 1.0e-6f;
-    const float dur = (float)(tc - start) * 1.0e-6f;
-    L.last_tc[s] = tc;
-    const uint32_t ts_ms = (uint32_t)((base_us + (uint64_t)(int64_t)tc) / 1000u);
-    res_insert<MAXS>(st, p, L, s, sbase, fct, dur, ts_ms);
-    int h = L.head[s] + 1;
-    if (h == p.Q) h = 0;
-    L.head[s] = h;
-    L.cnt[s] -= 1;
-    if (L.cnt[s] > 0) {
-      const int2 e = st.ring[sbase * p.Q + h];
-      L.head_tc[s] = e.x;
-      L.head_ta[s] = e.y;
-    }
-    L.score[s] = policy_score(p.policy, L.cnt[s], L.den[s]);
-  }
+// Arrival draw for arrival index `idx`: gap to it, its work, its two hash words.
+__device__ __forceinline__ void arrival_from_draw(const SimParams& p, const u32x4& d,
+                                                  int32_t t_prev, int32_t& next_arr,
+                                                  float& work, uint32_t& u2, uint32_t& u3) {
+  const int32_t gap = (int32_t)(-lb_logf(u01_open0(d.x)) * p.mean_gap_us);
+  next_arr = t_prev + gap;
+  work = -lb_logf(u01_open0(d.y));
+  u2 = d.z;
+  u3 = d.w;
 }
 
 template <int MAXS>
@@ -159,19 +118,24 @@ __device__ __forceinline__ void draw_arrival(const SimParams& p, LaneState<MAXS>
                                              int32_t t_prev) {
   const u32x4 d = philox4x32_10(u32x4{L.arr_idx, L.gid, L.episode, kStreamArrival << 24},
                                 p.key0, p.key1);
-  const int32_t gap = (int32_t)(-lb_logf(u01_open0(d.x)) * p.mean_gap_us);
-  L.next_arr = t_prev + gap;
-  L.next_work = -lb_logf(u01_open0(d.y));
-  L.u2 = d.z;
-  L.u3 = d.w;
+  arrival_from_draw(p, d, t_prev, L.next_arr, L.next_work, L.u2, L.u3);
 }
 
 // One simulated step of dt_us with server weights w[] (env.py:230-259 with real dynamics).
+//
+// Event loop, one event per iteration per lane: the earliest pending completion (if it is due no
+// later than the next arrival, or than the step end when no arrival is due) or else the next
+// arrival.  Both event kinds need exactly one Philox block (Algorithm R draw / next-arrival
+// draw), computed unconditionally so the 64 lanes stay converged through the expensive part.
+// Per server the completions are processed in t_complete order before any arrival at the same
+// or a later time, which is the order the oracle (server by server) produces, so every
+// reservoir sees the same insert sequence and the state is bit-identical.
 template <int MAXS>
 __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
                                          LaneState<MAXS>& L, size_t b, const float* w) {
   const int S = p.S, Q = p.Q;
-  const uint64_t base_us = (uint64_t)L.clock * (uint64_t)p.dt_us;
+  const int32_t dt = p.dt_us;
+  const uint64_t base_us = (uint64_t)L.clock * (uint64_t)dt;
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) {
     if (s < S) {
@@ -179,72 +143,133 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
       L.score[s] = policy_score(p.policy, L.cnt[s], L.den[s]);
     }
   }
-  while (L.next_arr < p.dt_us) {
-    const int32_t ta = L.next_arr;
+  for (;;) {
+    // earliest pending completion (ties: lowest server index)
+    int32_t tmin = 0x7FFFFFFF;
+    int smin = -1;
 #pragma unroll
     for (int s = 0; s < MAXS; ++s)
-      if (s < S) pop_until<MAXS>(st, p, L, s, b, ta, base_us);
+      if (s < S && L.cnt[s] > 0 && L.head_tc[s] < tmin) { tmin = L.head_tc[s]; smin = s; }
+    const bool arrival_due = L.next_arr < dt;
+    const int32_t horizon = arrival_due ? L.next_arr : dt;
+    const bool completion = smin >= 0 && tmin <= horizon;
+    if (!completion && !arrival_due) break;
 
-    // ---- choose a server (node.c:388-441); full servers (Q in flight) are not eligible
-    int chosen = -1;
-    if (p.policy == 1 || p.policy == 3) {  // SED2 / LSQ2: two uniform candidates
-      const int h1 = (int)(((uint64_t)L.u2 * (uint64_t)S) >> 32);
-      const int h2 = (int)(((uint64_t)L.u3 * (uint64_t)S) >> 32);
-      float s1 = 0.f, s2 = 0.f;
-      bool ok1 = false, ok2 = false;
+    // the one Philox block of this event
+    uint32_t cres = 0;
 #pragma unroll
-      for (int s = 0; s < MAXS; ++s) {
-        if (s == h1) { s1 = L.score[s]; ok1 = L.cnt[s] < Q; }
-        if (s == h2) { s2 = L.score[s]; ok2 = L.cnt[s] < Q; }
-      }
-      if (ok1 && ok2) chosen = (s2 < s1) ? h2 : h1;
-      else if (ok1) chosen = h1;
-      else if (ok2) chosen = h2;
-    } else {  // SED / LSQ: start at the hashed server, strict '<' scan in index order
-      const int h = (int)(((uint64_t)L.u2 * (uint64_t)S) >> 32);
-      float best = 0.f;
-#pragma unroll
-      for (int s = 0; s < MAXS; ++s)
-        if (s == h && L.cnt[s] < Q) { chosen = s; best = L.score[s]; }
-#pragma unroll
-      for (int s = 0; s < MAXS; ++s) {
-        if (s < S && L.cnt[s] < Q) {
-          if (chosen < 0 || L.score[s] < best) { chosen = s; best = L.score[s]; }
-        }
-      }
-    }
+    for (int s = 0; s < MAXS; ++s)
+      if (s == smin) cres = L.rcnt[s];
+    const u32x4 ctr = completion
+        ? u32x4{cres >> 1, L.gid, L.episode, (kStreamReservoir << 24) | (uint32_t)smin}
+        : u32x4{L.arr_idx + 1u, L.gid, L.episode, kStreamArrival << 24};
+    const u32x4 d = philox4x32_10(ctr, p.key0, p.key1);
 
-    if (chosen < 0) {
-      L.dropped += 1u;
-    } else {
+    if (completion) {
+      // ---- completion of the head flow of server smin (lbhash.h:116-124, 131-135)
 #pragma unroll
       for (int s = 0; s < MAXS; ++s) {
-        if (s == chosen) {
+        if (s == smin) {
           const size_t sbase = b * (size_t)S + (size_t)s;
-          const int32_t start = L.cnt[s] > 0 ? (L.tail_tc[s] > ta ? L.tail_tc[s] : ta) : ta;
-          int32_t svc = (int32_t)(L.next_work * p.svc_scale[s]);
-          if (svc < 1) svc = 1;
-          const int32_t tc = start + svc;
-          int pos = L.head[s] + L.cnt[s];
-          if (pos >= Q) pos -= Q;
-          st.ring[sbase * Q + pos] = make_int2(tc, ta);
-          if (L.cnt[s] == 0) { L.head_tc[s] = tc; L.head_ta[s] = ta; }
-          L.cnt[s] += 1;
-          L.tail_tc[s] = tc;
-          L.assigned[s] += 1;
+          const int32_t tc = L.head_tc[s], ta = L.head_ta[s];
+          const int32_t start = ta > L.last_tc[s] ? ta : L.last_tc[s];
+          const float fct = (float)(tc - ta) * 1.0e-6f;
+          const float dur = (float)(tc - start) * 1.0e-6f;
+          L.last_tc[s] = tc;
+          const uint32_t ts_ms = (uint32_t)((base_us + (uint64_t)(int64_t)tc) / 1000u);
+          // Algorithm R (reservoir.py:64-85): slot c while filling, else j = randint(0, c+1)
+          const uint32_t c = L.rcnt[s];
+          int slot;
+          if (c < (uint32_t)K) {
+            slot = (int)c;
+          } else {
+            const uint32_t hi = (c & 1u) ? d.w : d.y;
+            const uint32_t lo = (c & 1u) ? d.z : d.x;
+            const uint64_t j = mulhi64_by_u33(hi, lo, (uint64_t)c + 1u);
+            slot = j < (uint64_t)K ? (int)j : -1;
+          }
+          if (slot >= 0) {
+            const size_t r = sbase * K + (size_t)slot;
+            st.res_fct[r] = fct;
+            st.res_dur[r] = dur;
+            st.res_ts[r] = ts_ms;
+          }
+          if (c != 0xFFFFFFFFu) L.rcnt[s] = c + 1u;
+          int h = L.head[s] + 1;
+          if (h == Q) h = 0;
+          L.head[s] = h;
+          L.cnt[s] -= 1;
+          L.head_tc[s] = L.nxt_tc[s];
+          L.head_ta[s] = L.nxt_ta[s];
+          if (L.cnt[s] >= 2) {  // prefetch the entry after the new head
+            int h2 = h + 1;
+            if (h2 == Q) h2 = 0;
+            const int2 e = st.ring[sbase * Q + h2];
+            L.nxt_tc[s] = e.x;
+            L.nxt_ta[s] = e.y;
+          }
           L.score[s] = policy_score(p.policy, L.cnt[s], L.den[s]);
         }
       }
-    }
-    L.arr_idx += 1u;
-    draw_arrival<MAXS>(p, L, ta);
-  }
+    } else {
+      // ---- arrival at next_arr: choose a server (node.c:388-441); full servers ineligible
+      const int32_t ta = L.next_arr;
+      int chosen = -1;
+      if (p.policy == 1 || p.policy == 3) {  // SED2 / LSQ2: two uniform candidates
+        const int h1 = (int)(((uint64_t)L.u2 * (uint64_t)S) >> 32);
+        const int h2 = (int)(((uint64_t)L.u3 * (uint64_t)S) >> 32);
+        float s1 = 0.f, s2 = 0.f;
+        bool ok1 = false, ok2 = false;
 #pragma unroll
-  for (int s = 0; s < MAXS; ++s)
-    if (s < S) pop_until<MAXS>(st, p, L, s, b, p.dt_us, base_us);
+        for (int s = 0; s < MAXS; ++s) {
+          if (s == h1) { s1 = L.score[s]; ok1 = L.cnt[s] < Q; }
+          if (s == h2) { s2 = L.score[s]; ok2 = L.cnt[s] < Q; }
+        }
+        if (ok1 && ok2) chosen = (s2 < s1) ? h2 : h1;
+        else if (ok1) chosen = h1;
+        else if (ok2) chosen = h2;
+      } else {  // SED / LSQ: start at the hashed server, strict '<' scan in index order
+        const int h = (int)(((uint64_t)L.u2 * (uint64_t)S) >> 32);
+        float best = 0.f;
+#pragma unroll
+        for (int s = 0; s < MAXS; ++s)
+          if (s == h && L.cnt[s] < Q) { chosen = s; best = L.score[s]; }
+#pragma unroll
+        for (int s = 0; s < MAXS; ++s) {
+          if (s < S && L.cnt[s] < Q) {
+            if (chosen < 0 || L.score[s] < best) { chosen = s; best = L.score[s]; }
+          }
+        }
+      }
+      if (chosen < 0) {
+        L.dropped += 1u;
+      } else {
+#pragma unroll
+        for (int s = 0; s < MAXS; ++s) {
+          if (s == chosen) {  // FIFO service: start when the server's last queued flow ends
+            const size_t sbase = b * (size_t)S + (size_t)s;
+            const int32_t start = L.cnt[s] > 0 ? (L.tail_tc[s] > ta ? L.tail_tc[s] : ta) : ta;
+            int32_t svc = (int32_t)(L.next_work * p.svc_scale[s]);
+            if (svc < 1) svc = 1;
+            const int32_t tc = start + svc;
+            int pos = L.head[s] + L.cnt[s];
+            if (pos >= Q) pos -= Q;
+            st.ring[sbase * Q + pos] = make_int2(tc, ta);
+            if (L.cnt[s] == 0) { L.head_tc[s] = tc; L.head_ta[s] = ta; }
+            else if (L.cnt[s] == 1) { L.nxt_tc[s] = tc; L.nxt_ta[s] = ta; }
+            L.cnt[s] += 1;
+            L.tail_tc[s] = tc;
+            L.assigned[s] += 1;
+            L.score[s] = policy_score(p.policy, L.cnt[s], L.den[s]);
+          }
+        }
+      }
+      L.arr_idx += 1u;
+      arrival_from_draw(p, d, ta, L.next_arr, L.next_work, L.u2, L.u3);
+    }
+  }
 
   // ---- rebase relative times to the next step's start
-  const int32_t dt = p.dt_us;
   L.next_arr -= dt;
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) {
@@ -260,6 +285,8 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
       }
       L.head_tc[s] -= dt;
       L.head_ta[s] -= dt;
+      L.nxt_tc[s] -= dt;
+      L.nxt_ta[s] -= dt;
       L.tail_tc[s] -= dt;
       L.last_tc[s] = (L.last_tc[s] < kLastNone + dt) ? kLastNone : L.last_tc[s] - dt;
     }
@@ -282,10 +309,12 @@ __device__ __forceinline__ float action_weight(const SimParams& p, const void* a
   return a < p.min_w ? p.min_w : (a > p.max_w ? p.max_w : a);
 }
 
-template <int MAXS>
+// MODE is a template parameter so step and reset launches are separate kernels in profiles.
+template <int MAXS, int MODE>
 __global__ void __launch_bounds__(64)
     dynamics_kernel(DevState st, SimParams p, const void* action, int action_dtype,
-                    int32_t* assign_out, const uint8_t* reset_mask, int mode) {
+                    int32_t* assign_out, const uint8_t* reset_mask) {
+  constexpr int mode = MODE;
   const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= (size_t)p.B) return;
   const int S = p.S;
@@ -302,6 +331,7 @@ __global__ void __launch_bounds__(64)
 #pragma unroll
     for (int s = 0; s < MAXS; ++s) {
       L.cnt[s] = 0; L.head[s] = 0; L.head_tc[s] = 0; L.head_ta[s] = 0; L.tail_tc[s] = 0;
+      L.nxt_tc[s] = 0; L.nxt_ta[s] = 0;
       L.last_tc[s] = kLastNone; L.rcnt[s] = 0u; L.assigned[s] = 0;
     }
     float w1[MAXS];
@@ -329,6 +359,8 @@ __global__ void __launch_bounds__(64)
         L.last_tc[s] = st.last_tc[sb];
         L.rcnt[s] = st.res_count[sb];
         L.assigned[s] = 0;
+        L.head_tc[s] = 0; L.head_ta[s] = 0; L.tail_tc[s] = 0;
+        L.nxt_tc[s] = 0; L.nxt_ta[s] = 0;
         if (L.cnt[s] > 0) {
           const int2 e = st.ring[sb * p.Q + L.head[s]];
           L.head_tc[s] = e.x;
@@ -336,8 +368,13 @@ __global__ void __launch_bounds__(64)
           int tp = L.head[s] + L.cnt[s] - 1;
           if (tp >= p.Q) tp -= p.Q;
           L.tail_tc[s] = st.ring[sb * p.Q + tp].x;
-        } else {
-          L.head_tc[s] = 0; L.head_ta[s] = 0; L.tail_tc[s] = 0;
+        }
+        if (L.cnt[s] > 1) {
+          int h2 = L.head[s] + 1;
+          if (h2 >= p.Q) h2 -= p.Q;
+          const int2 e = st.ring[sb * p.Q + h2];
+          L.nxt_tc[s] = e.x;
+          L.nxt_ta[s] = e.y;
         }
       }
     }
@@ -683,8 +720,10 @@ struct ObsOutputs {
   double* ep_ret;
 };
 
+template <int MODE>
 __global__ void __launch_bounds__(64)
-    observe_kernel(DevState st, SimParams p, ObsOutputs out, const uint8_t* reset_mask, int mode) {
+    observe_kernel(DevState st, SimParams p, ObsOutputs out, const uint8_t* reset_mask) {
+  constexpr int mode = MODE;
   const size_t b = blockIdx.x;
   const int lane = threadIdx.x;
   if (mode == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;

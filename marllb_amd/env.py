@@ -207,6 +207,9 @@ class VecLoadBalanceEnv:
         self._ep_len = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
         self._ep_ret = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
         self._reset_done = False
+        # upper bound on every env's episode step since the last full reset: while it is below
+        # max_steps no env can be done, so the masked auto-reset launch is provably a no-op
+        self._step_bound = 0
 
     # -- helpers
     def _stream(self) -> int:
@@ -244,6 +247,7 @@ class VecLoadBalanceEnv:
             self.handle.check(self.handle.lib.lbsim_reset(self.handle.h, None, obs.data_ptr(),
                                                           self._stream()))
             self._reset_done = True
+            self._step_bound = 0
             self._last_obs = obs
             return obs
         if not self._reset_done:
@@ -284,7 +288,8 @@ class VecLoadBalanceEnv:
             info["assign_counts"] = assign
         if raw is not None:
             info["raw_obs"] = raw
-        if self.autoreset:
+        self._step_bound += 1
+        if self.autoreset and self._step_bound >= self.cfg.max_steps:
             if self.keep_terminal_obs:
                 info["terminal_obs"] = obs.clone()
             # envs with done == 0 are untouched by the masked reset (no host sync needed)
@@ -305,6 +310,7 @@ class VecLoadBalanceEnv:
     def set_state(self, data: bytes) -> None:
         self.handle.load_state(data)
         self._reset_done = True
+        self._step_bound = self.cfg.max_steps  # unknown episode steps: keep auto-reset armed
 
     def close(self) -> None:
         self.handle.close()

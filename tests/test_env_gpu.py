@@ -1,0 +1,202 @@
+"""The reference's env test-suite (simulation-mode/problem-03-rl-environment/tests/test_env.py)
+replayed on marllb_amd.LoadBalanceEnv, plus VecLoadBalanceEnv auto-reset semantics and the call
+pattern of problem-04's Trainer (trainer.py:92-126) as a drop-in check."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test run without a HIP device")
+
+
+def make(**kw):
+    from marllb_amd import LoadBalanceEnv
+    return LoadBalanceEnv(**kw)
+
+
+# ---- test_env.py:17-123 TestLoadBalanceEnvBasics
+def test_initialization():
+    env = make(num_servers=4, action_type="discrete", max_steps=100, use_shm=False, seed=42)
+    assert (env.num_servers, env.action_type, env.max_steps, env.use_shm) == (4, "discrete", 100, False)
+
+
+def test_spaces():
+    env = make(num_servers=4, seed=42)
+    assert env.observation_space.shape == (4, 11)
+    assert np.all(env.observation_space.low == 0) and np.all(env.observation_space.high == np.inf)
+    assert len(env.action_space.nvec) == 4 and np.all(env.action_space.nvec == 3)
+    env = make(num_servers=4, action_type="continuous", max_steps=100)
+    assert env.action_space.shape == (4,)
+    assert np.all(env.action_space.low == np.float32(0.1)) and np.all(env.action_space.high == 10.0)
+
+
+def test_reset_and_step():
+    env = make(num_servers=4, max_steps=100, seed=42)
+    obs = env.reset()
+    assert obs.shape == (4, 11) and obs.dtype == np.float32 and np.all(np.isfinite(obs))
+    assert env.current_step == 0
+    obs, reward, done, info = env.step(env.action_space.sample())
+    assert obs.shape == (4, 11) and np.all(np.isfinite(obs))
+    assert isinstance(reward, float) and np.isfinite(reward)
+    assert isinstance(done, bool)
+    assert {"step", "weights", "active_servers", "episode_return"} <= set(info)
+
+
+def test_episode_termination_and_return():
+    env = make(num_servers=4, max_steps=5, seed=42)
+    env.reset()
+    total = 0.0
+    for k in range(5):
+        obs, reward, done, info = env.step(env.action_space.sample())
+        total += reward
+        assert done == (k == 4)
+    assert info["episode"]["l"] == 5
+    assert info["episode"]["r"] == pytest.approx(total, abs=1e-5)
+    obs, reward, done, info = env.step(env.action_space.sample())  # reference keeps stepping
+    assert done and info["step"] == 6
+
+
+def test_seed_reproducibility():
+    a, b = make(num_servers=4, seed=42), make(num_servers=4, seed=42)
+    np.testing.assert_array_equal(a.reset(), b.reset())
+    act = np.array([0, 1, 2, 1])
+    np.testing.assert_array_equal(a.step(act)[0], b.step(act)[0])
+    c = make(num_servers=4, seed=43)
+    assert not np.array_equal(c.reset(), make(num_servers=4, seed=42).reset())
+    a.seed(7)
+    b.seed(7)
+    np.testing.assert_array_equal(a.reset(), b.reset())
+
+
+def test_action_conversion():
+    env = make(num_servers=4, action_type="discrete", discrete_weights=[1.0, 1.5, 2.0])
+    np.testing.assert_array_almost_equal(env._action_to_weights(np.array([0, 1, 2, 1])),
+                                         [1.0, 1.5, 2.0, 1.5])
+    env = make(num_servers=4, action_type="continuous", min_weight=0.5, max_weight=5.0)
+    np.testing.assert_array_almost_equal(env._action_to_weights(np.array([0.1, 2.0, 6.0, 3.0])),
+                                         [0.5, 2.0, 5.0, 3.0])
+
+
+def test_reward_in_jain_range():
+    env = make(num_servers=4, reward_metric="jain", seed=42)
+    env.reset()
+    for _ in range(5):
+        _, r, _, info = env.step(env.action_space.sample())
+        n = len(info["active_servers"])
+        assert 1.0 / n - 1e-6 <= r <= 1.0
+
+
+def test_normalization_updates():
+    env = make(num_servers=4, normalize_obs=True, seed=42)
+    env.reset()
+    obs, _, _, info = env.step(env.action_space.sample())
+    assert np.all(np.abs(obs) < 1e4) and info["active_servers"]
+
+
+def test_render_and_close(capsys):
+    env = make(num_servers=4, seed=1)
+    env.reset()
+    env.step(env.action_space.sample())
+    env.render(mode="human")
+    out = capsys.readouterr().out
+    assert "Step: 1/" in out and "Active Servers" in out
+    env.close()
+
+
+def test_errors_like_reference():
+    with pytest.raises(ValueError, match="Unsupported metric"):
+        make(num_servers=4, reward_metric="nope")
+    with pytest.raises(ValueError, match="Unknown action_type"):
+        make(num_servers=4, action_type="hybrid")
+    with pytest.raises(ValueError, match="shm_name"):
+        make(num_servers=4, use_shm=True)
+    env = make(num_servers=4, seed=1)
+    env.reset()
+    with pytest.raises(IndexError):
+        env.step(np.array([0, 1, 3, 0]))
+
+
+def test_unknown_reward_field_gives_zero():
+    env = make(num_servers=4, reward_field="no_such_field", seed=1)
+    env.reset()
+    assert env.step(np.array([0, 0, 0, 0]))[1] == 0.0
+
+
+# ---- problem-04 Trainer call pattern (continuous, tanh actions, flattened state)
+def test_trainer_call_pattern():
+    env = make(num_servers=4, action_type="continuous", max_steps=20, seed=3)
+    state = env.reset()
+    state = state.flatten() if state.ndim > 1 else state
+    assert state.shape == (44,)
+    w = torch.randn(44, 4)
+    for step in range(20):
+        if step < 5:
+            action = env.action_space.sample()
+        else:
+            action = torch.tanh(torch.from_numpy(state) @ w).numpy()  # SAC output in [-1, 1]
+        nxt, reward, done, info = env.step(action)
+        assert min(info["weights"]) >= np.float32(0.1) - 1e-7  # negatives clip to min_weight
+        state = nxt.flatten()
+        if done:
+            break
+    assert done and step == 19
+
+
+# ---- VecLoadBalanceEnv
+def test_vec_autoreset_matches_oracle(oracle_mod):
+    from marllb_amd import VecLoadBalanceEnv
+    from marllb_amd.env import make_config
+    B, S, T = 96, 4, 3
+    kw = dict(seed=77, max_steps=T)
+    env = VecLoadBalanceEnv(B, S, device="cuda:0", autoreset=True, keep_terminal_obs=True, **kw)
+    ora = oracle_mod.OracleEnv(make_config(B, S, **kw), threads=4)
+    np.testing.assert_array_equal(env.reset().cpu().numpy(), ora.reset())
+    rng = np.random.default_rng(1)
+    mask = (np.arange(B) % 2).astype(np.uint8)
+    env.reset(mask=torch.from_numpy(mask))
+    ora.reset(mask=mask)
+    for k in range(2 * T + 1):
+        a = rng.integers(0, 3, (B, S)).astype(np.int64)
+        obs, rew, done, info = env.step(torch.from_numpy(a))
+        oo, ro, do, _ = ora.step(a)
+        np.testing.assert_array_equal(rew.cpu().numpy(), ro)
+        np.testing.assert_array_equal(done.cpu().numpy(), do.astype(bool))
+        if "terminal_obs" in info:
+            np.testing.assert_array_equal(info["terminal_obs"].cpu().numpy(), oo)
+        if do.any():
+            oo = ora.reset(mask=do, obs=oo)
+        np.testing.assert_array_equal(obs.cpu().numpy(), oo, err_msg=f"step {k}")
+        ln, rt = ora.episode_stats()
+        np.testing.assert_array_equal(info["episode_length"].cpu().numpy()[do == 0], ln[do == 0])
+
+
+def test_vec_actions_any_dtype_and_device():
+    from marllb_amd import VecLoadBalanceEnv
+    B, S = 64, 4
+    envs = [VecLoadBalanceEnv(B, S, device="cuda:0", seed=5, autoreset=False) for _ in range(3)]
+    for e in envs:
+        e.reset()
+    a = np.random.default_rng(0).integers(0, 3, (B, S))
+    o1 = envs[0].step(a.astype(np.int64))[0]
+    o2 = envs[1].step(torch.from_numpy(a.astype(np.int32)).cuda())[0]
+    o3 = envs[2].step(a.tolist())[0]
+    assert torch.equal(o1, o2) and torch.equal(o1, o3)
+
+
+def test_vec_state_snapshot_roundtrip():
+    from marllb_amd import VecLoadBalanceEnv
+    B, S = 50, 8
+    e = VecLoadBalanceEnv(B, S, device="cuda:0", seed=11, autoreset=False)
+    e.reset()
+    a = torch.ones((B, S), dtype=torch.int64)
+    e.step(a)
+    snap = e.get_state()
+    r1 = [e.step(a)[0].clone() for _ in range(3)]
+    e.set_state(snap)
+    r2 = [e.step(a)[0].clone() for _ in range(3)]
+    assert all(torch.equal(x, y) for x, y in zip(r1, r2))
