@@ -28,6 +28,8 @@ constexpr int NF = 11;   // observation columns (env.py:46-48)
 constexpr int MAX_S = 16;
 constexpr int32_t kLastNone = -(1 << 30);
 constexpr int kModeStep = 0;
+// s_waitcnt immediate with vmcnt = 0 and expcnt/lgkmcnt left at their maxima (gfx9 encoding).
+constexpr int kWaitVmcnt0 = 0x0F70;
 constexpr int kModeReset = 1;
 
 struct DevState {
@@ -80,11 +82,20 @@ struct SimParams {
 
 // ================================================================ dynamics (one lane = one env)
 
+// Register window: the first W entries of each server's FIFO live in VGPRs, so the event loop
+// reads no memory (a load there forces s_waitcnt vmcnt(0) behind every outstanding store, which
+// at one wave per SIMD serialises the loop on memory latency).  The ring in HBM stays canonical
+// (write-through on push); an entry is loaded only when a queue longer than W advances.
+template <int MAXS>
+struct Win {
+  static constexpr int W = MAXS <= 4 ? 4 : (MAXS <= 8 ? 3 : 2);
+};
+
 template <int MAXS>
 struct LaneState {
+  static constexpr int W = Win<MAXS>::W;
   int32_t cnt[MAXS], head[MAXS];
-  int32_t head_tc[MAXS], head_ta[MAXS];  // entry at the ring head (valid if cnt >= 1)
-  int32_t nxt_tc[MAXS], nxt_ta[MAXS];    // entry after the head, prefetched (valid if cnt >= 2)
+  int32_t wtc[MAXS][W], wta[MAXS][W];  // queue entries 0..W-1 {t_complete, t_arrival}
   int32_t tail_tc[MAXS], last_tc[MAXS];
   uint32_t rcnt[MAXS];
   int32_t assigned[MAXS];
@@ -102,7 +113,7 @@ __device__ __forceinline__ float policy_score(int policy, int32_t cnt, double de
   return (float)((double)(cnt + 1) / den);
 }
 
-// Arrival draw for arrival index `idx`: gap to it, its work, its two hash words.
+// Arrival draw for one arrival index: gap to it, its work, its two hash words.
 __device__ __forceinline__ void arrival_from_draw(const SimParams& p, const u32x4& d,
                                                   int32_t t_prev, int32_t& next_arr,
                                                   float& work, uint32_t& u2, uint32_t& u3) {
@@ -121,6 +132,36 @@ __device__ __forceinline__ void draw_arrival(const SimParams& p, LaneState<MAXS>
   arrival_from_draw(p, d, t_prev, L.next_arr, L.next_work, L.u2, L.u3);
 }
 
+template <int MAXS>
+__device__ __forceinline__ void load_window(const DevState& st, const SimParams& p,
+                                            LaneState<MAXS>& L, size_t b) {
+  constexpr int W = LaneState<MAXS>::W;
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) {
+#pragma unroll
+    for (int i = 0; i < W; ++i) { L.wtc[s][i] = 0; L.wta[s][i] = 0; }
+    L.tail_tc[s] = 0;
+    if (s < p.S) {
+      const size_t sb = b * (size_t)p.S + (size_t)s;
+#pragma unroll
+      for (int i = 0; i < W; ++i) {
+        if (i < L.cnt[s]) {
+          int pos = L.head[s] + i;
+          if (pos >= p.Q) pos -= p.Q;
+          const int2 e = st.ring[sb * p.Q + pos];
+          L.wtc[s][i] = e.x;
+          L.wta[s][i] = e.y;
+        }
+      }
+      if (L.cnt[s] > 0) {
+        int tp = L.head[s] + L.cnt[s] - 1;
+        if (tp >= p.Q) tp -= p.Q;
+        L.tail_tc[s] = st.ring[sb * p.Q + tp].x;
+      }
+    }
+  }
+}
+
 // One simulated step of dt_us with server weights w[] (env.py:230-259 with real dynamics).
 //
 // Event loop, one event per iteration per lane: the earliest pending completion (if it is due no
@@ -128,11 +169,12 @@ __device__ __forceinline__ void draw_arrival(const SimParams& p, LaneState<MAXS>
 // arrival.  Both event kinds need exactly one Philox block (Algorithm R draw / next-arrival
 // draw), computed unconditionally so the 64 lanes stay converged through the expensive part.
 // Per server the completions are processed in t_complete order before any arrival at the same
-// or a later time, which is the order the oracle (server by server) produces, so every
-// reservoir sees the same insert sequence and the state is bit-identical.
+// or a later time — the order the oracle (server by server) produces — so every reservoir sees
+// the same insert sequence and the state is bit-identical.
 template <int MAXS>
 __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
                                          LaneState<MAXS>& L, size_t b, const float* w) {
+  constexpr int W = LaneState<MAXS>::W;
   const int S = p.S, Q = p.Q;
   const int32_t dt = p.dt_us;
   const uint64_t base_us = (uint64_t)L.clock * (uint64_t)dt;
@@ -149,7 +191,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     int smin = -1;
 #pragma unroll
     for (int s = 0; s < MAXS; ++s)
-      if (s < S && L.cnt[s] > 0 && L.head_tc[s] < tmin) { tmin = L.head_tc[s]; smin = s; }
+      if (s < S && L.cnt[s] > 0 && L.wtc[s][0] < tmin) { tmin = L.wtc[s][0]; smin = s; }
     const bool arrival_due = L.next_arr < dt;
     const int32_t horizon = arrival_due ? L.next_arr : dt;
     const bool completion = smin >= 0 && tmin <= horizon;
@@ -171,7 +213,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
       for (int s = 0; s < MAXS; ++s) {
         if (s == smin) {
           const size_t sbase = b * (size_t)S + (size_t)s;
-          const int32_t tc = L.head_tc[s], ta = L.head_ta[s];
+          const int32_t tc = L.wtc[s][0], ta = L.wta[s][0];
           const int32_t start = ta > L.last_tc[s] ? ta : L.last_tc[s];
           const float fct = (float)(tc - ta) * 1.0e-6f;
           const float dur = (float)(tc - start) * 1.0e-6f;
@@ -199,14 +241,17 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
           if (h == Q) h = 0;
           L.head[s] = h;
           L.cnt[s] -= 1;
-          L.head_tc[s] = L.nxt_tc[s];
-          L.head_ta[s] = L.nxt_ta[s];
-          if (L.cnt[s] >= 2) {  // prefetch the entry after the new head
-            int h2 = h + 1;
-            if (h2 == Q) h2 = 0;
-            const int2 e = st.ring[sbase * Q + h2];
-            L.nxt_tc[s] = e.x;
-            L.nxt_ta[s] = e.y;
+#pragma unroll
+          for (int i = 0; i + 1 < W; ++i) { L.wtc[s][i] = L.wtc[s][i + 1]; L.wta[s][i] = L.wta[s][i + 1]; }
+          if (L.cnt[s] >= W) {  // rare: the queue is longer than the window, refill its last slot
+            int pw = h + W - 1;
+            if (pw >= Q) pw -= Q;
+            const int2 e = st.ring[sbase * Q + pw];
+            // drain here, in the rare branch, so no load is pending at the loop back-edge
+            // (otherwise every iteration's header copies wait on vmcnt(0))
+            __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+            L.wtc[s][W - 1] = e.x;
+            L.wta[s][W - 1] = e.y;
           }
           L.score[s] = policy_score(p.policy, L.cnt[s], L.den[s]);
         }
@@ -254,9 +299,10 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
             const int32_t tc = start + svc;
             int pos = L.head[s] + L.cnt[s];
             if (pos >= Q) pos -= Q;
-            st.ring[sbase * Q + pos] = make_int2(tc, ta);
-            if (L.cnt[s] == 0) { L.head_tc[s] = tc; L.head_ta[s] = ta; }
-            else if (L.cnt[s] == 1) { L.nxt_tc[s] = tc; L.nxt_ta[s] = ta; }
+            st.ring[sbase * Q + pos] = make_int2(tc, ta);  // write-through, fire and forget
+#pragma unroll
+            for (int i = 0; i < W; ++i)
+              if (i == L.cnt[s]) { L.wtc[s][i] = tc; L.wta[s][i] = ta; }
             L.cnt[s] += 1;
             L.tail_tc[s] = tc;
             L.assigned[s] += 1;
@@ -269,29 +315,50 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     }
   }
 
-  // ---- rebase relative times to the next step's start
+  // ---- rebase relative times to the next step's start: the window in registers, the ring
+  //      entries beyond it read-modify-written (queues longer than W only)
   L.next_arr -= dt;
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) {
     if (s < S) {
+#pragma unroll
+      for (int i = 0; i < W; ++i) { L.wtc[s][i] -= dt; L.wta[s][i] -= dt; }
       const size_t sbase = b * (size_t)S + (size_t)s;
-      int pos = L.head[s];
-      for (int i = 0; i < L.cnt[s]; ++i) {
+      int pos = L.head[s] + W;
+      if (pos >= Q) pos -= Q;
+      for (int i = W; i < L.cnt[s]; ++i) {
         int2 e = st.ring[sbase * Q + pos];
         e.x -= dt;
         e.y -= dt;
         st.ring[sbase * Q + pos] = e;
         pos = (pos + 1 == Q) ? 0 : pos + 1;
       }
-      L.head_tc[s] -= dt;
-      L.head_ta[s] -= dt;
-      L.nxt_tc[s] -= dt;
-      L.nxt_ta[s] -= dt;
       L.tail_tc[s] -= dt;
       L.last_tc[s] = (L.last_tc[s] < kLastNone + dt) ? kLastNone : L.last_tc[s] - dt;
     }
   }
   L.clock += 1u;
+}
+
+// Write the (rebased) window back to the ring at kernel exit so HBM holds the canonical queue.
+template <int MAXS>
+__device__ __forceinline__ void store_window(const DevState& st, const SimParams& p,
+                                             const LaneState<MAXS>& L, size_t b) {
+  constexpr int W = LaneState<MAXS>::W;
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) {
+    if (s < p.S) {
+      const size_t sb = b * (size_t)p.S + (size_t)s;
+#pragma unroll
+      for (int i = 0; i < W; ++i) {
+        if (i < L.cnt[s]) {
+          int pos = L.head[s] + i;
+          if (pos >= p.Q) pos -= p.Q;
+          st.ring[sb * p.Q + pos] = make_int2(L.wtc[s][i], L.wta[s][i]);
+        }
+      }
+    }
+  }
 }
 
 __device__ __forceinline__ float action_weight(const SimParams& p, const void* action, int dtype,
@@ -330,8 +397,9 @@ __global__ void __launch_bounds__(64)
     draw_arrival<MAXS>(p, L, 0);
 #pragma unroll
     for (int s = 0; s < MAXS; ++s) {
-      L.cnt[s] = 0; L.head[s] = 0; L.head_tc[s] = 0; L.head_ta[s] = 0; L.tail_tc[s] = 0;
-      L.nxt_tc[s] = 0; L.nxt_ta[s] = 0;
+      L.cnt[s] = 0; L.head[s] = 0; L.tail_tc[s] = 0;
+#pragma unroll
+      for (int i = 0; i < LaneState<MAXS>::W; ++i) { L.wtc[s][i] = 0; L.wta[s][i] = 0; }
       L.last_tc[s] = kLastNone; L.rcnt[s] = 0u; L.assigned[s] = 0;
     }
     float w1[MAXS];
@@ -359,25 +427,11 @@ __global__ void __launch_bounds__(64)
         L.last_tc[s] = st.last_tc[sb];
         L.rcnt[s] = st.res_count[sb];
         L.assigned[s] = 0;
-        L.head_tc[s] = 0; L.head_ta[s] = 0; L.tail_tc[s] = 0;
-        L.nxt_tc[s] = 0; L.nxt_ta[s] = 0;
-        if (L.cnt[s] > 0) {
-          const int2 e = st.ring[sb * p.Q + L.head[s]];
-          L.head_tc[s] = e.x;
-          L.head_ta[s] = e.y;
-          int tp = L.head[s] + L.cnt[s] - 1;
-          if (tp >= p.Q) tp -= p.Q;
-          L.tail_tc[s] = st.ring[sb * p.Q + tp].x;
-        }
-        if (L.cnt[s] > 1) {
-          int h2 = L.head[s] + 1;
-          if (h2 >= p.Q) h2 -= p.Q;
-          const int2 e = st.ring[sb * p.Q + h2];
-          L.nxt_tc[s] = e.x;
-          L.nxt_ta[s] = e.y;
-        }
+      } else {
+        L.head[s] = 0; L.cnt[s] = 0; L.last_tc[s] = kLastNone; L.rcnt[s] = 0u; L.assigned[s] = 0;
       }
     }
+    load_window<MAXS>(st, p, L, b);
     float w[MAXS];
 #pragma unroll
     for (int s = 0; s < MAXS; ++s)
@@ -389,6 +443,7 @@ __global__ void __launch_bounds__(64)
         if (s < S) assign_out[b * (size_t)S + (size_t)s] = L.assigned[s];
     }
   }
+  store_window<MAXS>(st, p, L, b);
   st.episode[b] = L.episode;
   st.clock[b] = L.clock;
   st.dropped[b] = L.dropped;
