@@ -166,11 +166,13 @@ __device__ __forceinline__ void load_window(const DevState& st, const SimParams&
 //
 // Event loop, one event per iteration per lane: the earliest pending completion (if it is due no
 // later than the next arrival, or than the step end when no arrival is due) or else the next
-// arrival.  Both event kinds need exactly one Philox block (Algorithm R draw / next-arrival
-// draw), computed unconditionally so the 64 lanes stay converged through the expensive part.
-// Per server the completions are processed in t_complete order before any arrival at the same
-// or a later time — the order the oracle (server by server) produces — so every reservoir sees
-// the same insert sequence and the state is bit-identical.
+// arrival.  The body is straight-line and predicated: both event kinds are evaluated by every
+// lane, per-server state is updated through selects, and only the small stores are masked.  This
+// keeps the 64 lanes (64 envs) converged; a branchy body gets structurised by the compiler into
+// nested per-event-kind loops in which lanes wait for each other.  Per server the completions are
+// processed in t_complete order before any arrival at the same or a later time — the order the
+// oracle (server by server) produces — so every reservoir sees the same insert sequence and the
+// state is bit-identical.
 template <int MAXS>
 __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
                                          LaneState<MAXS>& L, size_t b, const float* w) {
@@ -178,6 +180,8 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
   const int S = p.S, Q = p.Q;
   const int32_t dt = p.dt_us;
   const uint64_t base_us = (uint64_t)L.clock * (uint64_t)dt;
+  const bool two_choice = (p.policy == 1 || p.policy == 3);
+  const size_t b0 = b * (size_t)S;
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) {
     if (s < S) {
@@ -186,133 +190,172 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     }
   }
   for (;;) {
-    // earliest pending completion (ties: lowest server index)
+    // ---- which event: earliest completion (ties: lowest server) vs next arrival
     int32_t tmin = 0x7FFFFFFF;
     int smin = -1;
 #pragma unroll
-    for (int s = 0; s < MAXS; ++s)
-      if (s < S && L.cnt[s] > 0 && L.wtc[s][0] < tmin) { tmin = L.wtc[s][0]; smin = s; }
+    for (int s = 0; s < MAXS; ++s) {
+      const bool c = s < S && L.cnt[s] > 0 && L.wtc[s][0] < tmin;
+      tmin = c ? L.wtc[s][0] : tmin;
+      smin = c ? s : smin;
+    }
     const bool arrival_due = L.next_arr < dt;
     const int32_t horizon = arrival_due ? L.next_arr : dt;
-    const bool completion = smin >= 0 && tmin <= horizon;
-    if (!completion && !arrival_due) break;
+    const bool comp = smin >= 0 && tmin <= horizon;
+    const bool arr = !comp && arrival_due;
+    if (!comp && !arr) break;
 
-    // the one Philox block of this event
+    // ---- gathers for the completing server
     uint32_t cres = 0;
+    int32_t h_ta = 0, h_last = 0, h_cnt = 0, h_head = 0;
 #pragma unroll
-    for (int s = 0; s < MAXS; ++s)
-      if (s == smin) cres = L.rcnt[s];
-    const u32x4 ctr = completion
+    for (int s = 0; s < MAXS; ++s) {
+      const bool m = s == smin;
+      cres = m ? L.rcnt[s] : cres;
+      h_ta = m ? L.wta[s][0] : h_ta;
+      h_last = m ? L.last_tc[s] : h_last;
+      h_cnt = m ? L.cnt[s] : h_cnt;
+      h_head = m ? L.head[s] : h_head;
+    }
+
+    // ---- the one Philox block of this event (Algorithm R draw, or the next arrival's draw)
+    const u32x4 ctr = comp
         ? u32x4{cres >> 1, L.gid, L.episode, (kStreamReservoir << 24) | (uint32_t)smin}
         : u32x4{L.arr_idx + 1u, L.gid, L.episode, kStreamArrival << 24};
     const u32x4 d = philox4x32_10(ctr, p.key0, p.key1);
 
-    if (completion) {
-      // ---- completion of the head flow of server smin (lbhash.h:116-124, 131-135)
+    // ---- completion (lbhash.h:116-124, 131-135) + Algorithm R (reservoir.py:64-85)
+    const int32_t tc = tmin;
+    const int32_t start_c = h_ta > h_last ? h_ta : h_last;
+    int slot;
+    {
+      const uint32_t hi = (cres & 1u) ? d.w : d.y;
+      const uint32_t lo = (cres & 1u) ? d.z : d.x;
+      const uint64_t j = mulhi64_by_u33(hi, lo, (uint64_t)cres + 1u);
+      slot = cres < (uint32_t)K ? (int)cres : (j < (uint64_t)K ? (int)j : -1);
+    }
+    if (comp && slot >= 0) {
+      const size_t r = (b0 + (size_t)smin) * K + (size_t)slot;
+      st.res_fct[r] = (float)(tc - h_ta) * 1.0e-6f;
+      st.res_dur[r] = (float)(tc - start_c) * 1.0e-6f;
+      st.res_ts[r] = (uint32_t)((base_us + (uint64_t)(int64_t)tc) / 1000u);
+    }
+    const int h_next = (h_head + 1 == Q) ? 0 : h_head + 1;
+
+    // ---- arrival: choose a server (node.c:388-441); full servers are not eligible
+    const int32_t ta = L.next_arr;
+    int chosen = -1;
+    if (two_choice) {  // SED2 / LSQ2: two uniform candidates, keep the second if strictly better
+      const int h1 = (int)(((uint64_t)L.u2 * (uint64_t)S) >> 32);
+      const int h2 = (int)(((uint64_t)L.u3 * (uint64_t)S) >> 32);
+      float s1 = 0.f, s2 = 0.f;
+      bool ok1 = false, ok2 = false;
 #pragma unroll
       for (int s = 0; s < MAXS; ++s) {
-        if (s == smin) {
-          const size_t sbase = b * (size_t)S + (size_t)s;
-          const int32_t tc = L.wtc[s][0], ta = L.wta[s][0];
-          const int32_t start = ta > L.last_tc[s] ? ta : L.last_tc[s];
-          const float fct = (float)(tc - ta) * 1.0e-6f;
-          const float dur = (float)(tc - start) * 1.0e-6f;
-          L.last_tc[s] = tc;
-          const uint32_t ts_ms = (uint32_t)((base_us + (uint64_t)(int64_t)tc) / 1000u);
-          // Algorithm R (reservoir.py:64-85): slot c while filling, else j = randint(0, c+1)
-          const uint32_t c = L.rcnt[s];
-          int slot;
-          if (c < (uint32_t)K) {
-            slot = (int)c;
-          } else {
-            const uint32_t hi = (c & 1u) ? d.w : d.y;
-            const uint32_t lo = (c & 1u) ? d.z : d.x;
-            const uint64_t j = mulhi64_by_u33(hi, lo, (uint64_t)c + 1u);
-            slot = j < (uint64_t)K ? (int)j : -1;
-          }
-          if (slot >= 0) {
-            const size_t r = sbase * K + (size_t)slot;
-            st.res_fct[r] = fct;
-            st.res_dur[r] = dur;
-            st.res_ts[r] = ts_ms;
-          }
-          if (c != 0xFFFFFFFFu) L.rcnt[s] = c + 1u;
-          int h = L.head[s] + 1;
-          if (h == Q) h = 0;
-          L.head[s] = h;
-          L.cnt[s] -= 1;
-#pragma unroll
-          for (int i = 0; i + 1 < W; ++i) { L.wtc[s][i] = L.wtc[s][i + 1]; L.wta[s][i] = L.wta[s][i + 1]; }
-          if (L.cnt[s] >= W) {  // rare: the queue is longer than the window, refill its last slot
-            int pw = h + W - 1;
-            if (pw >= Q) pw -= Q;
-            const int2 e = st.ring[sbase * Q + pw];
-            // drain here, in the rare branch, so no load is pending at the loop back-edge
-            // (otherwise every iteration's header copies wait on vmcnt(0))
-            __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
-            L.wtc[s][W - 1] = e.x;
-            L.wta[s][W - 1] = e.y;
-          }
-          L.score[s] = policy_score(p.policy, L.cnt[s], L.den[s]);
-        }
+        s1 = (s == h1) ? L.score[s] : s1;
+        ok1 = (s == h1) ? (L.cnt[s] < Q) : ok1;
+        s2 = (s == h2) ? L.score[s] : s2;
+        ok2 = (s == h2) ? (L.cnt[s] < Q) : ok2;
       }
-    } else {
-      // ---- arrival at next_arr: choose a server (node.c:388-441); full servers ineligible
-      const int32_t ta = L.next_arr;
-      int chosen = -1;
-      if (p.policy == 1 || p.policy == 3) {  // SED2 / LSQ2: two uniform candidates
-        const int h1 = (int)(((uint64_t)L.u2 * (uint64_t)S) >> 32);
-        const int h2 = (int)(((uint64_t)L.u3 * (uint64_t)S) >> 32);
-        float s1 = 0.f, s2 = 0.f;
-        bool ok1 = false, ok2 = false;
+      chosen = (ok1 && ok2) ? ((s2 < s1) ? h2 : h1) : (ok1 ? h1 : (ok2 ? h2 : -1));
+    } else {  // SED / LSQ: start at the hashed server, replace on strictly lower score
+      const int h = (int)(((uint64_t)L.u2 * (uint64_t)S) >> 32);
+      float best = 0.f;
 #pragma unroll
-        for (int s = 0; s < MAXS; ++s) {
-          if (s == h1) { s1 = L.score[s]; ok1 = L.cnt[s] < Q; }
-          if (s == h2) { s2 = L.score[s]; ok2 = L.cnt[s] < Q; }
-        }
-        if (ok1 && ok2) chosen = (s2 < s1) ? h2 : h1;
-        else if (ok1) chosen = h1;
-        else if (ok2) chosen = h2;
-      } else {  // SED / LSQ: start at the hashed server, strict '<' scan in index order
-        const int h = (int)(((uint64_t)L.u2 * (uint64_t)S) >> 32);
-        float best = 0.f;
-#pragma unroll
-        for (int s = 0; s < MAXS; ++s)
-          if (s == h && L.cnt[s] < Q) { chosen = s; best = L.score[s]; }
-#pragma unroll
-        for (int s = 0; s < MAXS; ++s) {
-          if (s < S && L.cnt[s] < Q) {
-            if (chosen < 0 || L.score[s] < best) { chosen = s; best = L.score[s]; }
-          }
-        }
+      for (int s = 0; s < MAXS; ++s) {
+        const bool m = s == h && L.cnt[s] < Q;
+        chosen = m ? s : chosen;
+        best = m ? L.score[s] : best;
       }
-      if (chosen < 0) {
-        L.dropped += 1u;
-      } else {
 #pragma unroll
-        for (int s = 0; s < MAXS; ++s) {
-          if (s == chosen) {  // FIFO service: start when the server's last queued flow ends
-            const size_t sbase = b * (size_t)S + (size_t)s;
-            const int32_t start = L.cnt[s] > 0 ? (L.tail_tc[s] > ta ? L.tail_tc[s] : ta) : ta;
-            int32_t svc = (int32_t)(L.next_work * p.svc_scale[s]);
-            if (svc < 1) svc = 1;
-            const int32_t tc = start + svc;
-            int pos = L.head[s] + L.cnt[s];
-            if (pos >= Q) pos -= Q;
-            st.ring[sbase * Q + pos] = make_int2(tc, ta);  // write-through, fire and forget
-#pragma unroll
-            for (int i = 0; i < W; ++i)
-              if (i == L.cnt[s]) { L.wtc[s][i] = tc; L.wta[s][i] = ta; }
-            L.cnt[s] += 1;
-            L.tail_tc[s] = tc;
-            L.assigned[s] += 1;
-            L.score[s] = policy_score(p.policy, L.cnt[s], L.den[s]);
-          }
-        }
+      for (int s = 0; s < MAXS; ++s) {
+        const bool m = s < S && L.cnt[s] < Q && (chosen < 0 || L.score[s] < best);
+        chosen = m ? s : chosen;
+        best = m ? L.score[s] : best;
       }
-      L.arr_idx += 1u;
-      arrival_from_draw(p, d, ta, L.next_arr, L.next_work, L.u2, L.u3);
     }
+    const bool push = arr && chosen >= 0;
+    L.dropped += (arr && chosen < 0) ? 1u : 0u;
+    int32_t a_cnt = 0, a_head = 0, a_tail = 0;
+    float a_scale = 0.f;
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) {
+      const bool m = s == chosen;
+      a_cnt = m ? L.cnt[s] : a_cnt;
+      a_head = m ? L.head[s] : a_head;
+      a_tail = m ? L.tail_tc[s] : a_tail;
+      a_scale = m ? p.svc_scale[s] : a_scale;
+    }
+    // FIFO service: start when the server's last queued flow ends
+    const int32_t start_a = a_cnt > 0 ? (a_tail > ta ? a_tail : ta) : ta;
+    int32_t svc = (int32_t)(L.next_work * a_scale);
+    svc = svc < 1 ? 1 : svc;
+    const int32_t tc_a = start_a + svc;
+    if (push) {
+      int pos = a_head + a_cnt;
+      pos = pos >= Q ? pos - Q : pos;
+      st.ring[(b0 + (size_t)chosen) * Q + pos] = make_int2(tc_a, ta);  // write-through
+    }
+
+    // ---- per-server state through selects (at most one server changes per event)
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) {
+      const bool pc = comp && s == smin;
+      const bool pa = push && s == chosen;
+      L.rcnt[s] = (pc && cres != 0xFFFFFFFFu) ? cres + 1u : L.rcnt[s];
+      L.last_tc[s] = pc ? tc : L.last_tc[s];
+      L.head[s] = pc ? h_next : L.head[s];
+#pragma unroll
+      for (int i = 0; i + 1 < W; ++i) {
+        L.wtc[s][i] = pc ? L.wtc[s][i + 1] : L.wtc[s][i];
+        L.wta[s][i] = pc ? L.wta[s][i + 1] : L.wta[s][i];
+      }
+#pragma unroll
+      for (int i = 0; i < W; ++i) {
+        const bool ins = pa && L.cnt[s] == i;
+        L.wtc[s][i] = ins ? tc_a : L.wtc[s][i];
+        L.wta[s][i] = ins ? ta : L.wta[s][i];
+      }
+      L.cnt[s] += (pa ? 1 : 0) - (pc ? 1 : 0);
+      L.tail_tc[s] = pa ? tc_a : L.tail_tc[s];
+      L.assigned[s] += pa ? 1 : 0;
+    }
+    // rare: a queue longer than the window advanced, refill the window's last slot
+    if (comp && h_cnt - 1 >= W) {
+      int pw = h_next + W - 1;
+      pw = pw >= Q ? pw - Q : pw;
+      const int2 e = st.ring[(b0 + (size_t)smin) * Q + pw];
+      // drain here, in the rare branch, so no load is pending at the loop back-edge
+      __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+#pragma unroll
+      for (int s = 0; s < MAXS; ++s) {
+        L.wtc[s][W - 1] = (s == smin) ? e.x : L.wtc[s][W - 1];
+        L.wta[s][W - 1] = (s == smin) ? e.y : L.wta[s][W - 1];
+      }
+    }
+    // score of the one server whose count changed
+    const int cs = comp ? smin : (push ? chosen : -1);
+    int32_t n_cs = 0;
+    double den_cs = 1.0;
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) {
+      n_cs = (s == cs) ? L.cnt[s] : n_cs;
+      den_cs = (s == cs) ? L.den[s] : den_cs;
+    }
+    const float sc_new = policy_score(p.policy, n_cs, den_cs);
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) L.score[s] = (s == cs) ? sc_new : L.score[s];
+
+    // ---- next arrival (draw d belongs to arrival index arr_idx + 1)
+    int32_t na;
+    float nw;
+    uint32_t nu2, nu3;
+    arrival_from_draw(p, d, ta, na, nw, nu2, nu3);
+    L.next_arr = arr ? na : L.next_arr;
+    L.next_work = arr ? nw : L.next_work;
+    L.u2 = arr ? nu2 : L.u2;
+    L.u3 = arr ? nu3 : L.u3;
+    L.arr_idx += arr ? 1u : 0u;
   }
 
   // ---- rebase relative times to the next step's start: the window in registers, the ring
@@ -323,7 +366,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     if (s < S) {
 #pragma unroll
       for (int i = 0; i < W; ++i) { L.wtc[s][i] -= dt; L.wta[s][i] -= dt; }
-      const size_t sbase = b * (size_t)S + (size_t)s;
+      const size_t sbase = b0 + (size_t)s;
       int pos = L.head[s] + W;
       if (pos >= Q) pos -= Q;
       for (int i = W; i < L.cnt[s]; ++i) {
