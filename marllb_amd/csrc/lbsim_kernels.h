@@ -82,20 +82,23 @@ struct SimParams {
 
 // ================================================================ dynamics (one lane = one env)
 
-// Register window: the first W entries of each server's FIFO live in VGPRs, so the event loop
-// reads no memory (a load there forces s_waitcnt vmcnt(0) behind every outstanding store, which
-// at one wave per SIMD serialises the loop on memory latency).  The ring in HBM stays canonical
-// (write-through on push); an entry is loaded only when a queue longer than W advances.
+// Queue window in LDS: the first WL entries of each server's FIFO live in LDS, laid out
+// [server][slot][lane] so a wave's 64 per-lane ds_read_b64 of one (server, slot) pair are
+// conflict-free whatever slot each lane is at.  The event loop then reads no global memory (a
+// global load there forces s_waitcnt vmcnt(0) behind every outstanding store, which at one wave
+// per SIMD serialises the loop on memory latency).  The ring in HBM stays canonical
+// (write-through on push, window written back at kernel exit); an entry is loaded from HBM only
+// when a queue longer than WL advances.
 template <int MAXS>
 struct Win {
-  static constexpr int W = MAXS <= 4 ? 4 : (MAXS <= 8 ? 3 : 2);
+  static constexpr int WL = MAXS <= 8 ? 8 : 4;
 };
 
 template <int MAXS>
 struct LaneState {
-  static constexpr int W = Win<MAXS>::W;
-  int32_t cnt[MAXS], head[MAXS];
-  int32_t wtc[MAXS][W], wta[MAXS][W];  // queue entries 0..W-1 {t_complete, t_arrival}
+  static constexpr int WL = Win<MAXS>::WL;
+  int32_t cnt[MAXS], head[MAXS], lh[MAXS];  // queue length, ring head, LDS window head
+  int32_t head_tc[MAXS];                      // t_complete of the head flow (valid if cnt > 0)
   int32_t tail_tc[MAXS], last_tc[MAXS];
   uint32_t rcnt[MAXS];
   int32_t assigned[MAXS];
@@ -106,6 +109,12 @@ struct LaneState {
   uint32_t u2, u3, arr_idx, episode, clock, dropped;
   uint32_t gid;
 };
+
+// LDS window slot (server s, slot i) of this lane.
+template <int MAXS>
+__device__ __forceinline__ int2* qslot(int2* q, int s, int i, int lane) {
+  return q + ((s * Win<MAXS>::WL + i) * 64 + lane);
+}
 
 // SED score (n_flow_on + 1) / (1e-9 + w) in double, stored as f32 (node.c:393-399); LSQ: n.
 __device__ __forceinline__ float policy_score(int policy, int32_t cnt, double den) {
@@ -132,31 +141,28 @@ __device__ __forceinline__ void draw_arrival(const SimParams& p, LaneState<MAXS>
   arrival_from_draw(p, d, t_prev, L.next_arr, L.next_work, L.u2, L.u3);
 }
 
+// Kernel entry: the first WL entries of every queue from the HBM ring into the LDS window.
 template <int MAXS>
 __device__ __forceinline__ void load_window(const DevState& st, const SimParams& p,
-                                            LaneState<MAXS>& L, size_t b) {
-  constexpr int W = LaneState<MAXS>::W;
+                                            LaneState<MAXS>& L, size_t b, int2* q, int lane) {
+  constexpr int WL = LaneState<MAXS>::WL;
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) {
-#pragma unroll
-    for (int i = 0; i < W; ++i) { L.wtc[s][i] = 0; L.wta[s][i] = 0; }
+    L.lh[s] = 0;
+    L.head_tc[s] = 0;
     L.tail_tc[s] = 0;
     if (s < p.S) {
       const size_t sb = b * (size_t)p.S + (size_t)s;
-#pragma unroll
-      for (int i = 0; i < W; ++i) {
-        if (i < L.cnt[s]) {
-          int pos = L.head[s] + i;
-          if (pos >= p.Q) pos -= p.Q;
-          const int2 e = st.ring[sb * p.Q + pos];
-          L.wtc[s][i] = e.x;
-          L.wta[s][i] = e.y;
-        }
+      for (int i = 0; i < WL && i < L.cnt[s]; ++i) {
+        int pos = L.head[s] + i;
+        if (pos >= p.Q) pos -= p.Q;
+        *qslot<MAXS>(q, s, i, lane) = st.ring[sb * p.Q + pos];
       }
       if (L.cnt[s] > 0) {
         int tp = L.head[s] + L.cnt[s] - 1;
         if (tp >= p.Q) tp -= p.Q;
         L.tail_tc[s] = st.ring[sb * p.Q + tp].x;
+        L.head_tc[s] = st.ring[sb * p.Q + L.head[s]].x;
       }
     }
   }
@@ -167,7 +173,7 @@ __device__ __forceinline__ void load_window(const DevState& st, const SimParams&
 // Event loop, one event per iteration per lane: the earliest pending completion (if it is due no
 // later than the next arrival, or than the step end when no arrival is due) or else the next
 // arrival.  The body is straight-line and predicated: both event kinds are evaluated by every
-// lane, per-server state is updated through selects, and only the small stores are masked.  This
+// lane, per-server scalars are updated through selects, only the small stores are masked.  This
 // keeps the 64 lanes (64 envs) converged; a branchy body gets structurised by the compiler into
 // nested per-event-kind loops in which lanes wait for each other.  Per server the completions are
 // processed in t_complete order before any arrival at the same or a later time — the order the
@@ -175,8 +181,9 @@ __device__ __forceinline__ void load_window(const DevState& st, const SimParams&
 // state is bit-identical.
 template <int MAXS>
 __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
-                                         LaneState<MAXS>& L, size_t b, const float* w) {
-  constexpr int W = LaneState<MAXS>::W;
+                                         LaneState<MAXS>& L, size_t b, const float* w, int2* q,
+                                         int lane) {
+  constexpr int WL = LaneState<MAXS>::WL;
   const int S = p.S, Q = p.Q;
   const int32_t dt = p.dt_us;
   const uint64_t base_us = (uint64_t)L.clock * (uint64_t)dt;
@@ -195,8 +202,8 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     int smin = -1;
 #pragma unroll
     for (int s = 0; s < MAXS; ++s) {
-      const bool c = s < S && L.cnt[s] > 0 && L.wtc[s][0] < tmin;
-      tmin = c ? L.wtc[s][0] : tmin;
+      const bool c = s < S && L.cnt[s] > 0 && L.head_tc[s] < tmin;
+      tmin = c ? L.head_tc[s] : tmin;
       smin = c ? s : smin;
     }
     const bool arrival_due = L.next_arr < dt;
@@ -207,16 +214,28 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
 
     // ---- gathers for the completing server
     uint32_t cres = 0;
-    int32_t h_ta = 0, h_last = 0, h_cnt = 0, h_head = 0;
+    int32_t h_last = 0, h_cnt = 0, h_head = 0, h_lh = 0;
 #pragma unroll
     for (int s = 0; s < MAXS; ++s) {
       const bool m = s == smin;
       cres = m ? L.rcnt[s] : cres;
-      h_ta = m ? L.wta[s][0] : h_ta;
       h_last = m ? L.last_tc[s] : h_last;
       h_cnt = m ? L.cnt[s] : h_cnt;
       h_head = m ? L.head[s] : h_head;
+      h_lh = m ? L.lh[s] : h_lh;
     }
+    const int ss = smin < 0 ? 0 : smin;
+    const int32_t h_ta = qslot<MAXS>(q, ss, h_lh, lane)->y;  // arrival time of the head flow
+    const int h_next = (h_head + 1 == Q) ? 0 : h_head + 1;
+    const int lh_next = (h_lh + 1 == WL) ? 0 : h_lh + 1;
+    // rare: the queue is longer than the window; bring entry WL-1 (after this pop) into LDS
+    if (comp && h_cnt - 1 >= WL) {
+      int pw = h_next + WL - 1;
+      pw = pw >= Q ? pw - Q : pw;
+      *qslot<MAXS>(q, ss, h_lh, lane) = st.ring[(b0 + (size_t)ss) * Q + pw];  // slot lh+WL-1 == lh
+      __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);  // drain in the rare branch, not at the back-edge
+    }
+    const int32_t nxt_tc = qslot<MAXS>(q, ss, lh_next, lane)->x;  // next head (valid if cnt > 1)
 
     // ---- the one Philox block of this event (Algorithm R draw, or the next arrival's draw)
     const u32x4 ctr = comp
@@ -240,7 +259,6 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
       st.res_dur[r] = (float)(tc - start_c) * 1.0e-6f;
       st.res_ts[r] = (uint32_t)((base_us + (uint64_t)(int64_t)tc) / 1000u);
     }
-    const int h_next = (h_head + 1 == Q) ? 0 : h_head + 1;
 
     // ---- arrival: choose a server (node.c:388-441); full servers are not eligible
     const int32_t ta = L.next_arr;
@@ -276,7 +294,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     }
     const bool push = arr && chosen >= 0;
     L.dropped += (arr && chosen < 0) ? 1u : 0u;
-    int32_t a_cnt = 0, a_head = 0, a_tail = 0;
+    int32_t a_cnt = 0, a_head = 0, a_tail = 0, a_lh = 0;
     float a_scale = 0.f;
 #pragma unroll
     for (int s = 0; s < MAXS; ++s) {
@@ -284,6 +302,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
       a_cnt = m ? L.cnt[s] : a_cnt;
       a_head = m ? L.head[s] : a_head;
       a_tail = m ? L.tail_tc[s] : a_tail;
+      a_lh = m ? L.lh[s] : a_lh;
       a_scale = m ? p.svc_scale[s] : a_scale;
     }
     // FIFO service: start when the server's last queued flow ends
@@ -294,10 +313,22 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     if (push) {
       int pos = a_head + a_cnt;
       pos = pos >= Q ? pos - Q : pos;
-      st.ring[(b0 + (size_t)chosen) * Q + pos] = make_int2(tc_a, ta);  // write-through
+      const int2 e = make_int2(tc_a, ta);
+      st.ring[(b0 + (size_t)chosen) * Q + pos] = e;  // write-through
+      if (a_cnt < WL) {
+        int li = a_lh + a_cnt;
+        li = li >= WL ? li - WL : li;
+        *qslot<MAXS>(q, chosen, li, lane) = e;
+      }
     }
 
-    // ---- per-server state through selects (at most one server changes per event)
+    // ---- per-server scalars through selects (at most one server changes per event)
+    const int cs = comp ? smin : (push ? chosen : -1);
+    const int32_t n_cs = comp ? h_cnt - 1 : a_cnt + 1;
+    double den_cs = 1.0;
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) den_cs = (s == cs) ? L.den[s] : den_cs;
+    const float sc_new = policy_score(p.policy, n_cs, den_cs);
 #pragma unroll
     for (int s = 0; s < MAXS; ++s) {
       const bool pc = comp && s == smin;
@@ -305,46 +336,13 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
       L.rcnt[s] = (pc && cres != 0xFFFFFFFFu) ? cres + 1u : L.rcnt[s];
       L.last_tc[s] = pc ? tc : L.last_tc[s];
       L.head[s] = pc ? h_next : L.head[s];
-#pragma unroll
-      for (int i = 0; i + 1 < W; ++i) {
-        L.wtc[s][i] = pc ? L.wtc[s][i + 1] : L.wtc[s][i];
-        L.wta[s][i] = pc ? L.wta[s][i + 1] : L.wta[s][i];
-      }
-#pragma unroll
-      for (int i = 0; i < W; ++i) {
-        const bool ins = pa && L.cnt[s] == i;
-        L.wtc[s][i] = ins ? tc_a : L.wtc[s][i];
-        L.wta[s][i] = ins ? ta : L.wta[s][i];
-      }
-      L.cnt[s] += (pa ? 1 : 0) - (pc ? 1 : 0);
+      L.lh[s] = pc ? lh_next : L.lh[s];
+      L.head_tc[s] = pc ? nxt_tc : ((pa && a_cnt == 0) ? tc_a : L.head_tc[s]);
+      L.cnt[s] = (s == cs) ? n_cs : L.cnt[s];
       L.tail_tc[s] = pa ? tc_a : L.tail_tc[s];
       L.assigned[s] += pa ? 1 : 0;
+      L.score[s] = (s == cs) ? sc_new : L.score[s];
     }
-    // rare: a queue longer than the window advanced, refill the window's last slot
-    if (comp && h_cnt - 1 >= W) {
-      int pw = h_next + W - 1;
-      pw = pw >= Q ? pw - Q : pw;
-      const int2 e = st.ring[(b0 + (size_t)smin) * Q + pw];
-      // drain here, in the rare branch, so no load is pending at the loop back-edge
-      __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
-#pragma unroll
-      for (int s = 0; s < MAXS; ++s) {
-        L.wtc[s][W - 1] = (s == smin) ? e.x : L.wtc[s][W - 1];
-        L.wta[s][W - 1] = (s == smin) ? e.y : L.wta[s][W - 1];
-      }
-    }
-    // score of the one server whose count changed
-    const int cs = comp ? smin : (push ? chosen : -1);
-    int32_t n_cs = 0;
-    double den_cs = 1.0;
-#pragma unroll
-    for (int s = 0; s < MAXS; ++s) {
-      n_cs = (s == cs) ? L.cnt[s] : n_cs;
-      den_cs = (s == cs) ? L.den[s] : den_cs;
-    }
-    const float sc_new = policy_score(p.policy, n_cs, den_cs);
-#pragma unroll
-    for (int s = 0; s < MAXS; ++s) L.score[s] = (s == cs) ? sc_new : L.score[s];
 
     // ---- next arrival (draw d belongs to arrival index arr_idx + 1)
     int32_t na;
@@ -358,24 +356,30 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     L.arr_idx += arr ? 1u : 0u;
   }
 
-  // ---- rebase relative times to the next step's start: the window in registers, the ring
-  //      entries beyond it read-modify-written (queues longer than W only)
+  // ---- rebase relative times to the next step's start: the LDS window in place, the HBM ring
+  //      entries beyond it read-modify-written (queues longer than WL only)
   L.next_arr -= dt;
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) {
     if (s < S) {
-#pragma unroll
-      for (int i = 0; i < W; ++i) { L.wtc[s][i] -= dt; L.wta[s][i] -= dt; }
+      for (int i = 0; i < WL && i < L.cnt[s]; ++i) {
+        int li = L.lh[s] + i;
+        li = li >= WL ? li - WL : li;
+        int2* e = qslot<MAXS>(q, s, li, lane);
+        e->x -= dt;
+        e->y -= dt;
+      }
       const size_t sbase = b0 + (size_t)s;
-      int pos = L.head[s] + W;
+      int pos = L.head[s] + WL;
       if (pos >= Q) pos -= Q;
-      for (int i = W; i < L.cnt[s]; ++i) {
+      for (int i = WL; i < L.cnt[s]; ++i) {
         int2 e = st.ring[sbase * Q + pos];
         e.x -= dt;
         e.y -= dt;
         st.ring[sbase * Q + pos] = e;
         pos = (pos + 1 == Q) ? 0 : pos + 1;
       }
+      L.head_tc[s] -= dt;
       L.tail_tc[s] -= dt;
       L.last_tc[s] = (L.last_tc[s] < kLastNone + dt) ? kLastNone : L.last_tc[s] - dt;
     }
@@ -383,22 +387,22 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
   L.clock += 1u;
 }
 
-// Write the (rebased) window back to the ring at kernel exit so HBM holds the canonical queue.
+// Kernel exit: write the (rebased) LDS window back to the ring so HBM holds the canonical queue.
 template <int MAXS>
 __device__ __forceinline__ void store_window(const DevState& st, const SimParams& p,
-                                             const LaneState<MAXS>& L, size_t b) {
-  constexpr int W = LaneState<MAXS>::W;
+                                             const LaneState<MAXS>& L, size_t b, int2* q,
+                                             int lane) {
+  constexpr int WL = LaneState<MAXS>::WL;
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) {
     if (s < p.S) {
       const size_t sb = b * (size_t)p.S + (size_t)s;
-#pragma unroll
-      for (int i = 0; i < W; ++i) {
-        if (i < L.cnt[s]) {
-          int pos = L.head[s] + i;
-          if (pos >= p.Q) pos -= p.Q;
-          st.ring[sb * p.Q + pos] = make_int2(L.wtc[s][i], L.wta[s][i]);
-        }
+      for (int i = 0; i < WL && i < L.cnt[s]; ++i) {
+        int pos = L.head[s] + i;
+        if (pos >= p.Q) pos -= p.Q;
+        int li = L.lh[s] + i;
+        li = li >= WL ? li - WL : li;
+        st.ring[sb * p.Q + pos] = *qslot<MAXS>(q, s, li, lane);
       }
     }
   }
@@ -426,6 +430,8 @@ __global__ void __launch_bounds__(64)
                     int32_t* assign_out, const uint8_t* reset_mask) {
   constexpr int mode = MODE;
   const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x;
+  __shared__ int2 qwin[MAXS * Win<MAXS>::WL * 64];
   if (b >= (size_t)p.B) return;
   const int S = p.S;
   LaneState<MAXS> L;
@@ -440,15 +446,13 @@ __global__ void __launch_bounds__(64)
     draw_arrival<MAXS>(p, L, 0);
 #pragma unroll
     for (int s = 0; s < MAXS; ++s) {
-      L.cnt[s] = 0; L.head[s] = 0; L.tail_tc[s] = 0;
-#pragma unroll
-      for (int i = 0; i < LaneState<MAXS>::W; ++i) { L.wtc[s][i] = 0; L.wta[s][i] = 0; }
+      L.cnt[s] = 0; L.head[s] = 0; L.lh[s] = 0; L.head_tc[s] = 0; L.tail_tc[s] = 0;
       L.last_tc[s] = kLastNone; L.rcnt[s] = 0u; L.assigned[s] = 0;
     }
     float w1[MAXS];
 #pragma unroll
     for (int s = 0; s < MAXS; ++s) w1[s] = 1.0f;
-    for (int k = 0; k < p.warmup_steps; ++k) sim_step<MAXS>(st, p, L, b, w1);
+    for (int k = 0; k < p.warmup_steps; ++k) sim_step<MAXS>(st, p, L, b, w1, qwin, lane);
     st.ep_step[b] = 0;
     st.ep_return[b] = 0.0;
   } else {
@@ -474,19 +478,19 @@ __global__ void __launch_bounds__(64)
         L.head[s] = 0; L.cnt[s] = 0; L.last_tc[s] = kLastNone; L.rcnt[s] = 0u; L.assigned[s] = 0;
       }
     }
-    load_window<MAXS>(st, p, L, b);
+    load_window<MAXS>(st, p, L, b, qwin, lane);
     float w[MAXS];
 #pragma unroll
     for (int s = 0; s < MAXS; ++s)
       w[s] = (s < S) ? action_weight(p, action, action_dtype, b * (size_t)S + (size_t)s) : 1.0f;
-    sim_step<MAXS>(st, p, L, b, w);
+    sim_step<MAXS>(st, p, L, b, w, qwin, lane);
     if (assign_out != nullptr) {
 #pragma unroll
       for (int s = 0; s < MAXS; ++s)
         if (s < S) assign_out[b * (size_t)S + (size_t)s] = L.assigned[s];
     }
   }
-  store_window<MAXS>(st, p, L, b);
+  store_window<MAXS>(st, p, L, b, qwin, lane);
   st.episode[b] = L.episode;
   st.clock[b] = L.clock;
   st.dropped[b] = L.dropped;
