@@ -227,14 +227,22 @@ int launch_dynamics(lbsim_t* h, const void* action, int dtype, int32_t* assign,
   return launch_check(h, "dynamics_kernel");
 }
 
+template <int MODE>
+void launch_observe_t(lbsim_t* h, const ObsOutputs& o, const uint8_t* mask, hipStream_t stream) {
+  const dim3 grid((unsigned)h->B), block(64);
+  if (h->S <= 4)
+    hipLaunchKernelGGL((observe_kernel<4, MODE>), grid, block, 0, stream, h->st, h->prm, o, mask);
+  else if (h->S <= 8)
+    hipLaunchKernelGGL((observe_kernel<8, MODE>), grid, block, 0, stream, h->st, h->prm, o, mask);
+  else
+    hipLaunchKernelGGL((observe_kernel<16, MODE>), grid, block, 0, stream, h->st, h->prm, o, mask);
+}
+
 int launch_observe(lbsim_t* h, const ObsOutputs& o, const uint8_t* mask, int mode,
                    hipStream_t stream) {
   ProfScope ps(h, stream, mode == kModeStep ? 1 : 3);
-  const dim3 grid((unsigned)h->B), block(64);
-  if (mode == kModeStep)
-    hipLaunchKernelGGL(observe_kernel<kModeStep>, grid, block, 0, stream, h->st, h->prm, o, mask);
-  else
-    hipLaunchKernelGGL(observe_kernel<kModeReset>, grid, block, 0, stream, h->st, h->prm, o, mask);
+  if (mode == kModeStep) launch_observe_t<kModeStep>(h, o, mask, stream);
+  else launch_observe_t<kModeReset>(h, o, mask, stream);
   return launch_check(h, "observe_kernel");
 }
 
@@ -430,8 +438,8 @@ int lbsim_reservoir_features(const float* values, const uint32_t* ts_ms, const u
   if (!(decay_factor > 0.0f) || !(decay_factor < 1.0f)) return LBSIM_EINVAL;
   if (n == 0) return LBSIM_OK;
   const float c = (float)(std::log2((double)decay_factor) / 1000.0);
-  hipLaunchKernelGGL(features_kernel, dim3((unsigned)n), dim3(64), 0, (hipStream_t)stream, values,
-                     ts_ms, counts, c, feats_out);
+  hipLaunchKernelGGL(features_kernel, dim3((unsigned)((n + 3) / 4)), dim3(64), 0,
+                     (hipStream_t)stream, values, ts_ms, counts, n, c, feats_out);
   return hipGetLastError() == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
 }
 

@@ -534,277 +534,329 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   return v;
 }
 
-// Bitonic sort of 128 (key, payload) pairs; element i = lane + 64*h lives in (k[h], v[h]).
-// Equal keys never swap, so the network is a deterministic permutation on every backend.
-__device__ __forceinline__ void bitonic128(uint32_t (&k)[2], uint32_t (&v)[2], int lane) {
+// numpy pairwise summation (numpy/_core/src/umath/loops_utils.h.src, n <= 128) by a group of 8
+// lanes (j = lane & 7): n < 8 -> sequential sum from 0; else 8 strided accumulators r[j] (same
+// per-accumulator order as numpy's unrolled loop), combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7))
+// by three xor-shuffles (IEEE addition is commutative, so every lane of the group gets the same
+// bits), then the n % 8 tail in order.  `term(i)` returns element i.
+template <typename T, typename F>
+__device__ __forceinline__ T pairwise8(int n, int j, F term) {
+  if (n < 8) {
+    T r = (T)0;
+    for (int i = 0; i < n; ++i) r += term(i);
+    return r;
+  }
+  const int m8 = n - (n % 8);
+  T acc = term(j);
+  for (int i = 8 + j; i < m8; i += 8) acc += term(i);
+  T t = acc + (T)__shfl_xor(acc, 1, 64);
+  t = t + (T)__shfl_xor(t, 2, 64);
+  t = t + (T)__shfl_xor(t, 4, 64);
+  for (int i = m8; i < n; ++i) t += term(i);
+  return t;
+}
+
+// ================================================================ features of one env
+
+// LDS image of one env's reservoirs during observe (one wave per env, 64-thread blocks).
+template <int MAXS>
+struct ObsScratch {
+  uint32_t vals[2 * MAXS][K];  // reservoir r = 2s (fct) / 2s+1 (duration), slot order; then sorted
+  float wts[MAXS][K];          // decay weights of server s (shared by its two reservoirs)
+  int n[2 * MAXS];             // valid slots per reservoir
+  float mean[2 * MAXS], sd[2 * MAXS], md[2 * MAXS], p90[2 * MAXS], p90d[2 * MAXS];
+  double swt[MAXS], svw[2 * MAXS];
+  float obs[MAXS * NF];
+};
+
+// Sort 128 (key, payload) pairs held by the 8 lanes of a group, 16 per lane: sorted index
+// i = 16 * t + e (t = lane & 7, e = register).  Bitonic network; stages with partner distance
+// < 16 stay in registers (22 of 28), the rest exchange with lane t ^ (j / 16) by xor-shuffle.
+// Equal keys never swap, so the network is a deterministic permutation.
+__device__ __forceinline__ void bitonic128_g8(uint32_t (&key)[16], uint32_t (&pay)[16], int t) {
 #pragma unroll
-  for (int kk = 2; kk <= 128; kk <<= 1) {
+  for (int k = 2; k <= 128; k <<= 1) {
 #pragma unroll
-    for (int j = kk >> 1; j > 0; j >>= 1) {
-      if (j == 64) {  // only at kk == 128: ascending, partner in the same lane
-        if (k[0] > k[1]) {
-          const uint32_t tk = k[0], tv = v[0];
-          k[0] = k[1]; v[0] = v[1];
-          k[1] = tk; v[1] = tv;
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j < 16) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int f = e ^ j;
+          if (f > e) {
+            // ascending iff ((16t + e) & k) == 0
+            const bool up = (k < 16) ? ((e & k) == 0) : ((t & (k >> 4)) == 0);
+            const bool sw = up ? (key[e] > key[f]) : (key[e] < key[f]);
+            const uint32_t k0 = key[e], k1 = key[f], p0 = pay[e], p1 = pay[f];
+            key[e] = sw ? k1 : k0;
+            key[f] = sw ? k0 : k1;
+            pay[e] = sw ? p1 : p0;
+            pay[f] = sw ? p0 : p1;
+          }
         }
       } else {
+        const int lj = j >> 4;  // lane distance 1, 2 or 4
+        const bool lower = (t & lj) == 0;
+        const bool up = (t & (k >> 4)) == 0;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int i = lane + 64 * h;
-          const uint32_t pk = shfl_xor_u32(k[h], j);
-          const uint32_t pv = shfl_xor_u32(v[h], j);
-          const bool up = (i & kk) == 0;
-          const bool lower = (i & j) == 0;
-          const bool take = (lower == up) ? (pk < k[h]) : (pk > k[h]);
-          if (take) { k[h] = pk; v[h] = pv; }
+        for (int e = 0; e < 16; ++e) {
+          const uint32_t pk = shfl_xor_u32(key[e], lj);
+          const uint32_t pp = shfl_xor_u32(pay[e], lj);
+          const bool take = (lower == up) ? (pk < key[e]) : (pk > key[e]);
+          key[e] = take ? pk : key[e];
+          pay[e] = take ? pp : pay[e];
         }
       }
     }
   }
 }
 
-// Inclusive wave scan of a u64 held as (hi, lo).
-__device__ __forceinline__ uint64_t wave_scan_u64(uint64_t x, int lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t lo = shfl_up_u32((uint32_t)x, d);
-    const uint32_t hi = shfl_up_u32((uint32_t)(x >> 32), d);
-    if (lane >= d) x += ((uint64_t)hi << 32) | lo;
-  }
-  return x;
-}
-
-// numpy pairwise summation (numpy/_core/src/umath/loops_utils.h.src, n <= 128): for n < 8 a
-// sequential sum from 0; else 8 strided accumulators, combined ((r0+r1)+(r2+r3))+((r4+r5)+
-// (r6+r7)), then the n % 8 tail added in order.  A group of 8 lanes (j = lane & 7) evaluates one
-// sum; `term(i)` gives element i.  Every lane of the group returns the same bits.
-template <typename T, typename F>
-__device__ __forceinline__ T pairwise_group(int n, int lane, F term) {
-  if (n < 8) {
-    T r = (T)0;
-    for (int i = 0; i < n; ++i) r += term(i);
-    return r;
-  }
-  const int j = lane & 7, g0 = lane & ~7;
-  const int m8 = n - (n % 8);
-  T acc = term(j);
-  for (int i = 8 + j; i < m8; i += 8) acc += term(i);
-  T r[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) r[q] = __shfl(acc, g0 + q, 64);
-  T res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-  for (int i = m8; i < n; ++i) res += term(i);
-  return res;
-}
-
-// ================================================================ features of one server
-
-struct FeatScratch {
-  float v[2][K];    // fct, duration values by slot
-  float w[K];       // decay weight by slot (f32)
-  uint64_t wq[K];   // decay weight in 2^-48 fixed point (exact, order-free sums)
-};
-
-// Features of the two reservoirs (fct, duration) of one server that share their timestamps.
-// n = min(count, K).  out[r][0..4] = {mean, p90, std, mean_decay, p90_decay}  (reservoir.py:105-
-// 196 with numpy 2 float32 semantics; decay weights relative to the newest sample).
-__device__ __forceinline__ void server_features(const float* __restrict__ v0, const float* __restrict__ v1,
-                                const uint32_t* __restrict__ ts, uint32_t count, float decay_c,
-                                FeatScratch& sc, float (&out)[2][5], int lane) {
-  const int n = count < (uint32_t)K ? (int)count : K;
-  if (n == 0) {
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-      for (int f = 0; f < 5; ++f) out[r][f] = 0.0f;
-    return;
-  }
-  float a[2][2];
-  uint32_t t[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int slot = lane + 64 * h;
-    const bool valid = slot < n;
-    a[0][h] = valid ? v0[slot] : 0.0f;
-    a[1][h] = valid ? v1[slot] : 0.0f;
-    t[h] = valid ? ts[slot] : 0u;
-  }
-  const uint32_t newest = wave_max_u32(t[0] > t[1] ? t[0] : t[1]);
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int slot = lane + 64 * h;
-    const bool valid = slot < n;
-    const float w = valid ? lb_exp2f((float)(newest - t[h]) * decay_c) : 0.0f;
-    sc.v[0][slot] = a[0][h];
-    sc.v[1][slot] = a[1][h];
-    sc.w[slot] = w;
-    sc.wq[slot] = (uint64_t)(w * 281474976710656.0f);  // * 2^48, exact scaling
-  }
-  __syncthreads();
-
-  // ---- mean (f32 pairwise) of fct (lanes 0-7) and duration (lanes 8-15)
-  const int grp = lane >> 3;
-  const float* arr = sc.v[grp & 1];
-  const float sum32 = pairwise_group<float>(n, lane, [&](int i) { return arr[i]; });
-  const float fn = (float)n;
-  const float mean_g = sum32 / fn;
-  float mean[2];
-  mean[0] = __shfl(mean_g, 0, 64);
-  mean[1] = __shfl(mean_g, 8, 64);
-  // ---- std: sqrt(pairwise((x - mean)^2) / n) in f32 (np.std, ddof 0)
-  const float mg = mean[grp & 1];
-  const float ss32 = pairwise_group<float>(n, lane, [&](int i) {
-    const float d = arr[i] - mg;
-    return d * d;
-  });
-  const float sd_g = sqrtf(ss32 / fn);
-  float sd[2];
-  sd[0] = __shfl(sd_g, 0, 64);
-  sd[1] = __shfl(sd_g, 8, 64);
-  // ---- decay-weighted mean in f64: pairwise(v*w) / pairwise(w) (np.average, weights f64)
-  //      lanes 0-7: sum w; 8-15: sum fct*w; 16-23: sum dur*w
-  const int g3 = grp < 3 ? grp : 2;
-  const float* arr3 = sc.v[g3 == 2 ? 1 : 0];
-  const double sum64 = pairwise_group<double>(n, lane, [&](int i) {
-    const double x = (g3 == 0) ? 1.0 : (double)arr3[i];
-    return x * (double)sc.w[i];
-  });
-  const double sw = __shfl(sum64, 0, 64);
-  float md[2];
-  md[0] = (float)(__shfl(sum64, 8, 64) / sw);
-  md[1] = (float)(__shfl(sum64, 16, 64) / sw);
-
-  // ---- order statistics: sort each reservoir, p90 (linear) and decay-weighted p90
-  const float q = 0.9f;
-  const float hidx = (float)(n - 1) * q;  // numpy 2: (n - 1) * float32(90 / 100)
-  const float fl = floorf(hidx);
-  const int lo = (int)fl;
-  const float g = hidx - fl;
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    uint32_t key[2], pay[2];
+// The 11-column observation of one env (features.py:256-286) into sc.obs, S servers.
+// Slot-order sums follow numpy exactly (reservoir.py:143-155); order statistics come from the
+// sorted keys (reservoir.py:144, 165-196).  All values >= 0, so float bits order like floats.
+template <int MAXS>
+__device__ __forceinline__ void observe_env(const DevState& st, const SimParams& p, size_t b,
+                                            ObsScratch<MAXS>& sc, int lane) {
+  const int S = p.S;
+  const int R = 2 * S;
+  const int g = lane >> 3, j = lane & 7;
+  // ---- phase 1: reservoirs into LDS, decay weights relative to each server's newest sample
+  for (int s = 0; s < S; ++s) {
+    const size_t sb = b * (size_t)S + (size_t)s;
+    const uint32_t rc = st.res_count[sb];
+    const int n = rc < (uint32_t)K ? (int)rc : K;
+    uint32_t f[2], d[2], t[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int slot = lane + 64 * h;
-      key[h] = slot < n ? as_u32(a[r][h]) : 0xFFFFFFFFu;  // values >= 0: bits are monotone
-      pay[h] = (uint32_t)slot;
+      const bool v = slot < n;
+      f[h] = v ? __float_as_uint(st.res_fct[sb * K + slot]) : 0u;
+      d[h] = v ? __float_as_uint(st.res_dur[sb * K + slot]) : 0u;
+      t[h] = v ? st.res_ts[sb * K + slot] : 0u;
     }
-    bitonic128(key, pay, lane);
-    const float va = as_f32(readlane_u32(lo >= 64 ? key[1] : key[0], lo & 63));
-    const int lo1 = (lo + 1 < n) ? lo + 1 : lo;
-    const float vb = as_f32(readlane_u32(lo1 >= 64 ? key[1] : key[0], lo1 & 63));
-    const float diff = vb - va;
-    const float p90 = (g >= 0.5f) ? (vb - diff * (1.0f - g)) : (va + diff * g);
-
-    // cumulative fixed-point weight in sorted order; first position with cum >= 0.9 * total
-    const uint64_t c0 = wave_scan_u64(sc.wq[pay[0]], lane);
-    const uint64_t t0 = ((uint64_t)readlane_u32((uint32_t)(c0 >> 32), 63) << 32) |
-                        readlane_u32((uint32_t)c0, 63);
-    const uint64_t c1 = wave_scan_u64(sc.wq[pay[1]], lane) + t0;
-    const uint64_t total = ((uint64_t)readlane_u32((uint32_t)(c1 >> 32), 63) << 32) |
-                           readlane_u32((uint32_t)c1, 63);
-    const uint64_t cut9 = total * 9u;
-    const uint64_t m0 = __ballot(c0 * 10u >= cut9);
-    const uint64_t m1 = __ballot(c1 * 10u >= cut9);
-    const int idx = m0 ? __builtin_ctzll(m0) : 64 + __builtin_ctzll(m1);
-    const float p90d = as_f32(readlane_u32(idx >= 64 ? key[1] : key[0], idx & 63));
-
-    out[r][0] = mean[r];
-    out[r][1] = p90;
-    out[r][2] = sd[r];
-    out[r][3] = md[r];
-    out[r][4] = p90d;
+    const uint32_t newest = wave_max_u32(t[0] > t[1] ? t[0] : t[1]);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int slot = lane + 64 * h;
+      sc.vals[2 * s][slot] = f[h];
+      sc.vals[2 * s + 1][slot] = d[h];
+      sc.wts[s][slot] = slot < n ? lb_exp2f((float)(newest - t[h]) * p.decay_c) : 0.0f;
+    }
+    if (lane == 0) {
+      sc.n[2 * s] = n;
+      sc.n[2 * s + 1] = n;
+    }
   }
-  __syncthreads();  // scratch is reused by the next server
+  __syncthreads();
+
+  // ---- phase 2: numpy-order sums, one job per 8-lane group
+  for (int job0 = 0; job0 < R; job0 += 8) {  // float32 means
+    const int r = job0 + g;
+    const int n = r < R ? sc.n[r] : 0;
+    const uint32_t* a = sc.vals[r < R ? r : 0];
+    const float sum = pairwise8<float>(n, j, [&](int i) { return __uint_as_float(a[i]); });
+    if (j == 0 && r < R) sc.mean[r] = n > 0 ? sum / (float)n : 0.0f;
+  }
+  for (int job0 = 0; job0 < 3 * S; job0 += 8) {  // float64 sum w (S jobs), sum v*w (R jobs)
+    const int q = job0 + g;
+    const bool wonly = q < S;
+    const int r = wonly ? 0 : q - S;
+    const int ws = wonly ? q : (r >> 1);
+    const int n = q < 3 * S ? sc.n[wonly ? 2 * q : r] : 0;
+    const uint32_t* a = sc.vals[r < R ? r : 0];
+    const float* w = sc.wts[ws < S ? ws : 0];
+    const double sum = pairwise8<double>(n, j, [&](int i) {
+      const double x = wonly ? 1.0 : (double)__uint_as_float(a[i]);
+      return x * (double)w[i];
+    });
+    if (j == 0 && q < 3 * S) {
+      if (wonly) sc.swt[q] = sum;
+      else sc.svw[r] = sum;
+    }
+  }
+  __syncthreads();
+  for (int job0 = 0; job0 < R; job0 += 8) {  // float32 sum (v - mean)^2
+    const int r = job0 + g;
+    const int n = r < R ? sc.n[r] : 0;
+    const uint32_t* a = sc.vals[r < R ? r : 0];
+    const float m = r < R ? sc.mean[r] : 0.0f;
+    const float ss = pairwise8<float>(n, j, [&](int i) {
+      const float dv = __uint_as_float(a[i]) - m;
+      return dv * dv;
+    });
+    if (j == 0 && r < R) {
+      sc.sd[r] = n > 0 ? sqrtf(ss / (float)n) : 0.0f;
+      sc.md[r] = n > 0 ? (float)(sc.svw[r] / sc.swt[r >> 1]) : 0.0f;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 3: order statistics, 8 reservoirs per pass (one per 8-lane group)
+  for (int r0 = 0; r0 < R; r0 += 8) {
+    const int r = r0 + g;
+    const bool act = r < R;
+    const int rr = act ? r : 0;
+    const int n = act ? sc.n[r] : 0;
+    uint32_t key[16], pay[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int slot = 16 * j + e;
+      const bool v = slot < n;
+      key[e] = v ? sc.vals[rr][slot] : 0xFFFFFFFFu;
+      pay[e] = v ? __float_as_uint(sc.wts[rr >> 1][slot]) : 0u;
+    }
+    bitonic128_g8(key, pay, j);
+    // decay-weighted p90: cumulative 2^-48 fixed-point weight in sorted order, first position
+    // with 10 * cum >= 9 * total (searchsorted 'left' of 0.9 * cumsum[-1])
+    uint64_t incl[16];
+    uint64_t run = 0;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      run += (uint64_t)(__uint_as_float(pay[e]) * 281474976710656.0f);
+      incl[e] = run;
+    }
+    uint64_t excl = 0;  // sum of the totals of lanes t' < t of this group (exact integers)
+#pragma unroll
+    for (int dd = 1; dd < 8; dd <<= 1) {
+      const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)(run + excl), (unsigned)dd, 8);
+      const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)((run + excl) >> 32), (unsigned)dd, 8);
+      if (j >= dd) excl += ((uint64_t)hi << 32) | lo;
+    }
+    // (the loop above is an inclusive scan of lane totals written as run + excl; excl now holds
+    //  the exclusive prefix)
+    const uint64_t tot_incl = run + excl;
+    const uint32_t tlo = (uint32_t)__shfl((int)(uint32_t)tot_incl, (lane & ~7) | 7, 64);
+    const uint32_t thi = (uint32_t)__shfl((int)(uint32_t)(tot_incl >> 32), (lane & ~7) | 7, 64);
+    const uint64_t cut9 = (((uint64_t)thi << 32) | tlo) * 9u;
+    int fe = 16;
+#pragma unroll
+    for (int e = 15; e >= 0; --e) fe = ((excl + incl[e]) * 10u >= cut9) ? e : fe;
+    const uint64_t m = __ballot(fe < 16);
+    const uint32_t gm = (uint32_t)(m >> (lane & ~7)) & 0xFFu;
+    const int tstar = gm ? __builtin_ctz(gm) : 7;
+    const int fstar = __shfl(fe, (lane & ~7) | tstar, 64);
+    const int pd = 16 * tstar + (fstar < 16 ? fstar : 15);
+    // sorted keys back into LDS (slot-order values are no longer needed)
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+      if (act) sc.vals[rr][16 * j + e] = key[e];
+    __syncthreads();
+    if (j == 0 && act) {
+      float p90 = 0.0f, p90d = 0.0f;
+      if (n > 0) {
+        // numpy 2 'linear' (float32): virtual index (n - 1) * float32(0.9), _lerp
+        const float hidx = (float)(n - 1) * 0.9f;
+        const float fl = floorf(hidx);
+        const int lo = (int)fl;
+        const float gg = hidx - fl;
+        const float va = __uint_as_float(sc.vals[r][lo]);
+        const float vb = __uint_as_float(sc.vals[r][lo + 1 < n ? lo + 1 : lo]);
+        const float diff = vb - va;
+        p90 = (gg >= 0.5f) ? (vb - diff * (1.0f - gg)) : (va + diff * gg);
+        p90d = __uint_as_float(sc.vals[r][pd]);
+      }
+      sc.p90[r] = p90;
+      sc.p90d[r] = p90d;
+    }
+    __syncthreads();
+  }
+
+  // ---- observation rows: [n_flow_on, fct x5, duration x5]
+  for (int e = lane; e < S * NF; e += 64) {
+    const int s = e / NF, c = e - s * NF;
+    float v;
+    if (c == 0) {
+      v = (float)(st.hc[b * (size_t)S + (size_t)s] >> 16);
+    } else {
+      const int r = 2 * s + (c >= 6 ? 1 : 0);
+      const int f = (c - 1) % 5;
+      v = f == 0 ? sc.mean[r] : f == 1 ? sc.p90[r] : f == 2 ? sc.sd[r] : f == 3 ? sc.md[r] : sc.p90d[r];
+    }
+    sc.obs[e] = v;
+  }
+  __syncthreads();
 }
 
 // ================================================================ reward (rewards.py)
 
-// numpy pairwise sum of a small f64 array (n <= 16) in one thread.
-__device__ __forceinline__ double pw_sum64(const double* x, int n) {
+// numpy pairwise sum of n <= 16 float64 terms in one thread (term(i) = element i).
+template <typename F>
+__device__ __forceinline__ double pw_sum64(int n, F term) {
   if (n < 8) {
     double r = 0.0;
-    for (int i = 0; i < n; ++i) r += x[i];
+    for (int i = 0; i < n; ++i) r += term(i);
     return r;
   }
-  double r[8];
-  for (int q = 0; q < 8; ++q) r[q] = x[q];
+  double r0 = term(0), r1 = term(1), r2 = term(2), r3 = term(3);
+  double r4 = term(4), r5 = term(5), r6 = term(6), r7 = term(7);
   const int m8 = n - (n % 8);
-  for (int i = 8; i < m8; i += 8)
-    for (int q = 0; q < 8; ++q) r[q] += x[i + q];
-  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-  for (int i = m8; i < n; ++i) res += x[i];
+  for (int i = 8; i < m8; i += 8) {
+    r0 += term(i); r1 += term(i + 1); r2 += term(i + 2); r3 += term(i + 3);
+    r4 += term(i + 4); r5 += term(i + 5); r6 += term(i + 6); r7 += term(i + 7);
+  }
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (int i = m8; i < n; ++i) res += term(i);
   return res;
 }
 
-__device__ __forceinline__ double np_var64(const double* x, int n) {
-  const double mean = pw_sum64(x, n) / (double)n;
-  double d[MAX_S];
-  for (int i = 0; i < n; ++i) {
-    const double t = x[i] - mean;
-    d[i] = t * t;
-  }
-  return pw_sum64(d, n) / (double)n;
-}
-
 // RewardFunction.compute on one (S, 11) observation (rewards.py:329-381): values of the active
-// servers (any column > 0, env.py:410-413) at column `field`, metric in float64.
+// servers (any column > 0, env.py:410-413) at column `field`, metric in float64.  The active
+// servers' indices are packed into a 64-bit nibble list so no runtime-indexed local array (and
+// hence no scratch memory) is needed.
 __device__ double reward_of(const float* obs, int S, int metric, int field) {
   if (field < 0 || field >= NF) return 0.0;
-  double x[MAX_S];
+  uint64_t ids = 0;
   int n = 0;
   for (int s = 0; s < S; ++s) {
     bool active = false;
     for (int f = 0; f < NF; ++f) active |= obs[s * NF + f] > 0.0f;
-    if (active) x[n++] = (double)obs[s * NF + field];
+    if (active) { ids |= (uint64_t)s << (4 * n); ++n; }
   }
   if (n == 0) return 0.0;
+  auto x = [&](int i) { return (double)obs[(int)((ids >> (4 * i)) & 15u) * NF + field]; };
   const double eps = 1e-10;
+  auto var = [&]() {
+    const double mean = pw_sum64(n, x) / (double)n;
+    return pw_sum64(n, [&](int i) { const double t = x(i) - mean; return t * t; }) / (double)n;
+  };
   switch (metric) {
     case 0: {  // jain_fairness 21-67
-      const double sv = pw_sum64(x, n);
+      const double sv = pw_sum64(n, x);
       if (sv < eps) return 1.0;
-      double x2[MAX_S];
-      for (int i = 0; i < n; ++i) x2[i] = x[i] * x[i];
-      const double sq = pw_sum64(x2, n);
+      const double sq = pw_sum64(n, [&](int i) { const double v = x(i); return v * v; });
       if (sq < eps) return 1.0;
       const double j = (sv * sv) / ((double)n * sq);
       const double lo = 1.0 / (double)n;
       return j < lo ? lo : (j > 1.0 ? 1.0 : j);
     }
-    case 1: return -np_var64(x, n);        // variance_fairness 70-94
-    case 2: return -sqrt(np_var64(x, n));  // std_fairness 97-114
-    case 3: {                              // coefficient_of_variation 117-144
-      const double mean = pw_sum64(x, n) / (double)n;
+    case 1: return -var();        // variance_fairness 70-94
+    case 2: return -sqrt(var());  // std_fairness 97-114
+    case 3: {                     // coefficient_of_variation 117-144
+      const double mean = pw_sum64(n, x) / (double)n;
       if (mean < eps) return 0.0;
-      return -(sqrt(np_var64(x, n)) / (mean + eps));
+      return -(sqrt(var()) / (mean + eps));
     }
     case 4: {  // max_min_fairness 147-171
-      double m = x[0];
-      for (int i = 1; i < n; ++i) m = x[i] > m ? x[i] : m;
+      double m = x(0);
+      for (int i = 1; i < n; ++i) m = x(i) > m ? x(i) : m;
       return -m;
     }
     case 5: {  // min_max_fairness 174-191
-      double m = x[0];
-      for (int i = 1; i < n; ++i) m = x[i] < m ? x[i] : m;
+      double m = x(0);
+      for (int i = 1; i < n; ++i) m = x(i) < m ? x(i) : m;
       return m;
     }
-    case 6: {  // product_fairness 194-225
-      double l[MAX_S];
-      for (int i = 0; i < n; ++i) l[i] = log(x[i] + eps);
-      return pw_sum64(l, n);
-    }
+    case 6: return pw_sum64(n, [&](int i) { return log(x(i) + eps); });  // product 194-225
     case 7: {  // range_fairness 228-246
-      double mx = x[0], mn = x[0];
-      for (int i = 1; i < n; ++i) { mx = x[i] > mx ? x[i] : mx; mn = x[i] < mn ? x[i] : mn; }
+      double mx = x(0), mn = x(0);
+      for (int i = 1; i < n; ++i) { mx = x(i) > mx ? x(i) : mx; mn = x(i) < mn ? x(i) : mn; }
       return -(mx - mn);
     }
     case 8: {  // gini_coefficient 249-287
-      const double mean = pw_sum64(x, n) / (double)n;
+      const double mean = pw_sum64(n, x) / (double)n;
       if (mean == 0.0) return 0.0;
       double ds = 0.0;
       for (int i = 0; i < n; ++i)
-        for (int k = 0; k < n; ++k) ds += fabs(x[i] - x[k]);
+        for (int k = 0; k < n; ++k) ds += fabs(x(i) - x(k));
       return -(ds / ((double)(2 * n * n) * mean));
     }
     default: return 0.0;
@@ -822,33 +874,17 @@ struct ObsOutputs {
   double* ep_ret;
 };
 
-template <int MODE>
+template <int MAXS, int MODE>
 __global__ void __launch_bounds__(64)
     observe_kernel(DevState st, SimParams p, ObsOutputs out, const uint8_t* reset_mask) {
   constexpr int mode = MODE;
   const size_t b = blockIdx.x;
   const int lane = threadIdx.x;
   if (mode == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
-  __shared__ FeatScratch sc;
-  __shared__ float s_obs[MAX_S * NF];
+  __shared__ ObsScratch<MAXS> sc;
   const int S = p.S;
-  for (int s = 0; s < S; ++s) {
-    const size_t sb = b * (size_t)S + (size_t)s;
-    const uint32_t cnt = st.hc[sb] >> 16;
-    const uint32_t rc = st.res_count[sb];
-    float f[2][5];
-    server_features(st.res_fct + sb * K, st.res_dur + sb * K, st.res_ts + sb * K, rc, p.decay_c,
-                    sc, f, lane);
-    if (lane == 0) {
-      s_obs[s * NF + 0] = (float)cnt;
-#pragma unroll
-      for (int q = 0; q < 5; ++q) {
-        s_obs[s * NF + 1 + q] = f[0][q];
-        s_obs[s * NF + 6 + q] = f[1][q];
-      }
-    }
-  }
-  __syncthreads();
+  observe_env<MAXS>(st, p, b, sc, lane);
+  const float* s_obs = sc.obs;
 
   if (mode == kModeStep && lane == 0) {
     const double r = reward_of(s_obs, S, p.reward_metric, p.reward_field);
@@ -891,17 +927,31 @@ __global__ void __launch_bounds__(64)
 
 // ================================================================ stateless entry points
 
+// Reservoir features of caller-given reservoirs: 4 reservoirs per block, each presented to
+// observe_env as one "server" whose fct and duration arrays are both the given values.
 __global__ void __launch_bounds__(64)
-    features_kernel(const float* values, const uint32_t* ts, const uint32_t* counts,
+    features_kernel(const float* values, const uint32_t* ts, const uint32_t* counts, int64_t n,
                     float decay_c, float* out) {
-  const size_t r = blockIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * 4;
   const int lane = threadIdx.x;
-  __shared__ FeatScratch sc;
-  float f[2][5];
-  server_features(values + r * K, values + r * K, ts + r * K, counts[r], decay_c, sc, f, lane);
-  if (lane == 0) {
-#pragma unroll
-    for (int q = 0; q < 5; ++q) out[r * 5 + q] = f[0][q];
+  __shared__ ObsScratch<4> sc;
+  const int S = (int)(n - r0 < 4 ? n - r0 : 4);
+  DevState st{};
+  st.res_fct = const_cast<float*>(values) + r0 * K;
+  st.res_dur = const_cast<float*>(values) + r0 * K;
+  st.res_ts = const_cast<uint32_t*>(ts) + r0 * K;
+  st.res_count = const_cast<uint32_t*>(counts) + r0;
+  __shared__ uint32_t hc0[4];
+  if (lane < 4) hc0[lane] = 0;
+  st.hc = hc0;
+  SimParams p{};
+  p.S = S;
+  p.decay_c = decay_c;
+  __syncthreads();
+  observe_env<4>(st, p, 0, sc, lane);
+  for (int e = lane; e < S * 5; e += 64) {
+    const int s = e / 5, f = e - s * 5;
+    out[(r0 + s) * 5 + f] = sc.obs[s * NF + 1 + f];
   }
 }
 
