@@ -26,21 +26,24 @@ sys.path.insert(0, ROOT)
 
 METRIC = ("env-steps/sec (whole node), 4-server LB env, batch 4k→512k at 1/2/4/8 MI355X")
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
+ARRIVAL_RATE = 400.0   # flows/s per env (bench workload)
+STEP_INTERVAL = 0.25   # simulated seconds per step
 K = 128
 
 
-def algorithmic_bytes(S: int):
+def algorithmic_bytes(S: int, flows_per_step: float):
     """Bytes each kernel must move per env-step with the state layout of DESIGN.md §4.
 
-    observe : read 3 reservoir arrays (fct, dur, ts: 128 x 4 B each) + hc + res_count per server,
-              ep_step/ep_return read+write, obs 44 B/server, reward 4, done 1, ep outputs 12.
-    dynamics: read+write env header (8 x 4 B) and per-server hc/last_tc/res_count, action 8 B and
-              assign-count 4 B per server (ring and reservoir-insert traffic is data dependent
-              and not counted: a lower bound).
+    observe : read the 3 reservoir arrays (fct, dur, ts: 128 x 4 B each) + hc + res_count per
+              server, ep_step/ep_return read+write, obs 44 B/server, reward 4, done 1, ep outputs 12.
+    dynamics: env header (8 x 4 B) and per-server hc/last_tc/res_count read+write, action 8 B and
+              assign count 4 B per server, and every flow's 8-B ring entry written once and read
+              once (flows_per_step = lambda * dt).  Reservoir inserts (data dependent, ~12 B per
+              accepted sample) are not counted: a lower bound.
     """
     obs = S * (3 * K * 4 + 8 + 44) + 12 + 12 + 4 + 1 + 12
-    dyn = 2 * 32 + S * (2 * 12 + 8 + 4)
-    return {"observe": obs, "dynamics": dyn}
+    dyn = 2 * 32 + S * (2 * 12 + 8 + 4) + 16 * flows_per_step
+    return {"observe_kernel": obs, "dynamics_kernel": dyn}
 
 
 def parse():
@@ -152,8 +155,15 @@ def main():
         value = world * B * args.steps / elapsed
         names = ["dynamics_kernel", "observe_kernel"]
         avg = {names[i]: ms[i] / max(1, cnt[i]) for i in range(2)}
+        abytes = algorithmic_bytes(S, ARRIVAL_RATE * STEP_INTERVAL)
+        per_kernel = {}
+        for k in names:
+            ab_k = abytes[k] * B
+            ach = ab_k / (avg[k] * 1e-3) / 1e9
+            per_kernel[k] = {"avg_launch_ms": avg[k], "algorithmic_bytes_per_launch": ab_k,
+                             "achieved_GBps": ach, "frac": ach / HBM_PEAK_GBS}
         dom = max(avg, key=avg.get)
-        ab = algorithmic_bytes(S)["observe" if dom == "observe_kernel" else "dynamics"] * B
+        ab = abytes[dom] * B
         achieved = ab / (avg[dom] * 1e-3) / 1e9
         traffic = None
         tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -177,7 +187,7 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "algorithmic_bytes_per_launch": ab,
                          "avg_launch_ms": avg[dom],
-                         "kernel_avg_ms": avg},
+                         "kernel_avg_ms": avg, "kernels": per_kernel},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
