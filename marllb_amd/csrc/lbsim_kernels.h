@@ -86,9 +86,11 @@ struct SimParams {
 // [server][slot][lane] so a wave's 64 per-lane ds_read_b64 of one (server, slot) pair are
 // conflict-free whatever slot each lane is at.  The event loop then reads no global memory (a
 // global load there forces s_waitcnt vmcnt(0) behind every outstanding store, which at one wave
-// per SIMD serialises the loop on memory latency).  The ring in HBM stays canonical
-// (write-through on push, window written back at kernel exit); an entry is loaded from HBM only
-// when a queue longer than WL advances.
+// per SIMD serialises the loop on memory latency) and writes the HBM ring only for queue entries
+// at index >= WL (an entry's index only decreases, so such entries stay in HBM until a refill
+// brings them into the window).  At kernel exit the window is written back, so between kernels
+// the HBM ring holds every in-flight flow (the snapshot layout of DESIGN.md §4).  Most flows are
+// born and complete inside one step and never touch HBM.
 template <int MAXS>
 struct Win {
   static constexpr int WL = MAXS <= 8 ? 8 : 4;
@@ -310,15 +312,16 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     int32_t svc = (int32_t)(L.next_work * a_scale);
     svc = svc < 1 ? 1 : svc;
     const int32_t tc_a = start_a + svc;
-    if (push) {
-      int pos = a_head + a_cnt;
-      pos = pos >= Q ? pos - Q : pos;
+    if (push) {  // queue index < WL: LDS window only; beyond it: the HBM ring (overflow)
       const int2 e = make_int2(tc_a, ta);
-      st.ring[(b0 + (size_t)chosen) * Q + pos] = e;  // write-through
       if (a_cnt < WL) {
         int li = a_lh + a_cnt;
         li = li >= WL ? li - WL : li;
         *qslot<MAXS>(q, chosen, li, lane) = e;
+      } else {
+        int pos = a_head + a_cnt;
+        pos = pos >= Q ? pos - Q : pos;
+        st.ring[(b0 + (size_t)chosen) * Q + pos] = e;
       }
     }
 
@@ -559,10 +562,16 @@ __device__ __forceinline__ T pairwise8(int n, int j, F term) {
 // ================================================================ features of one env
 
 // LDS image of one env's reservoirs during observe (one wave per env, 64-thread blocks).
+// Rows are padded to KP = 136 dwords: row r starts at bank 8r (mod 32), so the 8 lanes x 8
+// groups of a sort pass (lane t of group g reads slot 8e + t of row g) and the 8-lane pairwise
+// groups hit distinct banks.
+constexpr int KP = K + 8;
+
 template <int MAXS>
 struct ObsScratch {
-  uint32_t vals[2 * MAXS][K];  // reservoir r = 2s (fct) / 2s+1 (duration), slot order; then sorted
-  float wts[MAXS][K];          // decay weights of server s (shared by its two reservoirs)
+  uint32_t vals[2 * MAXS][KP];  // reservoir r = 2s (fct) / 2s+1 (duration), slot order; then
+                                // sorted, transposed: sorted position p at (p & 15) * 8 + (p >> 4)
+  float wts[MAXS][KP];          // decay weights of server s (shared by its two reservoirs)
   int n[2 * MAXS];             // valid slots per reservoir
   float mean[2 * MAXS], sd[2 * MAXS], md[2 * MAXS], p90[2 * MAXS], p90d[2 * MAXS];
   double swt[MAXS], svw[2 * MAXS];
@@ -697,9 +706,11 @@ __device__ __forceinline__ void observe_env(const DevState& st, const SimParams&
     const int rr = act ? r : 0;
     const int n = act ? sc.n[r] : 0;
     uint32_t key[16], pay[16];
+    // any initial placement sorts to the same keys; ties only permute equal keys, which changes
+    // neither p90 nor the weighted p90 (exact integer cumsums), so load strided (bank-free)
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const int slot = 16 * j + e;
+      const int slot = 8 * e + j;
       const bool v = slot < n;
       key[e] = v ? sc.vals[rr][slot] : 0xFFFFFFFFu;
       pay[e] = v ? __float_as_uint(sc.wts[rr >> 1][slot]) : 0u;
@@ -738,7 +749,7 @@ __device__ __forceinline__ void observe_env(const DevState& st, const SimParams&
     // sorted keys back into LDS (slot-order values are no longer needed)
 #pragma unroll
     for (int e = 0; e < 16; ++e)
-      if (act) sc.vals[rr][16 * j + e] = key[e];
+      if (act) sc.vals[rr][e * 8 + j] = key[e];  // sorted position 16 j + e, transposed
     __syncthreads();
     if (j == 0 && act) {
       float p90 = 0.0f, p90d = 0.0f;
@@ -748,11 +759,12 @@ __device__ __forceinline__ void observe_env(const DevState& st, const SimParams&
         const float fl = floorf(hidx);
         const int lo = (int)fl;
         const float gg = hidx - fl;
-        const float va = __uint_as_float(sc.vals[r][lo]);
-        const float vb = __uint_as_float(sc.vals[r][lo + 1 < n ? lo + 1 : lo]);
+        auto sorted = [&](int pos) { return __uint_as_float(sc.vals[r][(pos & 15) * 8 + (pos >> 4)]); };
+        const float va = sorted(lo);
+        const float vb = sorted(lo + 1 < n ? lo + 1 : lo);
         const float diff = vb - va;
         p90 = (gg >= 0.5f) ? (vb - diff * (1.0f - gg)) : (va + diff * gg);
-        p90d = __uint_as_float(sc.vals[r][pd]);
+        p90d = sorted(pd);
       }
       sc.p90[r] = p90;
       sc.p90d[r] = p90d;
