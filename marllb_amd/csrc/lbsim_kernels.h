@@ -93,29 +93,47 @@ struct SimParams {
 // born and complete inside one step and never touch HBM.
 template <int MAXS>
 struct Win {
-  static constexpr int WL = MAXS <= 8 ? 8 : 4;
+  static constexpr int WL = MAXS <= 4 ? 8 : (MAXS <= 8 ? 4 : 2);  // LDS <= 24 / 32 / 48 KiB
 };
+
+// Per-server fields touched only by the server an event changes live in LDS, lane-major
+// ([field][server][lane], conflict-free): one ds_read/ds_write per field per event instead of an
+// S-way register select chain.  cnt / head_tc / score stay in registers (scanned every event).
+enum SrvField { F_HEAD = 0, F_LH, F_TAIL, F_LAST, F_RCNT, F_ASSIGNED, F_DEN_LO, F_DEN_HI, F_NUM };
 
 template <int MAXS>
 struct LaneState {
   static constexpr int WL = Win<MAXS>::WL;
-  int32_t cnt[MAXS], head[MAXS], lh[MAXS];  // queue length, ring head, LDS window head
-  int32_t head_tc[MAXS];                      // t_complete of the head flow (valid if cnt > 0)
-  int32_t tail_tc[MAXS], last_tc[MAXS];
-  uint32_t rcnt[MAXS];
-  int32_t assigned[MAXS];
-  float score[MAXS];
-  double den[MAXS];
+  int32_t cnt[MAXS];      // flows in flight (n_flow_on)
+  int32_t head_tc[MAXS];  // t_complete of the head flow (valid if cnt > 0)
+  float score[MAXS];      // SED / LSQ score
   int32_t next_arr;
   float next_work;
   uint32_t u2, u3, arr_idx, episode, clock, dropped;
   uint32_t gid;
 };
 
+struct Lds {
+  int2* q;       // queue window [server][slot][lane]
+  int32_t* f;    // per-server fields [field][server][lane]
+  int lane;
+};
+
+template <int MAXS>
+__device__ __forceinline__ int32_t& fld(const Lds& l, int field, int s) {
+  return l.f[(field * MAXS + s) * 64 + l.lane];
+}
+
+template <int MAXS>
+__device__ __forceinline__ double den_of(const Lds& l, int s) {
+  const uint32_t lo = (uint32_t)fld<MAXS>(l, F_DEN_LO, s), hi = (uint32_t)fld<MAXS>(l, F_DEN_HI, s);
+  return __hiloint2double((int)hi, (int)lo);
+}
+
 // LDS window slot (server s, slot i) of this lane.
 template <int MAXS>
-__device__ __forceinline__ int2* qslot(int2* q, int s, int i, int lane) {
-  return q + ((s * Win<MAXS>::WL + i) * 64 + lane);
+__device__ __forceinline__ int2* qslot(const Lds& l, int s, int i) {
+  return l.q + ((s * Win<MAXS>::WL + i) * 64 + l.lane);
 }
 
 // SED score (n_flow_on + 1) / (1e-9 + w) in double, stored as f32 (node.c:393-399); LSQ: n.
@@ -143,30 +161,58 @@ __device__ __forceinline__ void draw_arrival(const SimParams& p, LaneState<MAXS>
   arrival_from_draw(p, d, t_prev, L.next_arr, L.next_work, L.u2, L.u3);
 }
 
-// Kernel entry: the first WL entries of every queue from the HBM ring into the LDS window.
+// Kernel entry: per-server state from HBM; the first WL entries of every queue into LDS.
 template <int MAXS>
-__device__ __forceinline__ void load_window(const DevState& st, const SimParams& p,
-                                            LaneState<MAXS>& L, size_t b, int2* q, int lane) {
+__device__ __forceinline__ void load_servers(const DevState& st, const SimParams& p,
+                                             LaneState<MAXS>& L, uint32_t b, const Lds& l) {
   constexpr int WL = LaneState<MAXS>::WL;
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) {
-    L.lh[s] = 0;
+    L.cnt[s] = 0;
     L.head_tc[s] = 0;
-    L.tail_tc[s] = 0;
+    L.score[s] = 0.f;
     if (s < p.S) {
-      const size_t sb = b * (size_t)p.S + (size_t)s;
+      const uint32_t sb = b * (uint32_t)p.S + (uint32_t)s;
+      const uint32_t hc = st.hc[sb];
+      const int head = (int)(hc & 0xFFFFu);
+      L.cnt[s] = (int32_t)(hc >> 16);
+      fld<MAXS>(l, F_HEAD, s) = head;
+      fld<MAXS>(l, F_LH, s) = 0;
+      fld<MAXS>(l, F_LAST, s) = st.last_tc[sb];
+      fld<MAXS>(l, F_RCNT, s) = (int32_t)st.res_count[sb];
+      fld<MAXS>(l, F_ASSIGNED, s) = 0;
+      int32_t tail = 0;
       for (int i = 0; i < WL && i < L.cnt[s]; ++i) {
-        int pos = L.head[s] + i;
+        int pos = head + i;
         if (pos >= p.Q) pos -= p.Q;
-        *qslot<MAXS>(q, s, i, lane) = st.ring[sb * p.Q + pos];
+        *qslot<MAXS>(l, s, i) = st.ring[sb * (uint32_t)p.Q + (uint32_t)pos];
       }
       if (L.cnt[s] > 0) {
-        int tp = L.head[s] + L.cnt[s] - 1;
+        int tp = head + L.cnt[s] - 1;
         if (tp >= p.Q) tp -= p.Q;
-        L.tail_tc[s] = st.ring[sb * p.Q + tp].x;
-        L.head_tc[s] = st.ring[sb * p.Q + L.head[s]].x;
+        tail = st.ring[sb * (uint32_t)p.Q + (uint32_t)tp].x;
+        L.head_tc[s] = st.ring[sb * (uint32_t)p.Q + (uint32_t)head].x;
       }
+      fld<MAXS>(l, F_TAIL, s) = tail;
     }
+  }
+}
+
+// Reset: empty queues and reservoirs.
+template <int MAXS>
+__device__ __forceinline__ void clear_servers(const SimParams& p, LaneState<MAXS>& L,
+                                              const Lds& l) {
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) {
+    L.cnt[s] = 0;
+    L.head_tc[s] = 0;
+    L.score[s] = 0.f;
+    fld<MAXS>(l, F_HEAD, s) = 0;
+    fld<MAXS>(l, F_LH, s) = 0;
+    fld<MAXS>(l, F_TAIL, s) = 0;
+    fld<MAXS>(l, F_LAST, s) = kLastNone;
+    fld<MAXS>(l, F_RCNT, s) = 0;
+    fld<MAXS>(l, F_ASSIGNED, s) = 0;
   }
 }
 
@@ -175,27 +221,32 @@ __device__ __forceinline__ void load_window(const DevState& st, const SimParams&
 // Event loop, one event per iteration per lane: the earliest pending completion (if it is due no
 // later than the next arrival, or than the step end when no arrival is due) or else the next
 // arrival.  The body is straight-line and predicated: both event kinds are evaluated by every
-// lane, per-server scalars are updated through selects, only the small stores are masked.  This
-// keeps the 64 lanes (64 envs) converged; a branchy body gets structurised by the compiler into
-// nested per-event-kind loops in which lanes wait for each other.  Per server the completions are
-// processed in t_complete order before any arrival at the same or a later time — the order the
-// oracle (server by server) produces — so every reservoir sees the same insert sequence and the
-// state is bit-identical.
+// lane and at most one server changes per event; its LDS fields are read once and written once.
+// This keeps the 64 lanes (64 envs) converged; a branchy body gets structurised by the compiler
+// into nested per-event-kind loops in which lanes wait for each other.  Per server the
+// completions are processed in t_complete order before any arrival at the same or a later time —
+// the order the oracle (server by server) produces — so every reservoir sees the same insert
+// sequence and the state is bit-identical.
 template <int MAXS>
 __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
-                                         LaneState<MAXS>& L, size_t b, const float* w, int2* q,
-                                         int lane) {
+                                         LaneState<MAXS>& L, uint32_t b, const float* w,
+                                         const Lds& l) {
   constexpr int WL = LaneState<MAXS>::WL;
   const int S = p.S, Q = p.Q;
   const int32_t dt = p.dt_us;
+  // sample timestamps: ts_ms = (clock * dt + tc) / 1000 = base_ms + (base_rem + tc) / 1000
   const uint64_t base_us = (uint64_t)L.clock * (uint64_t)dt;
+  const uint32_t base_ms = (uint32_t)(base_us / 1000u);
+  const uint32_t base_rem = (uint32_t)(base_us - (uint64_t)base_ms * 1000u);
   const bool two_choice = (p.policy == 1 || p.policy == 3);
-  const size_t b0 = b * (size_t)S;
+  const uint32_t b0 = b * (uint32_t)S;
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) {
     if (s < S) {
-      L.den[s] = (double)w[s] + 1e-9;
-      L.score[s] = policy_score(p.policy, L.cnt[s], L.den[s]);
+      const double den = (double)w[s] + 1e-9;
+      fld<MAXS>(l, F_DEN_LO, s) = (int32_t)__double2loint(den);
+      fld<MAXS>(l, F_DEN_HI, s) = (int32_t)__double2hiint(den);
+      L.score[s] = policy_score(p.policy, L.cnt[s], den);
     }
   }
   for (;;) {
@@ -213,54 +264,6 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     const bool comp = smin >= 0 && tmin <= horizon;
     const bool arr = !comp && arrival_due;
     if (!comp && !arr) break;
-
-    // ---- gathers for the completing server
-    uint32_t cres = 0;
-    int32_t h_last = 0, h_cnt = 0, h_head = 0, h_lh = 0;
-#pragma unroll
-    for (int s = 0; s < MAXS; ++s) {
-      const bool m = s == smin;
-      cres = m ? L.rcnt[s] : cres;
-      h_last = m ? L.last_tc[s] : h_last;
-      h_cnt = m ? L.cnt[s] : h_cnt;
-      h_head = m ? L.head[s] : h_head;
-      h_lh = m ? L.lh[s] : h_lh;
-    }
-    const int ss = smin < 0 ? 0 : smin;
-    const int32_t h_ta = qslot<MAXS>(q, ss, h_lh, lane)->y;  // arrival time of the head flow
-    const int h_next = (h_head + 1 == Q) ? 0 : h_head + 1;
-    const int lh_next = (h_lh + 1 == WL) ? 0 : h_lh + 1;
-    // rare: the queue is longer than the window; bring entry WL-1 (after this pop) into LDS
-    if (comp && h_cnt - 1 >= WL) {
-      int pw = h_next + WL - 1;
-      pw = pw >= Q ? pw - Q : pw;
-      *qslot<MAXS>(q, ss, h_lh, lane) = st.ring[(b0 + (size_t)ss) * Q + pw];  // slot lh+WL-1 == lh
-      __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);  // drain in the rare branch, not at the back-edge
-    }
-    const int32_t nxt_tc = qslot<MAXS>(q, ss, lh_next, lane)->x;  // next head (valid if cnt > 1)
-
-    // ---- the one Philox block of this event (Algorithm R draw, or the next arrival's draw)
-    const u32x4 ctr = comp
-        ? u32x4{cres >> 1, L.gid, L.episode, (kStreamReservoir << 24) | (uint32_t)smin}
-        : u32x4{L.arr_idx + 1u, L.gid, L.episode, kStreamArrival << 24};
-    const u32x4 d = philox4x32_10(ctr, p.key0, p.key1);
-
-    // ---- completion (lbhash.h:116-124, 131-135) + Algorithm R (reservoir.py:64-85)
-    const int32_t tc = tmin;
-    const int32_t start_c = h_ta > h_last ? h_ta : h_last;
-    int slot;
-    {
-      const uint32_t hi = (cres & 1u) ? d.w : d.y;
-      const uint32_t lo = (cres & 1u) ? d.z : d.x;
-      const uint64_t j = mulhi64_by_u33(hi, lo, (uint64_t)cres + 1u);
-      slot = cres < (uint32_t)K ? (int)cres : (j < (uint64_t)K ? (int)j : -1);
-    }
-    if (comp && slot >= 0) {
-      const size_t r = (b0 + (size_t)smin) * K + (size_t)slot;
-      st.res_fct[r] = (float)(tc - h_ta) * 1.0e-6f;
-      st.res_dur[r] = (float)(tc - start_c) * 1.0e-6f;
-      st.res_ts[r] = (uint32_t)((base_us + (uint64_t)(int64_t)tc) / 1000u);
-    }
 
     // ---- arrival: choose a server (node.c:388-441); full servers are not eligible
     const int32_t ta = L.next_arr;
@@ -296,55 +299,95 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     }
     const bool push = arr && chosen >= 0;
     L.dropped += (arr && chosen < 0) ? 1u : 0u;
-    int32_t a_cnt = 0, a_head = 0, a_tail = 0, a_lh = 0;
+
+    // ---- the one server this event changes, and its fields
+    const int cs = comp ? smin : (push ? chosen : -1);
+    const int csi = cs < 0 ? 0 : cs;
+    int32_t c_cnt = 0;
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) c_cnt = (s == cs) ? L.cnt[s] : c_cnt;
+    const int32_t c_head = fld<MAXS>(l, F_HEAD, csi);
+    const int32_t c_lh = fld<MAXS>(l, F_LH, csi);
+    const int32_t c_tail = fld<MAXS>(l, F_TAIL, csi);
+    const int32_t c_last = fld<MAXS>(l, F_LAST, csi);
+    const uint32_t cres = (uint32_t)fld<MAXS>(l, F_RCNT, csi);
+    const double c_den = den_of<MAXS>(l, csi);
+
+    // ---- the one Philox block of this event (Algorithm R draw, or the next arrival's draw)
+    const u32x4 ctr = comp
+        ? u32x4{cres >> 1, L.gid, L.episode, (kStreamReservoir << 24) | (uint32_t)smin}
+        : u32x4{L.arr_idx + 1u, L.gid, L.episode, kStreamArrival << 24};
+    const u32x4 d = philox4x32_10(ctr, p.key0, p.key1);
+
+    // ---- completion (lbhash.h:116-124, 131-135) + Algorithm R (reservoir.py:64-85)
+    const int32_t tc = tmin;
+    const int32_t h_ta = qslot<MAXS>(l, csi, c_lh)->y;  // arrival time of the head flow
+    const int32_t start_c = h_ta > c_last ? h_ta : c_last;
+    const int h_next = (c_head + 1 == Q) ? 0 : c_head + 1;
+    const int lh_next = (c_lh + 1 == WL) ? 0 : c_lh + 1;
+    int slot;
+    {
+      const uint32_t hi = (cres & 1u) ? d.w : d.y;
+      const uint32_t lo = (cres & 1u) ? d.z : d.x;
+      const uint64_t j = mulhi64_by_u33(hi, lo, (uint64_t)cres + 1u);
+      slot = cres < (uint32_t)K ? (int)cres : (j < (uint64_t)K ? (int)j : -1);
+    }
+    if (comp && slot >= 0) {
+      const uint32_t r = (b0 + (uint32_t)smin) * (uint32_t)K + (uint32_t)slot;
+      st.res_fct[r] = (float)(tc - h_ta) * 1.0e-6f;
+      st.res_dur[r] = (float)(tc - start_c) * 1.0e-6f;
+      st.res_ts[r] = base_ms + (base_rem + (uint32_t)tc) / 1000u;
+    }
+    // rare: the queue is longer than the window; bring entry WL-1 (after this pop) into LDS
+    if (comp && c_cnt - 1 >= WL) {
+      int pw = h_next + WL - 1;
+      pw = pw >= Q ? pw - Q : pw;
+      *qslot<MAXS>(l, csi, c_lh) = st.ring[(b0 + (uint32_t)csi) * (uint32_t)Q + (uint32_t)pw];
+      __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);  // drain in the rare branch, not at the back-edge
+    }
+    const int32_t nxt_tc = qslot<MAXS>(l, csi, lh_next)->x;  // next head (valid if cnt > 1)
+
+    // ---- arrival: FIFO service starts when the server's last queued flow ends
     float a_scale = 0.f;
 #pragma unroll
-    for (int s = 0; s < MAXS; ++s) {
-      const bool m = s == chosen;
-      a_cnt = m ? L.cnt[s] : a_cnt;
-      a_head = m ? L.head[s] : a_head;
-      a_tail = m ? L.tail_tc[s] : a_tail;
-      a_lh = m ? L.lh[s] : a_lh;
-      a_scale = m ? p.svc_scale[s] : a_scale;
-    }
-    // FIFO service: start when the server's last queued flow ends
-    const int32_t start_a = a_cnt > 0 ? (a_tail > ta ? a_tail : ta) : ta;
+    for (int s = 0; s < MAXS; ++s) a_scale = (s == chosen) ? p.svc_scale[s] : a_scale;
+    const int32_t start_a = c_cnt > 0 ? (c_tail > ta ? c_tail : ta) : ta;
     int32_t svc = (int32_t)(L.next_work * a_scale);
     svc = svc < 1 ? 1 : svc;
     const int32_t tc_a = start_a + svc;
     if (push) {  // queue index < WL: LDS window only; beyond it: the HBM ring (overflow)
       const int2 e = make_int2(tc_a, ta);
-      if (a_cnt < WL) {
-        int li = a_lh + a_cnt;
+      if (c_cnt < WL) {
+        int li = c_lh + c_cnt;
         li = li >= WL ? li - WL : li;
-        *qslot<MAXS>(q, chosen, li, lane) = e;
+        *qslot<MAXS>(l, csi, li) = e;
       } else {
-        int pos = a_head + a_cnt;
+        int pos = c_head + c_cnt;
         pos = pos >= Q ? pos - Q : pos;
-        st.ring[(b0 + (size_t)chosen) * Q + pos] = e;
+        st.ring[(b0 + (uint32_t)csi) * (uint32_t)Q + (uint32_t)pos] = e;
       }
     }
 
-    // ---- per-server scalars through selects (at most one server changes per event)
-    const int cs = comp ? smin : (push ? chosen : -1);
-    const int32_t n_cs = comp ? h_cnt - 1 : a_cnt + 1;
-    double den_cs = 1.0;
-#pragma unroll
-    for (int s = 0; s < MAXS; ++s) den_cs = (s == cs) ? L.den[s] : den_cs;
-    const float sc_new = policy_score(p.policy, n_cs, den_cs);
+    // ---- write back the changed server
+    const int32_t n_cs = comp ? c_cnt - 1 : c_cnt + 1;
+    const float sc_new = policy_score(p.policy, n_cs, c_den);
+    if (comp) {
+      fld<MAXS>(l, F_RCNT, csi) = (int32_t)(cres != 0xFFFFFFFFu ? cres + 1u : cres);
+      fld<MAXS>(l, F_LAST, csi) = tc;
+      fld<MAXS>(l, F_HEAD, csi) = h_next;
+      fld<MAXS>(l, F_LH, csi) = lh_next;
+    }
+    if (push) {
+      fld<MAXS>(l, F_TAIL, csi) = tc_a;
+      fld<MAXS>(l, F_ASSIGNED, csi) += 1;
+    }
+    const int32_t new_head_tc = comp ? nxt_tc : tc_a;
 #pragma unroll
     for (int s = 0; s < MAXS; ++s) {
-      const bool pc = comp && s == smin;
-      const bool pa = push && s == chosen;
-      L.rcnt[s] = (pc && cres != 0xFFFFFFFFu) ? cres + 1u : L.rcnt[s];
-      L.last_tc[s] = pc ? tc : L.last_tc[s];
-      L.head[s] = pc ? h_next : L.head[s];
-      L.lh[s] = pc ? lh_next : L.lh[s];
-      L.head_tc[s] = pc ? nxt_tc : ((pa && a_cnt == 0) ? tc_a : L.head_tc[s]);
-      L.cnt[s] = (s == cs) ? n_cs : L.cnt[s];
-      L.tail_tc[s] = pa ? tc_a : L.tail_tc[s];
-      L.assigned[s] += pa ? 1 : 0;
-      L.score[s] = (s == cs) ? sc_new : L.score[s];
+      const bool m = s == cs;
+      L.cnt[s] = m ? n_cs : L.cnt[s];
+      L.score[s] = m ? sc_new : L.score[s];
+      L.head_tc[s] = (m && (comp || c_cnt == 0)) ? new_head_tc : L.head_tc[s];
     }
 
     // ---- next arrival (draw d belongs to arrival index arr_idx + 1)
@@ -365,48 +408,56 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) {
     if (s < S) {
+      const int lh = fld<MAXS>(l, F_LH, s);
       for (int i = 0; i < WL && i < L.cnt[s]; ++i) {
-        int li = L.lh[s] + i;
+        int li = lh + i;
         li = li >= WL ? li - WL : li;
-        int2* e = qslot<MAXS>(q, s, li, lane);
+        int2* e = qslot<MAXS>(l, s, li);
         e->x -= dt;
         e->y -= dt;
       }
-      const size_t sbase = b0 + (size_t)s;
-      int pos = L.head[s] + WL;
+      const uint32_t sbase = b0 + (uint32_t)s;
+      int pos = fld<MAXS>(l, F_HEAD, s) + WL;
       if (pos >= Q) pos -= Q;
       for (int i = WL; i < L.cnt[s]; ++i) {
-        int2 e = st.ring[sbase * Q + pos];
+        int2 e = st.ring[sbase * (uint32_t)Q + (uint32_t)pos];
         e.x -= dt;
         e.y -= dt;
-        st.ring[sbase * Q + pos] = e;
+        st.ring[sbase * (uint32_t)Q + (uint32_t)pos] = e;
         pos = (pos + 1 == Q) ? 0 : pos + 1;
       }
       L.head_tc[s] -= dt;
-      L.tail_tc[s] -= dt;
-      L.last_tc[s] = (L.last_tc[s] < kLastNone + dt) ? kLastNone : L.last_tc[s] - dt;
+      fld<MAXS>(l, F_TAIL, s) -= dt;
+      const int32_t last = fld<MAXS>(l, F_LAST, s);
+      fld<MAXS>(l, F_LAST, s) = (last < kLastNone + dt) ? kLastNone : last - dt;
     }
   }
   L.clock += 1u;
 }
 
-// Kernel exit: write the (rebased) LDS window back to the ring so HBM holds the canonical queue.
+// Kernel exit: the LDS window back to the ring so HBM holds every in-flight flow, and the
+// per-server state words.
 template <int MAXS>
-__device__ __forceinline__ void store_window(const DevState& st, const SimParams& p,
-                                             const LaneState<MAXS>& L, size_t b, int2* q,
-                                             int lane) {
+__device__ __forceinline__ void store_servers(const DevState& st, const SimParams& p,
+                                              const LaneState<MAXS>& L, uint32_t b,
+                                              const Lds& l, int32_t* assign_out) {
   constexpr int WL = LaneState<MAXS>::WL;
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) {
     if (s < p.S) {
-      const size_t sb = b * (size_t)p.S + (size_t)s;
+      const uint32_t sb = b * (uint32_t)p.S + (uint32_t)s;
+      const int head = fld<MAXS>(l, F_HEAD, s), lh = fld<MAXS>(l, F_LH, s);
       for (int i = 0; i < WL && i < L.cnt[s]; ++i) {
-        int pos = L.head[s] + i;
+        int pos = head + i;
         if (pos >= p.Q) pos -= p.Q;
-        int li = L.lh[s] + i;
+        int li = lh + i;
         li = li >= WL ? li - WL : li;
-        st.ring[sb * p.Q + pos] = *qslot<MAXS>(q, s, li, lane);
+        st.ring[sb * (uint32_t)p.Q + (uint32_t)pos] = *qslot<MAXS>(l, s, li);
       }
+      st.hc[sb] = (uint32_t)head | ((uint32_t)L.cnt[s] << 16);
+      st.last_tc[sb] = fld<MAXS>(l, F_LAST, s);
+      st.res_count[sb] = (uint32_t)fld<MAXS>(l, F_RCNT, s);
+      if (assign_out != nullptr) assign_out[sb] = fld<MAXS>(l, F_ASSIGNED, s);
     }
   }
 }
@@ -432,13 +483,14 @@ __global__ void __launch_bounds__(64)
     dynamics_kernel(DevState st, SimParams p, const void* action, int action_dtype,
                     int32_t* assign_out, const uint8_t* reset_mask) {
   constexpr int mode = MODE;
-  const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int lane = threadIdx.x;
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   __shared__ int2 qwin[MAXS * Win<MAXS>::WL * 64];
-  if (b >= (size_t)p.B) return;
+  __shared__ int32_t fields[F_NUM * MAXS * 64];
+  const Lds l{qwin, fields, (int)threadIdx.x};
+  if (b >= (uint32_t)p.B) return;
   const int S = p.S;
   LaneState<MAXS> L;
-  L.gid = p.env_id_offset + (uint32_t)b;
+  L.gid = p.env_id_offset + b;
 
   if (mode == kModeReset) {
     if (reset_mask != nullptr && reset_mask[b] == 0) return;
@@ -447,17 +499,14 @@ __global__ void __launch_bounds__(64)
     L.dropped = 0u;
     L.arr_idx = 0u;
     draw_arrival<MAXS>(p, L, 0);
-#pragma unroll
-    for (int s = 0; s < MAXS; ++s) {
-      L.cnt[s] = 0; L.head[s] = 0; L.lh[s] = 0; L.head_tc[s] = 0; L.tail_tc[s] = 0;
-      L.last_tc[s] = kLastNone; L.rcnt[s] = 0u; L.assigned[s] = 0;
-    }
+    clear_servers<MAXS>(p, L, l);
     float w1[MAXS];
 #pragma unroll
     for (int s = 0; s < MAXS; ++s) w1[s] = 1.0f;
-    for (int k = 0; k < p.warmup_steps; ++k) sim_step<MAXS>(st, p, L, b, w1, qwin, lane);
+    for (int k = 0; k < p.warmup_steps; ++k) sim_step<MAXS>(st, p, L, b, w1, l);
     st.ep_step[b] = 0;
     st.ep_return[b] = 0.0;
+    store_servers<MAXS>(st, p, L, b, l, nullptr);
   } else {
     L.episode = st.episode[b];
     L.clock = st.clock[b];
@@ -467,33 +516,14 @@ __global__ void __launch_bounds__(64)
     L.next_work = st.next_work[b];
     L.u2 = st.next_u2[b];
     L.u3 = st.next_u3[b];
-#pragma unroll
-    for (int s = 0; s < MAXS; ++s) {
-      if (s < S) {
-        const size_t sb = b * (size_t)S + (size_t)s;
-        const uint32_t hc = st.hc[sb];
-        L.head[s] = (int32_t)(hc & 0xFFFFu);
-        L.cnt[s] = (int32_t)(hc >> 16);
-        L.last_tc[s] = st.last_tc[sb];
-        L.rcnt[s] = st.res_count[sb];
-        L.assigned[s] = 0;
-      } else {
-        L.head[s] = 0; L.cnt[s] = 0; L.last_tc[s] = kLastNone; L.rcnt[s] = 0u; L.assigned[s] = 0;
-      }
-    }
-    load_window<MAXS>(st, p, L, b, qwin, lane);
+    load_servers<MAXS>(st, p, L, b, l);
     float w[MAXS];
 #pragma unroll
     for (int s = 0; s < MAXS; ++s)
-      w[s] = (s < S) ? action_weight(p, action, action_dtype, b * (size_t)S + (size_t)s) : 1.0f;
-    sim_step<MAXS>(st, p, L, b, w, qwin, lane);
-    if (assign_out != nullptr) {
-#pragma unroll
-      for (int s = 0; s < MAXS; ++s)
-        if (s < S) assign_out[b * (size_t)S + (size_t)s] = L.assigned[s];
-    }
+      w[s] = (s < S) ? action_weight(p, action, action_dtype, (size_t)b * S + (size_t)s) : 1.0f;
+    sim_step<MAXS>(st, p, L, b, w, l);
+    store_servers<MAXS>(st, p, L, b, l, assign_out);
   }
-  store_window<MAXS>(st, p, L, b, qwin, lane);
   st.episode[b] = L.episode;
   st.clock[b] = L.clock;
   st.dropped[b] = L.dropped;
@@ -502,15 +532,6 @@ __global__ void __launch_bounds__(64)
   st.next_work[b] = L.next_work;
   st.next_u2[b] = L.u2;
   st.next_u3[b] = L.u3;
-#pragma unroll
-  for (int s = 0; s < MAXS; ++s) {
-    if (s < S) {
-      const size_t sb = b * (size_t)S + (size_t)s;
-      st.hc[sb] = (uint32_t)L.head[s] | ((uint32_t)L.cnt[s] << 16);
-      st.last_tc[sb] = L.last_tc[s];
-      st.res_count[sb] = L.rcnt[s];
-    }
-  }
 }
 
 // ================================================================ wave-level helpers (wave64)

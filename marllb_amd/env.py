@@ -204,8 +204,6 @@ class VecLoadBalanceEnv:
         self.autoreset = autoreset
         self.keep_terminal_obs = keep_terminal_obs
         self.handle = Handle(self.cfg, self.device_index)
-        self._ep_len = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
-        self._ep_ret = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
         self._reset_done = False
         # upper bound on every env's episode step since the last full reset: while it is below
         # max_steps no env can be done, so the masked auto-reset launch is provably a no-op
@@ -268,7 +266,7 @@ class VecLoadBalanceEnv:
         B, S = self.num_envs, self.num_servers
         obs = self._obs_buffer()
         reward = torch.empty(B, dtype=torch.float32, device=self.device)
-        done = torch.empty(B, dtype=torch.uint8, device=self.device)
+        done = torch.empty(B, dtype=torch.bool, device=self.device)  # 1-byte 0/1, as u8
         out = _lib.StepOutputs()
         out.obs, out.reward, out.done = obs.data_ptr(), reward.data_ptr(), done.data_ptr()
         assign = raw = None
@@ -278,12 +276,13 @@ class VecLoadBalanceEnv:
         if raw_obs:
             raw = self._obs_buffer()
             out.raw_obs = raw.data_ptr()
-        out.episode_length = self._ep_len.data_ptr()
-        out.episode_return = self._ep_ret.data_ptr()
+        ep_len = torch.empty(B, dtype=torch.int32, device=self.device)
+        ep_ret = torch.empty(B, dtype=torch.float64, device=self.device)
+        out.episode_length = ep_len.data_ptr()
+        out.episode_return = ep_ret.data_ptr()
         self.handle.check(self.handle.lib.lbsim_step_ex(self.handle.h, a.data_ptr(), dt,
                                                         ctypes.byref(out), self._stream()))
-        info: Dict[str, Any] = {"episode_length": self._ep_len.clone(),
-                                "episode_return": self._ep_ret.clone()}
+        info: Dict[str, Any] = {"episode_length": ep_len, "episode_return": ep_ret}
         if assign is not None:
             info["assign_counts"] = assign
         if raw is not None:
@@ -296,7 +295,7 @@ class VecLoadBalanceEnv:
             self.handle.check(self.handle.lib.lbsim_reset(self.handle.h, done.data_ptr(),
                                                           obs.data_ptr(), self._stream()))
         self._last_obs = obs
-        return obs, reward, done.bool(), info
+        return obs, reward, done, info
 
     def seed(self, seed: Optional[int] = None):
         if seed is None:
