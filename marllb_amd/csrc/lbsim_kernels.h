@@ -549,12 +549,48 @@ __device__ __forceinline__ uint32_t readlane_u32(uint32_t v, int lane) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
 }
 
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-  for (int m = 32; m > 0; m >>= 1) {
-    const uint32_t o = shfl_xor_u32(v, m);
-    v = o > v ? o : v;
-  }
+// Lane exchanges inside a 16-lane DPP row, VALU only (no LDS crossbar):
+//   xor 1 / xor 2: quad_perm [1,0,3,2] / [2,3,0,1];  xor 8: row_ror:8;
+//   xor 4: row_shl:4 (lane i reads i+4) for lanes with bit 2 clear, row_shr:4 (reads i-4) else.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int M>
+__device__ __forceinline__ uint32_t xor_lane_u32(uint32_t v, int lane) {
+  if constexpr (M == 1) return dpp_u32<0xB1>(v);
+  else if constexpr (M == 2) return dpp_u32<0x4E>(v);
+  else if constexpr (M == 4) {
+    const uint32_t up = dpp_u32<0x104>(v), dn = dpp_u32<0x114>(v);
+    return (lane & 4) ? dn : up;
+  } else if constexpr (M == 8) return dpp_u32<0x128>(v);
+  else return shfl_xor_u32(v, M);
+}
+template <int M>
+__device__ __forceinline__ float xor_lane_f32(float v, int lane) {
+  return __uint_as_float(xor_lane_u32<M>(__float_as_uint(v), lane));
+}
+template <int M>
+__device__ __forceinline__ double xor_lane_f64(double v, int lane) {
+  const uint32_t lo = xor_lane_u32<M>((uint32_t)__double2loint(v), lane);
+  const uint32_t hi = xor_lane_u32<M>((uint32_t)__double2hiint(v), lane);
+  return __hiloint2double((int)hi, (int)lo);
+}
+__device__ __forceinline__ float xor_lane(float v, int lane, int m) {
+  return m == 1 ? xor_lane_f32<1>(v, lane) : m == 2 ? xor_lane_f32<2>(v, lane) : xor_lane_f32<4>(v, lane);
+}
+__device__ __forceinline__ double xor_lane(double v, int lane, int m) {
+  return m == 1 ? xor_lane_f64<1>(v, lane) : m == 2 ? xor_lane_f64<2>(v, lane) : xor_lane_f64<4>(v, lane);
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v, int lane) {
+  uint32_t o;
+  o = xor_lane_u32<1>(v, lane); v = o > v ? o : v;
+  o = xor_lane_u32<2>(v, lane); v = o > v ? o : v;
+  o = xor_lane_u32<4>(v, lane); v = o > v ? o : v;
+  o = xor_lane_u32<8>(v, lane); v = o > v ? o : v;
+  o = shfl_xor_u32(v, 16); v = o > v ? o : v;
+  o = shfl_xor_u32(v, 32); v = o > v ? o : v;
   return v;
 }
 
@@ -573,9 +609,10 @@ __device__ __forceinline__ T pairwise8(int n, int j, F term) {
   const int m8 = n - (n % 8);
   T acc = term(j);
   for (int i = 8 + j; i < m8; i += 8) acc += term(i);
-  T t = acc + (T)__shfl_xor(acc, 1, 64);
-  t = t + (T)__shfl_xor(t, 2, 64);
-  t = t + (T)__shfl_xor(t, 4, 64);
+  const int lane = j;  // only bit 2 of the lane index is consulted (lane & 4 == j & 4)
+  T t = acc + xor_lane(acc, lane, 1);
+  t = t + xor_lane(t, lane, 2);
+  t = t + xor_lane(t, lane, 4);
   for (int i = m8; i < n; ++i) t += term(i);
   return t;
 }
@@ -629,8 +666,10 @@ __device__ __forceinline__ void bitonic128_g8(uint32_t (&key)[16], uint32_t (&pa
         const bool up = (t & (k >> 4)) == 0;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const uint32_t pk = shfl_xor_u32(key[e], lj);
-          const uint32_t pp = shfl_xor_u32(pay[e], lj);
+          const uint32_t pk = lj == 1 ? xor_lane_u32<1>(key[e], t)
+                              : lj == 2 ? xor_lane_u32<2>(key[e], t) : xor_lane_u32<4>(key[e], t);
+          const uint32_t pp = lj == 1 ? xor_lane_u32<1>(pay[e], t)
+                              : lj == 2 ? xor_lane_u32<2>(pay[e], t) : xor_lane_u32<4>(pay[e], t);
           const bool take = (lower == up) ? (pk < key[e]) : (pk > key[e]);
           key[e] = take ? pk : key[e];
           pay[e] = take ? pp : pay[e];
@@ -649,31 +688,43 @@ __device__ __forceinline__ void observe_env(const DevState& st, const SimParams&
   const int S = p.S;
   const int R = 2 * S;
   const int g = lane >> 3, j = lane & 7;
-  // ---- phase 1: reservoirs into LDS, decay weights relative to each server's newest sample
-  for (int s = 0; s < S; ++s) {
-    const size_t sb = b * (size_t)S + (size_t)s;
-    const uint32_t rc = st.res_count[sb];
-    const int n = rc < (uint32_t)K ? (int)rc : K;
-    uint32_t f[2], d[2], t[2];
+  // ---- phase 1: reservoirs into LDS, decay weights relative to each server's newest sample.
+  //      Loads of 4 servers are issued before any is consumed (memory-level parallelism).
+  for (int s0 = 0; s0 < S; s0 += 4) {
+    uint32_t f[4][2], d[4][2], t[4][2];
+    int nn[4];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int slot = lane + 64 * h;
-      const bool v = slot < n;
-      f[h] = v ? __float_as_uint(st.res_fct[sb * K + slot]) : 0u;
-      d[h] = v ? __float_as_uint(st.res_dur[sb * K + slot]) : 0u;
-      t[h] = v ? st.res_ts[sb * K + slot] : 0u;
-    }
-    const uint32_t newest = wave_max_u32(t[0] > t[1] ? t[0] : t[1]);
+    for (int u = 0; u < 4; ++u) {
+      const int s = s0 + u;
+      const size_t sb = b * (size_t)S + (size_t)(s < S ? s : 0);
+      const uint32_t rc = s < S ? st.res_count[sb] : 0u;
+      nn[u] = rc < (uint32_t)K ? (int)rc : K;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int slot = lane + 64 * h;
-      sc.vals[2 * s][slot] = f[h];
-      sc.vals[2 * s + 1][slot] = d[h];
-      sc.wts[s][slot] = slot < n ? lb_exp2f((float)(newest - t[h]) * p.decay_c) : 0.0f;
+      for (int h = 0; h < 2; ++h) {
+        const int slot = lane + 64 * h;
+        const bool v = slot < nn[u];
+        f[u][h] = v ? __float_as_uint(st.res_fct[sb * K + slot]) : 0u;
+        d[u][h] = v ? __float_as_uint(st.res_dur[sb * K + slot]) : 0u;
+        t[u][h] = v ? st.res_ts[sb * K + slot] : 0u;
+      }
     }
-    if (lane == 0) {
-      sc.n[2 * s] = n;
-      sc.n[2 * s + 1] = n;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int s = s0 + u;
+      if (s < S) {
+        const uint32_t newest = wave_max_u32(t[u][0] > t[u][1] ? t[u][0] : t[u][1], lane);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int slot = lane + 64 * h;
+          sc.vals[2 * s][slot] = f[u][h];
+          sc.vals[2 * s + 1][slot] = d[u][h];
+          sc.wts[s][slot] = slot < nn[u] ? lb_exp2f((float)(newest - t[u][h]) * p.decay_c) : 0.0f;
+        }
+        if (lane == 0) {
+          sc.n[2 * s] = nn[u];
+          sc.n[2 * s + 1] = nn[u];
+        }
+      }
     }
   }
   __syncthreads();
