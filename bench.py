@@ -104,10 +104,11 @@ def main():
     import torch.distributed as dist
 
     from marllb_amd import _lib
+    from marllb_amd import dist as lbdist
     from marllb_amd.env import VecLoadBalanceEnv
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
+    shard = lbdist.from_env(args.batch)
+    world, rank = shard.world, shard.rank
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
@@ -118,7 +119,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     B, S = args.batch, args.servers
-    env = VecLoadBalanceEnv(B, S, device=dev, seed=args.seed, env_id_offset=rank * B,
+    env = VecLoadBalanceEnv(B, S, device=dev, seed=args.seed, env_id_offset=shard.env_id_offset,
                             autoreset=True, max_steps=10000)
     env.reset()
     gen = torch.Generator(device=dev)
@@ -145,14 +146,10 @@ def main():
     ms = (ctypes.c_double * 4)()
     cnt = (ctypes.c_int64 * 4)()
     env.handle.check(lib.lbsim_profile_end(env.handle.h, ms, cnt))
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = lbdist.max_over_ranks(t1 - t0, dev)
 
     if rank == 0:
-        value = world * B * args.steps / elapsed
+        value = lbdist.throughput(shard, args.steps, elapsed)
         names = ["dynamics_kernel", "observe_kernel"]
         avg = {names[i]: ms[i] / max(1, cnt[i]) for i in range(2)}
         abytes = algorithmic_bytes(S, ARRIVAL_RATE * STEP_INTERVAL)

@@ -1,0 +1,88 @@
+"""Multi-rank path: env sharding by global id, no data-path collective.
+
+world_size-2 gloo runs of tests/dist_worker.py (each rank a separate process, as under
+torch.distributed.run) must reproduce, bit for bit, one process stepping the whole batch.  The CPU
+variant shards the oracle; the gpu variant shards the HIP product path (both ranks on cuda:0 — the
+point is the id-keyed sharding, not the card count).
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from marllb_amd import dist as lbdist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from dist_worker import actions  # noqa: E402
+
+B, S, T, SEED = 24, 4, 4, 1234
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_ranks(mode: str, world: int, out: str):
+    port = free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(
+            [sys.executable, os.path.join(HERE, "dist_worker.py"), "--mode", mode,
+             "--port", str(port), "--out", out, "--batch", str(B), "--servers", str(S),
+             "--steps", str(T), "--seed", str(SEED)], env=env))
+    rcs = []
+    for p in procs:
+        try:
+            rcs.append(p.wait(timeout=240))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    assert rcs == [0] * world, rcs
+    return np.load(out)
+
+
+def single_process_reference(oracle_mod, world: int):
+    from marllb_amd.env import make_config
+    n = world * B
+    env = oracle_mod.OracleEnv(make_config(n, S, seed=SEED, max_steps=1000), threads=2)
+    gids = np.arange(n, dtype=np.int64)
+    obs, rew = [env.reset()], []
+    for k in range(T):
+        o, r, _, _ = env.step(actions(gids, S, k))
+        obs.append(o)
+        rew.append(r)
+    return np.stack(obs), np.stack(rew)
+
+
+def test_shard_arithmetic():
+    sh = lbdist.Shard(rank=3, world=8, envs_per_rank=65536)
+    assert sh.env_id_offset == 3 * 65536 and sh.global_envs == 8 * 65536
+    assert list(sh.global_ids())[:2] == [196608, 196609]
+    assert lbdist.throughput(sh, 10, 2.0) == 8 * 65536 * 10 / 2.0
+    assert lbdist.max_over_ranks(1.5) == 1.5  # no process group: identity
+
+
+def test_two_rank_oracle_shards_equal_single_process(tmp_path, oracle_mod):
+    res = run_ranks("oracle", 2, str(tmp_path / "r.npz"))
+    assert list(res["offsets"]) == [0, B]
+    assert float(res["slowest"]) == 2.0 and float(res["rate"]) == 2 * B * T / 2.0
+    obs, rew = single_process_reference(oracle_mod, 2)
+    np.testing.assert_array_equal(res["obs"], obs)
+    np.testing.assert_array_equal(res["rew"], rew)
+
+
+@pytest.mark.gpu
+def test_two_rank_gpu_shards_equal_single_process_oracle(tmp_path, oracle_mod):
+    res = run_ranks("gpu", 2, str(tmp_path / "g.npz"))
+    obs, rew = single_process_reference(oracle_mod, 2)
+    np.testing.assert_array_equal(res["obs"], obs)
+    np.testing.assert_array_equal(res["rew"], rew)
