@@ -51,9 +51,10 @@ struct DevState {
   uint32_t* res_count;  // samples offered to the reservoirs (Algorithm R count)
   // ring [B*S*Q] of {t_complete, t_arrival}, relative us
   int2* ring;
-  // reservoirs [B*S*K]
-  float* res_fct;
-  float* res_dur;
+  // reservoirs [B*S*K]; flow completion time / duration samples in integer microseconds (the
+  // feature value of a sample is (float)us * 1e-6f seconds, us_to_seconds)
+  uint32_t* res_fct;
+  uint32_t* res_dur;
   uint32_t* res_ts;     // sample time, integer ms since episode start
   // running normalisation [B*S*11] (nullptr when disabled)
   double* norm_mean;
@@ -334,8 +335,8 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     }
     if (comp && slot >= 0) {
       const uint32_t r = (b0 + (uint32_t)smin) * (uint32_t)K + (uint32_t)slot;
-      st.res_fct[r] = (float)(tc - h_ta) * 1.0e-6f;
-      st.res_dur[r] = (float)(tc - start_c) * 1.0e-6f;
+      st.res_fct[r] = (uint32_t)(tc - h_ta);
+      st.res_dur[r] = (uint32_t)(tc - start_c);
       st.res_ts[r] = base_ms + (base_rem + (uint32_t)tc) / 1000u;
     }
     // rare: the queue is longer than the window; bring entry WL-1 (after this pop) into LDS
@@ -563,7 +564,9 @@ __device__ __forceinline__ uint32_t xor_lane_u32(uint32_t v, int lane) {
   else if constexpr (M == 4) {
     const uint32_t up = dpp_u32<0x104>(v), dn = dpp_u32<0x114>(v);
     return (lane & 4) ? dn : up;
-  } else if constexpr (M == 8) return dpp_u32<0x128>(v);
+  } else if constexpr (M == 3) return dpp_u32<0x1B>(v);   // quad_perm [3,2,1,0]
+  else if constexpr (M == 7) return dpp_u32<0x141>(v);     // row_half_mirror
+  else if constexpr (M == 8) return dpp_u32<0x128>(v);
   else return shfl_xor_u32(v, M);
 }
 template <int M>
@@ -634,55 +637,86 @@ struct ObsScratch {
   float mean[2 * MAXS], sd[2 * MAXS], md[2 * MAXS], p90[2 * MAXS], p90d[2 * MAXS];
   double swt[MAXS], svw[2 * MAXS];
   float obs[MAXS * NF];
+  uint8_t perm[8][K];           // two-pass sort: slot at each position after the first pass
 };
 
-// Sort 128 (key, payload) pairs held by the 8 lanes of a group, 16 per lane: sorted index
-// i = 16 * t + e (t = lane & 7, e = register).  Bitonic network; stages with partner distance
-// < 16 stay in registers (22 of 28), the rest exchange with lane t ^ (j / 16) by xor-shuffle.
-// Equal keys never swap, so the network is a deterministic permutation.
-__device__ __forceinline__ void bitonic128_g8(uint32_t (&key)[16], uint32_t (&pay)[16], int t) {
+// Key-only sort of 128 keys held by the 8 lanes of a group (sorted index 16 t + e), all-ascending
+// "flip" form of the bitonic network: the first step of the merge of size k pairs i with
+// i ^ (k - 1), the following steps pair i with i ^ j, and every pair leaves its minimum at the
+// lower index -- no step depends on a direction bit.  In-register pairs are one v_min + one v_max;
+// a cross-lane step fetches the partner's key by DPP and keeps med3(key, partner, lower ? 0 : ~0).
+template <int M, bool FLIP>
+__device__ __forceinline__ void cross_step_keys(uint32_t (&key)[16], int t, int lowbit) {
+  const uint32_t bound = (t & lowbit) ? 0xFFFFFFFFu : 0u;
+  uint32_t pk[16];
 #pragma unroll
-  for (int k = 2; k <= 128; k <<= 1) {
+  for (int e = 0; e < 16; ++e) pk[e] = xor_lane_u32<M>(key[FLIP ? (e ^ 15) : e], t);
 #pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      if (j < 16) {
+  for (int e = 0; e < 16; ++e) {
+    const uint32_t a = key[e], b = pk[e];
+    const uint32_t mn = a < b ? a : b, mx = a < b ? b : a;
+    const uint32_t hi = mx < bound ? mx : bound;
+    key[e] = mn > hi ? mn : hi;  // med3(a, b, bound)
+  }
+}
+
+__device__ __forceinline__ void inreg_steps_keys(uint32_t (&key)[16], int kflip, int jtop) {
+  if (kflip) {
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int f = e ^ j;
-          if (f > e) {
-            // ascending iff ((16t + e) & k) == 0
-            const bool up = (k < 16) ? ((e & k) == 0) : ((t & (k >> 4)) == 0);
-            const bool sw = up ? (key[e] > key[f]) : (key[e] < key[f]);
-            const uint32_t k0 = key[e], k1 = key[f], p0 = pay[e], p1 = pay[f];
-            key[e] = sw ? k1 : k0;
-            key[f] = sw ? k0 : k1;
-            pay[e] = sw ? p1 : p0;
-            pay[f] = sw ? p0 : p1;
-          }
-        }
-      } else {
-        const int lj = j >> 4;  // lane distance 1, 2 or 4
-        const bool lower = (t & lj) == 0;
-        const bool up = (t & (k >> 4)) == 0;
+    for (int e = 0; e < 16; ++e) {
+      const int f = e ^ (kflip - 1);
+      if (f > e) {
+        const uint32_t a = key[e], b = key[f];
+        key[e] = a < b ? a : b;
+        key[f] = a < b ? b : a;
+      }
+    }
+  }
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const uint32_t pk = lj == 1 ? xor_lane_u32<1>(key[e], t)
-                              : lj == 2 ? xor_lane_u32<2>(key[e], t) : xor_lane_u32<4>(key[e], t);
-          const uint32_t pp = lj == 1 ? xor_lane_u32<1>(pay[e], t)
-                              : lj == 2 ? xor_lane_u32<2>(pay[e], t) : xor_lane_u32<4>(pay[e], t);
-          const bool take = (lower == up) ? (pk < key[e]) : (pk > key[e]);
-          key[e] = take ? pk : key[e];
-          pay[e] = take ? pp : pay[e];
-        }
+  for (int j = jtop; j > 0; j >>= 1) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int f = e ^ j;
+      if (f > e) {
+        const uint32_t a = key[e], b = key[f];
+        key[e] = a < b ? a : b;
+        key[f] = a < b ? b : a;
       }
     }
   }
 }
 
+__device__ __forceinline__ void bitonic128_keys_g8(uint32_t (&key)[16], int t) {
+  inreg_steps_keys(key, 2, 0);
+  inreg_steps_keys(key, 4, 1);
+  inreg_steps_keys(key, 8, 2);
+  inreg_steps_keys(key, 16, 4);
+  cross_step_keys<1, true>(key, t, 1);   // k = 32
+  inreg_steps_keys(key, 0, 8);
+  cross_step_keys<3, true>(key, t, 2);   // k = 64
+  cross_step_keys<1, false>(key, t, 1);
+  inreg_steps_keys(key, 0, 8);
+  cross_step_keys<7, true>(key, t, 4);   // k = 128
+  cross_step_keys<2, false>(key, t, 2);
+  cross_step_keys<1, false>(key, t, 1);
+  inreg_steps_keys(key, 0, 8);
+}
+
+// Reservoir sample -> float seconds.  Simulator reservoirs hold integer microseconds (US); the
+// stateless features API hands in float bits.
+template <bool US>
+__device__ __forceinline__ float sample_value(uint32_t raw) {
+  if constexpr (US) return (float)raw * 1.0e-6f;
+  else return __uint_as_float(raw);
+}
+
+// us << 7 | slot must stay below the 0xFFFFFFFF filler of empty slots.
+constexpr uint32_t kPackLimit = (1u << 25) - 1u;
+
 // The 11-column observation of one env (features.py:256-286) into sc.obs, S servers.
 // Slot-order sums follow numpy exactly (reservoir.py:143-155); order statistics come from the
 // sorted keys (reservoir.py:144, 165-196).  All values >= 0, so float bits order like floats.
-template <int MAXS>
+template <int MAXS, bool US>
 __device__ __forceinline__ void observe_env(const DevState& st, const SimParams& p, size_t b,
                                             ObsScratch<MAXS>& sc, int lane) {
   const int S = p.S;
@@ -703,8 +737,8 @@ __device__ __forceinline__ void observe_env(const DevState& st, const SimParams&
       for (int h = 0; h < 2; ++h) {
         const int slot = lane + 64 * h;
         const bool v = slot < nn[u];
-        f[u][h] = v ? __float_as_uint(st.res_fct[sb * K + slot]) : 0u;
-        d[u][h] = v ? __float_as_uint(st.res_dur[sb * K + slot]) : 0u;
+        f[u][h] = v ? st.res_fct[sb * K + slot] : 0u;
+        d[u][h] = v ? st.res_dur[sb * K + slot] : 0u;
         t[u][h] = v ? st.res_ts[sb * K + slot] : 0u;
       }
     }
@@ -734,7 +768,7 @@ __device__ __forceinline__ void observe_env(const DevState& st, const SimParams&
     const int r = job0 + g;
     const int n = r < R ? sc.n[r] : 0;
     const uint32_t* a = sc.vals[r < R ? r : 0];
-    const float sum = pairwise8<float>(n, j, [&](int i) { return __uint_as_float(a[i]); });
+    const float sum = pairwise8<float>(n, j, [&](int i) { return sample_value<US>(a[i]); });
     if (j == 0 && r < R) sc.mean[r] = n > 0 ? sum / (float)n : 0.0f;
   }
   for (int job0 = 0; job0 < 3 * S; job0 += 8) {  // float64 sum w (S jobs), sum v*w (R jobs)
@@ -746,7 +780,7 @@ __device__ __forceinline__ void observe_env(const DevState& st, const SimParams&
     const uint32_t* a = sc.vals[r < R ? r : 0];
     const float* w = sc.wts[ws < S ? ws : 0];
     const double sum = pairwise8<double>(n, j, [&](int i) {
-      const double x = wonly ? 1.0 : (double)__uint_as_float(a[i]);
+      const double x = wonly ? 1.0 : (double)sample_value<US>(a[i]);
       return x * (double)w[i];
     });
     if (j == 0 && q < 3 * S) {
@@ -761,7 +795,7 @@ __device__ __forceinline__ void observe_env(const DevState& st, const SimParams&
     const uint32_t* a = sc.vals[r < R ? r : 0];
     const float m = r < R ? sc.mean[r] : 0.0f;
     const float ss = pairwise8<float>(n, j, [&](int i) {
-      const float dv = __uint_as_float(a[i]) - m;
+      const float dv = sample_value<US>(a[i]) - m;
       return dv * dv;
     });
     if (j == 0 && r < R) {
@@ -777,17 +811,55 @@ __device__ __forceinline__ void observe_env(const DevState& st, const SimParams&
     const bool act = r < R;
     const int rr = act ? r : 0;
     const int n = act ? sc.n[r] : 0;
-    uint32_t key[16], pay[16];
+    const float* wrow = sc.wts[rr >> 1];
+    uint32_t* vrow = sc.vals[rr];
     // any initial placement sorts to the same keys; ties only permute equal keys, which changes
     // neither p90 nor the weighted p90 (exact integer cumsums), so load strided (bank-free)
+    uint32_t key[16];
+    uint32_t pay[16];  // float weight bits of sorted element e
+    uint32_t vmax = 0;
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int slot = 8 * e + j;
-      const bool v = slot < n;
-      key[e] = v ? sc.vals[rr][slot] : 0xFFFFFFFFu;
-      pay[e] = v ? __float_as_uint(sc.wts[rr >> 1][slot]) : 0u;
+      key[e] = slot < n ? vrow[slot] : 0u;
+      vmax = key[e] > vmax ? key[e] : vmax;
     }
-    bitonic128_g8(key, pay, j);
+    // Key-only sorts of (sample << 7 | slot).  One pass when every sample of the wave's 8
+    // reservoirs is below 2^25 - 1 (simulator samples in us: flows under 33 s); otherwise, and
+    // always for float bits, an LSD pair of passes: low 16 bits then (high 16 bits << 7 | rank
+    // after the first pass), which orders by the full 32-bit sample.  Wave-uniform branch.
+    const bool one = US && !__any(vmax >= kPackLimit);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int slot = 8 * e + j;
+      key[e] = slot < n ? (((one ? key[e] : (key[e] & 0xFFFFu)) << 7) | (uint32_t)slot) : 0xFFFFFFFFu;
+    }
+    bitonic128_keys_g8(key, j);
+    if (one) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const bool v = 16 * j + e < n;
+        pay[e] = v ? __float_as_uint(wrow[key[e] & 127u]) : 0u;
+        key[e] = v ? key[e] >> 7 : 0xFFFFFFFFu;
+      }
+    } else {
+      uint8_t* perm = sc.perm[g];  // slot at each position of the first pass
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int pos = 16 * j + e;
+        const uint32_t slot = key[e] & 127u;
+        if (pos < n) perm[pos] = (uint8_t)slot;
+        key[e] = pos < n ? (((vrow[slot] >> 16) << 7) | (uint32_t)pos) : 0xFFFFFFFFu;
+      }
+      bitonic128_keys_g8(key, j);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const bool v = 16 * j + e < n;
+        const int slot = v ? perm[key[e] & 127u] : 0;
+        pay[e] = v ? __float_as_uint(wrow[slot]) : 0u;
+        key[e] = v ? vrow[slot] : 0xFFFFFFFFu;
+      }
+    }
     // decay-weighted p90: cumulative 2^-48 fixed-point weight in sorted order, first position
     // with 10 * cum >= 9 * total (searchsorted 'left' of 0.9 * cumsum[-1])
     uint64_t incl[16];
@@ -809,10 +881,12 @@ __device__ __forceinline__ void observe_env(const DevState& st, const SimParams&
     const uint64_t tot_incl = run + excl;
     const uint32_t tlo = (uint32_t)__shfl((int)(uint32_t)tot_incl, (lane & ~7) | 7, 64);
     const uint32_t thi = (uint32_t)__shfl((int)(uint32_t)(tot_incl >> 32), (lane & ~7) | 7, 64);
-    const uint64_t cut9 = (((uint64_t)thi << 32) | tlo) * 9u;
-    int fe = 16;
+    // 10 c >= 9 T  <=>  c >= ceil(9 T / 10) for integers (T < 2^55, so 9 T fits)
+    const uint64_t thr = ((((uint64_t)thi << 32) | tlo) * 9u + 9u) / 10u;
+    const uint64_t thr_lane = thr > excl ? thr - excl : 0u;  // this lane's share of the threshold
+    int fe = 0;  // first e with excl + incl[e] >= thr (incl is non-decreasing): count of those below
 #pragma unroll
-    for (int e = 15; e >= 0; --e) fe = ((excl + incl[e]) * 10u >= cut9) ? e : fe;
+    for (int e = 0; e < 16; ++e) fe += incl[e] < thr_lane ? 1 : 0;
     const uint64_t m = __ballot(fe < 16);
     const uint32_t gm = (uint32_t)(m >> (lane & ~7)) & 0xFFu;
     const int tstar = gm ? __builtin_ctz(gm) : 7;
@@ -831,7 +905,7 @@ __device__ __forceinline__ void observe_env(const DevState& st, const SimParams&
         const float fl = floorf(hidx);
         const int lo = (int)fl;
         const float gg = hidx - fl;
-        auto sorted = [&](int pos) { return __uint_as_float(sc.vals[r][(pos & 15) * 8 + (pos >> 4)]); };
+        auto sorted = [&](int pos) { return sample_value<US>(sc.vals[r][(pos & 15) * 8 + (pos >> 4)]); };
         const float va = sorted(lo);
         const float vb = sorted(lo + 1 < n ? lo + 1 : lo);
         const float diff = vb - va;
@@ -958,8 +1032,13 @@ struct ObsOutputs {
   double* ep_ret;
 };
 
+// Waves per SIMD the LDS footprint allows (ObsScratch: 8 / 15 / 29 KB); at S <= 4 this caps
+// the kernel at 96 VGPRs.
+template <int MAXS>
+constexpr int kObsWaves = MAXS <= 4 ? 5 : (MAXS <= 8 ? 3 : 2);
+
 template <int MAXS, int MODE>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64, kObsWaves<MAXS>)
     observe_kernel(DevState st, SimParams p, ObsOutputs out, const uint8_t* reset_mask) {
   constexpr int mode = MODE;
   const size_t b = blockIdx.x;
@@ -967,7 +1046,7 @@ __global__ void __launch_bounds__(64)
   if (mode == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
   __shared__ ObsScratch<MAXS> sc;
   const int S = p.S;
-  observe_env<MAXS>(st, p, b, sc, lane);
+  observe_env<MAXS, true>(st, p, b, sc, lane);
   const float* s_obs = sc.obs;
 
   if (mode == kModeStep && lane == 0) {
@@ -1021,8 +1100,8 @@ __global__ void __launch_bounds__(64)
   __shared__ ObsScratch<4> sc;
   const int S = (int)(n - r0 < 4 ? n - r0 : 4);
   DevState st{};
-  st.res_fct = const_cast<float*>(values) + r0 * K;
-  st.res_dur = const_cast<float*>(values) + r0 * K;
+  st.res_fct = reinterpret_cast<uint32_t*>(const_cast<float*>(values)) + r0 * K;
+  st.res_dur = st.res_fct;
   st.res_ts = const_cast<uint32_t*>(ts) + r0 * K;
   st.res_count = const_cast<uint32_t*>(counts) + r0;
   __shared__ uint32_t hc0[4];
@@ -1032,7 +1111,7 @@ __global__ void __launch_bounds__(64)
   p.S = S;
   p.decay_c = decay_c;
   __syncthreads();
-  observe_env<4>(st, p, 0, sc, lane);
+  observe_env<4, false>(st, p, 0, sc, lane);
   for (int e = lane; e < S * 5; e += 64) {
     const int s = e / 5, f = e - s * 5;
     out[(r0 + s) * 5 + f] = sc.obs[s * NF + 1 + f];

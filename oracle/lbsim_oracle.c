@@ -293,7 +293,8 @@ typedef struct oracle {
   double* ep_return;
   uint32_t* hc; int32_t* last_tc; uint32_t* res_count;
   int32_t* ring; /* [B*S*Q][2] = {t_complete, t_arrival} */
-  float* res_fct; float* res_dur; uint32_t* res_ts;
+  uint32_t* res_fct; uint32_t* res_dur; /* integer microseconds; value = (float)us * 1e-6f */
+  uint32_t* res_ts;
   double* norm_mean; double* norm_std;
 } oracle_t;
 
@@ -379,7 +380,10 @@ static void ring_set(oracle_t* o, size_t sb, int head, int cnt) {
 }
 
 /* Algorithm R insert of one completion into both reservoirs of server s (shared decision). */
-static void reservoir_add(env_ctx* e, int s, float fct, float dur, uint32_t ts_ms) {
+/* A reservoir sample in seconds from its integer-microsecond form (env.py reports seconds). */
+static float us_to_seconds(uint32_t us) { return (float)us * 1.0e-6f; }
+
+static void reservoir_add(env_ctx* e, int s, uint32_t fct, uint32_t dur, uint32_t ts_ms) {
   oracle_t* o = e->o;
   const size_t sb = e->b * (size_t)o->S + (size_t)s;
   const uint32_t c = o->res_count[sb];
@@ -415,8 +419,8 @@ static void pop_until(env_ctx* e, int s, int32_t t, uint64_t base_us, double den
     const int32_t tc = ent[0], ta = ent[1];
     if (tc > t) break;
     const int32_t start = ta > o->last_tc[sb] ? ta : o->last_tc[sb];
-    const float fct = (float)(tc - ta) * 1.0e-6f;
-    const float dur = (float)(tc - start) * 1.0e-6f;
+    const uint32_t fct = (uint32_t)(tc - ta);   /* the sample is (float)fct * 1e-6f seconds */
+    const uint32_t dur = (uint32_t)(tc - start);
     o->last_tc[sb] = tc;
     const uint32_t ts_ms = (uint32_t)((base_us + (uint64_t)(int64_t)tc) / 1000u);
     reservoir_add(e, s, fct, dur, ts_ms);
@@ -565,9 +569,13 @@ static void observe(oracle_t* o, size_t b, float* obs_out, float* reward_out, ui
     float w[K];
     uint64_t wq[K];
     slot_weights(o->res_ts + sb * K, n, o->decay_c, w, wq);
-    float ff[5], fd[5];
-    features_one(o->res_fct + sb * K, w, wq, n, ff);
-    features_one(o->res_dur + sb * K, w, wq, n, fd);
+    float ff[5], fd[5], vf[K], vd[K];
+    for (int i = 0; i < n; ++i) {
+      vf[i] = us_to_seconds(o->res_fct[sb * K + i]);
+      vd[i] = us_to_seconds(o->res_dur[sb * K + i]);
+    }
+    features_one(vf, w, wq, n, ff);
+    features_one(vd, w, wq, n, fd);
     raw[s * NF + 0] = (float)ring_count(o, sb);
     for (int f = 0; f < 5; ++f) { raw[s * NF + 1 + f] = ff[f]; raw[s * NF + 6 + f] = fd[f]; }
   }

@@ -11,7 +11,7 @@ def sections(B, S, Q, normalize):
            ("clock", np.uint32, B), ("ep_step", np.int32, B), ("dropped", np.uint32, B),
            ("norm_count", np.int32, B), ("ep_return", np.float64, B), ("hc", np.uint32, BS),
            ("last_tc", np.int32, BS), ("res_count", np.uint32, BS), ("ring", np.int32, BS * Q * 2),
-           ("res_fct", np.float32, BS * K), ("res_dur", np.float32, BS * K),
+           ("res_fct", np.uint32, BS * K), ("res_dur", np.uint32, BS * K),
            ("res_ts", np.uint32, BS * K)]
     if normalize:
         out += [("norm_mean", np.float64, BS * NF), ("norm_std", np.float64, BS * NF)]

@@ -88,6 +88,9 @@ CONFIGS = [
     dict(B=40, S=6, kw={"reward_metric": "variance", "reward_field": "fct_mean",
                         "discrete_weights": [0.25, 1.0, 4.0, 9.0], "queue_capacity": 64,
                         "max_steps": 7}),
+    # slow servers, 5 s steps: flows wait > 2^25 us (33 s), so observe takes the two-pass sort
+    dict(B=48, S=4, kw={"server_rates": [1.0, 1.0, 1.5, 2.0], "arrival_rate": 20.0,
+                        "step_interval": 5.0, "queue_capacity": 64}),
 ]
 
 

@@ -1,0 +1,48 @@
+"""The GPU parity cases (tests/test_gpu_parity.py CONFIGS) reach the rare code paths of the
+kernels -- checked here on the CPU with the oracle, which follows the same state layout:
+  * reservoir samples >= 2^25 - 1 us  -> observe's two-pass (LSD) key sort;
+  * queues longer than the dynamics kernel's LDS window -> HBM ring refills;
+  * arrivals dropped because every queue is full.
+"""
+import numpy as np
+import pytest
+
+from tests import statelayout
+
+pytest.importorskip("torch")
+from tests.test_gpu_parity import CONFIGS, _actions  # noqa: E402
+
+PACK_LIMIT = (1 << 25) - 1
+
+
+def window(S):
+    return 8 if S <= 4 else (4 if S <= 8 else 2)
+
+
+def run_case(oracle_mod, case, steps=12):
+    from marllb_amd.env import make_config
+    c = CONFIGS[case]
+    B, S, kw = c["B"], c["S"], dict(c["kw"])
+    kw.setdefault("seed", 1000 + case)
+    cfg = make_config(B, S, **kw)
+    ora = oracle_mod.OracleEnv(cfg, threads=4)
+    ora.reset()
+    rng = np.random.default_rng(case)
+    max_q = 0
+    for _ in range(steps):
+        ora.step(_actions(rng, B, S, kw))
+        st = statelayout.parse(ora.state_bytes(), B, S, cfg.queue_capacity, bool(cfg.normalize_obs))
+        max_q = max(max_q, int((st["hc"] >> 16).max()))
+    return st, max_q, S
+
+
+def test_parity_cases_cover_rare_paths(oracle_mod):
+    two_pass = overflow = dropped = False
+    for case in range(len(CONFIGS)):
+        st, max_q, S = run_case(oracle_mod, case)
+        two_pass |= bool(max(st["res_fct"].max(), st["res_dur"].max()) >= PACK_LIMIT)
+        overflow |= max_q > window(S)
+        dropped |= bool(st["dropped"].sum() > 0)
+    assert two_pass, "no parity case produces a sample >= 2^25 - 1 us"
+    assert overflow, "no parity case queues more flows than the LDS window"
+    assert dropped, "no parity case drops arrivals"
