@@ -63,12 +63,14 @@ enum lbsim_reward_metric {
   LBSIM_METRIC_GINI = 8
 };
 
-/* node.c:393-441: LB_SED, LB_SED2 (power of two), LB_LSQ, LB_LSQ2 */
+/* node.c:393-441: LB_SED, LB_SED2 (power of two), LB_LSQ, LB_LSQ2; node.c:442-460 LB_ALIAS with
+ * the table of gen_alias (src/lb/shm_proxy.py:127-146) over the action weights */
 enum lbsim_assign_policy {
   LBSIM_POLICY_SED = 0,
   LBSIM_POLICY_SED2 = 1,
   LBSIM_POLICY_LSQ = 2,
-  LBSIM_POLICY_LSQ2 = 3
+  LBSIM_POLICY_LSQ2 = 3,
+  LBSIM_POLICY_ALIAS = 4
 };
 
 enum lbsim_arrival_source { LBSIM_ARRIVAL_POISSON = 0 };
@@ -181,6 +183,14 @@ int lbsim_reward(const lbsim_config_t* cfg, const float* obs, int64_t n, float* 
  * feats_out[r, 5] = {mean, p90, std, mean_decay, p90_decay} (reservoir.py:105-196). */
 int lbsim_reservoir_features(const float* values, const uint32_t* ts_ms, const uint32_t* counts,
                              int64_t n, float decay_factor, float* feats_out, void* stream);
+
+/* Stateless: n alias tables of S weights each (weights[n, S] f32, device pointers): gen_alias
+ * (src/lb/shm_proxy.py:127-146) over the weights > 0 of each row, as the ALIAS policy builds it
+ * every step -> odd_out[n, S] (float32, as packed into shm.h alias_t), alias_out[n, S] (position
+ * in the row's active list), active_out[n, S] (server of each active position; -1 past the end).
+ * Entries past a row's active count are (1, 0, -1). */
+int lbsim_alias_tables(const float* weights, int64_t n, int S, float* odd_out, int32_t* alias_out,
+                       int32_t* active_out, void* stream);
 
 /*
  * Kernel timing: between lbsim_profile_begin and lbsim_profile_end every kernel launch of this

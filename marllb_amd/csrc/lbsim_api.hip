@@ -98,7 +98,7 @@ int validate(const lbsim_config_t* c, char* msg, size_t n) {
   if ((int64_t)std::llround((double)c->step_interval * 1e6) < 1)
     return bad("step_interval must be >= 1 us");
   if (c->max_steps < 1) return bad("max_steps must be >= 1");
-  if (c->assign_policy < LBSIM_POLICY_SED || c->assign_policy > LBSIM_POLICY_LSQ2)
+  if (c->assign_policy < LBSIM_POLICY_SED || c->assign_policy > LBSIM_POLICY_ALIAS)
     return bad("unknown assign_policy %d", c->assign_policy);
   if (c->arrival_source != LBSIM_ARRIVAL_POISSON) return bad("unknown arrival_source");
   if (!(c->arrival_rate >= 0.1f) || !(c->arrival_rate <= 1.0e6f))
@@ -204,19 +204,32 @@ struct ProfScope {
   }
 };
 
+template <int MAXS, int MODE, int POLICY>
+void launch_dyn(lbsim_t* h, const void* action, int dtype, int32_t* assign, const uint8_t* mask,
+                hipStream_t stream) {
+  const dim3 block(64), grid((unsigned)((h->B + 63) / 64));
+  hipLaunchKernelGGL((dynamics_kernel<MAXS, MODE, POLICY>), grid, block, 0, stream, h->st, h->prm,
+                     action, dtype, assign, mask);
+}
+
+template <int MAXS, int MODE>
+void launch_dyn_policy(lbsim_t* h, const void* action, int dtype, int32_t* assign,
+                       const uint8_t* mask, hipStream_t stream) {
+  switch (h->prm.policy) {
+    case LBSIM_POLICY_SED: launch_dyn<MAXS, MODE, 0>(h, action, dtype, assign, mask, stream); break;
+    case LBSIM_POLICY_SED2: launch_dyn<MAXS, MODE, 1>(h, action, dtype, assign, mask, stream); break;
+    case LBSIM_POLICY_LSQ: launch_dyn<MAXS, MODE, 2>(h, action, dtype, assign, mask, stream); break;
+    case LBSIM_POLICY_LSQ2: launch_dyn<MAXS, MODE, 3>(h, action, dtype, assign, mask, stream); break;
+    default: launch_dyn<MAXS, MODE, 4>(h, action, dtype, assign, mask, stream); break;
+  }
+}
+
 template <int MODE>
 void launch_dynamics_t(lbsim_t* h, const void* action, int dtype, int32_t* assign,
                        const uint8_t* mask, hipStream_t stream) {
-  const dim3 block(64), grid((unsigned)((h->B + 63) / 64));
-  if (h->S <= 4)
-    hipLaunchKernelGGL((dynamics_kernel<4, MODE>), grid, block, 0, stream, h->st, h->prm, action,
-                       dtype, assign, mask);
-  else if (h->S <= 8)
-    hipLaunchKernelGGL((dynamics_kernel<8, MODE>), grid, block, 0, stream, h->st, h->prm, action,
-                       dtype, assign, mask);
-  else
-    hipLaunchKernelGGL((dynamics_kernel<16, MODE>), grid, block, 0, stream, h->st, h->prm, action,
-                       dtype, assign, mask);
+  if (h->S <= 4) launch_dyn_policy<4, MODE>(h, action, dtype, assign, mask, stream);
+  else if (h->S <= 8) launch_dyn_policy<8, MODE>(h, action, dtype, assign, mask, stream);
+  else launch_dyn_policy<16, MODE>(h, action, dtype, assign, mask, stream);
 }
 
 int launch_dynamics(lbsim_t* h, const void* action, int dtype, int32_t* assign,
@@ -428,6 +441,16 @@ int lbsim_reward(const lbsim_config_t* cfg, const float* obs, int64_t n, float* 
   hipLaunchKernelGGL(reward_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, obs, n, cfg->num_servers, cfg->reward_metric,
                      cfg->reward_field, reward_out);
+  return hipGetLastError() == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
+}
+
+int lbsim_alias_tables(const float* weights, int64_t n, int S, float* odd_out, int32_t* alias_out,
+                       int32_t* active_out, void* stream) {
+  if (n < 0 || S < 1 || S > LBSIM_MAX_SERVERS) return LBSIM_EINVAL;
+  if (n == 0) return LBSIM_OK;
+  if (!weights || !odd_out || !alias_out || !active_out) return LBSIM_EINVAL;
+  hipLaunchKernelGGL(alias_tables_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
+                     (hipStream_t)stream, weights, n, S, odd_out, alias_out, active_out);
   return hipGetLastError() == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
 }
 

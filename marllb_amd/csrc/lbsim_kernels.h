@@ -137,10 +137,77 @@ __device__ __forceinline__ int2* qslot(const Lds& l, int s, int i) {
   return l.q + ((s * Win<MAXS>::WL + i) * 64 + l.lane);
 }
 
+constexpr int kPolicyAlias = 4;
+
 // SED score (n_flow_on + 1) / (1e-9 + w) in double, stored as f32 (node.c:393-399); LSQ: n.
+// (ALIAS keeps its table in the den fields and uses no score.)
 __device__ __forceinline__ float policy_score(int policy, int32_t cnt, double den) {
   if (policy == 2 /*LSQ*/ || policy == 3 /*LSQ2*/) return (float)cnt;
+  if (policy == kPolicyAlias) return 0.0f;
   return (float)((double)(cnt + 1) / den);
+}
+
+template <int MAXS, typename T>
+__device__ __forceinline__ T sel(const T (&a)[MAXS], int i) {
+  T v = a[0];
+#pragma unroll
+  for (int k = 1; k < MAXS; ++k) v = (k == i) ? a[k] : v;
+  return v;
+}
+
+// ALIAS table of this step (node.c:442-460 over gen_alias, src/lb/shm_proxy.py:127-146): the
+// servers with weight > 0 in index order (register_as_weights, shm_proxy.py:642-648) are the
+// active list; gen_alias runs in float64 exactly as the reference's Python (sequential sum,
+// avg = sum / (n + 1e-6), p = w / (avg + 1e-6), small / big generators in index order, a big
+// reduced below 1 becomes the next small).  Stored per active position k in the lane's den
+// fields: F_DEN_LO = odd (f32 bits, the alias_t float), F_DEN_HI = alias | server << 8.
+// Returns the active count.
+template <int MAXS>
+__device__ int build_alias(const float (&w)[MAXS], int S, const Lds& l) {
+  int n = 0;
+  double sum = 0.0;
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) {
+    if (s < S && w[s] > 0.0f) {
+      fld<MAXS>(l, F_DEN_LO, n) = (int32_t)0x3f800000;  // (1, 0)
+      fld<MAXS>(l, F_DEN_HI, n) = s << 8;
+      sum += (double)w[s];
+      ++n;
+    }
+  }
+  const double avg = sum / ((double)n + 1e-6);
+  auto wk = [&](int k) { return (double)sel<MAXS>(w, fld<MAXS>(l, F_DEN_HI, k) >> 8); };
+  int si = 0, bi = 0, sk = -1, bk = -1;
+  double sp = 0.0, bp = 0.0;
+  auto next_small = [&]() {
+    while (si < n && !(wk(si) < avg)) ++si;
+    if (si < n) { sk = si; sp = wk(si) / (avg + 1e-6); ++si; } else { sk = -1; }
+  };
+  auto next_big = [&]() {
+    while (bi < n && !(wk(bi) >= avg)) ++bi;
+    if (bi < n) { bk = bi; bp = wk(bi) / (avg + 1e-6); ++bi; } else { bk = -1; }
+  };
+  next_small();
+  next_big();
+  while (bk >= 0 && sk >= 0) {
+    fld<MAXS>(l, F_DEN_LO, sk) = (int32_t)__float_as_uint((float)sp);
+    fld<MAXS>(l, F_DEN_HI, sk) = (fld<MAXS>(l, F_DEN_HI, sk) & ~0xFF) | bk;
+    bp = bp - (1.0 - sp);
+    if (bp < 1.0) { sk = bk; sp = bp; next_big(); } else { next_small(); }
+  }
+  return n;
+}
+
+// ALIAS pick for an arrival with hash word u: rand_num = U * n (U = 24 bits of u, in [0, 1)),
+// bucket = (int)rand_num, the alias if rand_num - bucket > odd[bucket] (node.c:449-460).
+template <int MAXS>
+__device__ __forceinline__ int alias_pick(const Lds& l, int n, uint32_t u) {
+  const float rn = (float)(u >> 8) * 5.9604644775390625e-8f * (float)n;
+  int bucket = (int)rn;
+  bucket = bucket > n - 1 ? n - 1 : bucket;
+  const float odd = __uint_as_float((uint32_t)fld<MAXS>(l, F_DEN_LO, bucket));
+  const int k = (rn - (float)bucket) > odd ? (fld<MAXS>(l, F_DEN_HI, bucket) & 0xFF) : bucket;
+  return fld<MAXS>(l, F_DEN_HI, k) >> 8;
 }
 
 // Arrival draw for one arrival index: gap to it, its work, its two hash words.
@@ -228,9 +295,9 @@ __device__ __forceinline__ void clear_servers(const SimParams& p, LaneState<MAXS
 // completions are processed in t_complete order before any arrival at the same or a later time —
 // the order the oracle (server by server) produces — so every reservoir sees the same insert
 // sequence and the state is bit-identical.
-template <int MAXS>
+template <int MAXS, int POLICY>
 __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
-                                         LaneState<MAXS>& L, uint32_t b, const float* w,
+                                         LaneState<MAXS>& L, uint32_t b, const float (&w)[MAXS],
                                          const Lds& l) {
   constexpr int WL = LaneState<MAXS>::WL;
   const int S = p.S, Q = p.Q;
@@ -239,15 +306,21 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
   const uint64_t base_us = (uint64_t)L.clock * (uint64_t)dt;
   const uint32_t base_ms = (uint32_t)(base_us / 1000u);
   const uint32_t base_rem = (uint32_t)(base_us - (uint64_t)base_ms * 1000u);
-  const bool two_choice = (p.policy == 1 || p.policy == 3);
+  constexpr bool two_choice = (POLICY == 1 || POLICY == 3);
+  constexpr bool alias = POLICY == kPolicyAlias;
   const uint32_t b0 = b * (uint32_t)S;
+  int n_alias = 0;
+  if constexpr (alias) {
+    n_alias = build_alias<MAXS>(w, S, l);
+  } else {
 #pragma unroll
-  for (int s = 0; s < MAXS; ++s) {
-    if (s < S) {
-      const double den = (double)w[s] + 1e-9;
-      fld<MAXS>(l, F_DEN_LO, s) = (int32_t)__double2loint(den);
-      fld<MAXS>(l, F_DEN_HI, s) = (int32_t)__double2hiint(den);
-      L.score[s] = policy_score(p.policy, L.cnt[s], den);
+    for (int s = 0; s < MAXS; ++s) {
+      if (s < S) {
+        const double den = (double)w[s] + 1e-9;
+        fld<MAXS>(l, F_DEN_LO, s) = (int32_t)__double2loint(den);
+        fld<MAXS>(l, F_DEN_HI, s) = (int32_t)__double2hiint(den);
+        L.score[s] = policy_score(POLICY, L.cnt[s], den);
+      }
     }
   }
   for (;;) {
@@ -269,7 +342,12 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     // ---- arrival: choose a server (node.c:388-441); full servers are not eligible
     const int32_t ta = L.next_arr;
     int chosen = -1;
-    if (two_choice) {  // SED2 / LSQ2: two uniform candidates, keep the second if strictly better
+    if constexpr (alias) {  // full server: the flow is dropped (ALIAS has no eligibility test)
+      if (n_alias > 0) {
+        const int a = alias_pick<MAXS>(l, n_alias, L.u2);
+        chosen = sel<MAXS>(L.cnt, a) < Q ? a : -1;
+      }
+    } else if constexpr (two_choice) {  // SED2 / LSQ2: two candidates, keep the second if strictly better
       const int h1 = (int)(((uint64_t)L.u2 * (uint64_t)S) >> 32);
       const int h2 = (int)(((uint64_t)L.u3 * (uint64_t)S) >> 32);
       float s1 = 0.f, s2 = 0.f;
@@ -371,7 +449,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
 
     // ---- write back the changed server
     const int32_t n_cs = comp ? c_cnt - 1 : c_cnt + 1;
-    const float sc_new = policy_score(p.policy, n_cs, c_den);
+    const float sc_new = policy_score(POLICY, n_cs, c_den);
     if (comp) {
       fld<MAXS>(l, F_RCNT, csi) = (int32_t)(cres != 0xFFFFFFFFu ? cres + 1u : cres);
       fld<MAXS>(l, F_LAST, csi) = tc;
@@ -479,7 +557,8 @@ __device__ __forceinline__ float action_weight(const SimParams& p, const void* a
 }
 
 // MODE is a template parameter so step and reset launches are separate kernels in profiles.
-template <int MAXS, int MODE>
+// POLICY is a template parameter: each assignment rule gets its own straight-line event loop.
+template <int MAXS, int MODE, int POLICY>
 __global__ void __launch_bounds__(64)
     dynamics_kernel(DevState st, SimParams p, const void* action, int action_dtype,
                     int32_t* assign_out, const uint8_t* reset_mask) {
@@ -504,7 +583,7 @@ __global__ void __launch_bounds__(64)
     float w1[MAXS];
 #pragma unroll
     for (int s = 0; s < MAXS; ++s) w1[s] = 1.0f;
-    for (int k = 0; k < p.warmup_steps; ++k) sim_step<MAXS>(st, p, L, b, w1, l);
+    for (int k = 0; k < p.warmup_steps; ++k) sim_step<MAXS, POLICY>(st, p, L, b, w1, l);
     st.ep_step[b] = 0;
     st.ep_return[b] = 0.0;
     store_servers<MAXS>(st, p, L, b, l, nullptr);
@@ -522,7 +601,7 @@ __global__ void __launch_bounds__(64)
 #pragma unroll
     for (int s = 0; s < MAXS; ++s)
       w[s] = (s < S) ? action_weight(p, action, action_dtype, (size_t)b * S + (size_t)s) : 1.0f;
-    sim_step<MAXS>(st, p, L, b, w, l);
+    sim_step<MAXS, POLICY>(st, p, L, b, w, l);
     store_servers<MAXS>(st, p, L, b, l, assign_out);
   }
   st.episode[b] = L.episode;
@@ -1115,6 +1194,27 @@ __global__ void __launch_bounds__(64)
   for (int e = lane; e < S * 5; e += 64) {
     const int s = e / 5, f = e - s * 5;
     out[(r0 + s) * 5 + f] = sc.obs[s * NF + 1 + f];
+  }
+}
+
+// ALIAS tables of caller-given weight rows, one lane per row (the per-step build of
+// dynamics_kernel, exposed for the gen_alias parity test).
+__global__ void __launch_bounds__(64)
+    alias_tables_kernel(const float* weights, int64_t n, int S, float* odd_out,
+                        int32_t* alias_out, int32_t* active_out) {
+  __shared__ int32_t fields[F_NUM * MAX_S * 64];
+  const Lds l{nullptr, fields, (int)threadIdx.x};
+  const int64_t r = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (r >= n) return;
+  float w[MAX_S];
+#pragma unroll
+  for (int s = 0; s < MAX_S; ++s) w[s] = s < S ? weights[r * S + s] : 0.0f;
+  const int na = build_alias<MAX_S>(w, S, l);
+  for (int k = 0; k < S; ++k) {
+    const bool v = k < na;
+    odd_out[r * S + k] = v ? __uint_as_float((uint32_t)fld<MAX_S>(l, F_DEN_LO, k)) : 1.0f;
+    alias_out[r * S + k] = v ? (fld<MAX_S>(l, F_DEN_HI, k) & 0xFF) : 0;
+    active_out[r * S + k] = v ? (fld<MAX_S>(l, F_DEN_HI, k) >> 8) : -1;
   }
 }
 

@@ -55,6 +55,7 @@ def load() -> ctypes.CDLL:
         "oracle_step": (ctypes.c_int, [_P, _P, ctypes.c_int, _P, _P, _P, _P]),
         "oracle_episode_stats": (None, [_P, _P, _P]),
         "oracle_normalize": (None, [_P, ctypes.c_int, _P, _P, _P, _P]),
+        "oracle_gen_alias": (None, [_P, ctypes.c_int, _P, _P]),
         "oracle_algr_slot": (ctypes.c_long, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                              ctypes.c_uint32, _P]),
     }
@@ -69,6 +70,15 @@ def load() -> ctypes.CDLL:
 def ptr(a: np.ndarray) -> int:
     assert a.flags["C_CONTIGUOUS"]
     return a.ctypes.data
+
+
+def gen_alias(weights):
+    """oracle_gen_alias: (odd float64[n], alias int32[n]) of gen_alias (shm_proxy.py:127-146)."""
+    w = np.ascontiguousarray(weights, np.float32)
+    odd = np.zeros(len(w), np.float64)
+    alias = np.zeros(len(w), np.int32)
+    load().oracle_gen_alias(ptr(w), len(w), ptr(odd), ptr(alias))
+    return odd, alias
 
 
 def philox(ctr, key) -> np.ndarray:

@@ -373,6 +373,43 @@ static float score_of(int policy, int32_t cnt, double den) {
   return (float)((double)(cnt + 1) / den);
 }
 
+/* gen_alias (src/lb/shm_proxy.py:127-146) on n weights, in float64 as the reference's Python:
+ * avg = sum(w) / (n + 1e-6) (sequential sum), p_i = w_i / (avg + 1e-6); the "small" (w < avg)
+ * and "big" (w >= avg) generators walk the weights in index order; a big reduced below 1 becomes
+ * the next small.  Unassigned entries keep (1, 0).  odd_out in float64 (the value the reference
+ * packs into shm.h alias_t as float32). */
+void oracle_gen_alias(const float* w, int n, double* odd_out, int32_t* alias_out) {
+  double sum = 0.0;
+  for (int i = 0; i < n; ++i) sum += (double)w[i];
+  const double avg = sum / ((double)n + 1e-6);
+  for (int i = 0; i < n; ++i) { odd_out[i] = 1.0; alias_out[i] = 0; }
+  int si = 0, bi = 0, sk = -1, bk = -1;
+  double sp = 0.0, bp = 0.0;
+#define NEXT_SMALL()                                                    \
+  do {                                                                  \
+    while (si < n && !((double)w[si] < avg)) ++si;                      \
+    if (si < n) { sk = si; sp = (double)w[si] / (avg + 1e-6); ++si; }   \
+    else sk = -1;                                                       \
+  } while (0)
+#define NEXT_BIG()                                                      \
+  do {                                                                  \
+    while (bi < n && !((double)w[bi] >= avg)) ++bi;                     \
+    if (bi < n) { bk = bi; bp = (double)w[bi] / (avg + 1e-6); ++bi; }   \
+    else bk = -1;                                                       \
+  } while (0)
+  NEXT_SMALL();
+  NEXT_BIG();
+  while (bk >= 0 && sk >= 0) {
+    odd_out[sk] = sp;
+    alias_out[sk] = bk;
+    bp = bp - (1.0 - sp);
+    if (bp < 1.0) { sk = bk; sp = bp; NEXT_BIG(); }
+    else NEXT_SMALL();
+  }
+#undef NEXT_SMALL
+#undef NEXT_BIG
+}
+
 static int ring_head(const oracle_t* o, size_t sb) { return (int)(o->hc[sb] & 0xFFFFu); }
 static int ring_count(const oracle_t* o, size_t sb) { return (int)(o->hc[sb] >> 16); }
 static void ring_set(oracle_t* o, size_t sb, int head, int cnt) {
@@ -452,6 +489,18 @@ static void sim_step(env_ctx* e, const float* w) {
   const uint64_t base_us = (uint64_t)o->clock[b] * (uint64_t)o->dt_us;
   double den[LBSIM_MAX_SERVERS];
   for (int s = 0; s < S; ++s) den[s] = (double)w[s] + 1e-9;
+  /* ALIAS: the table over the servers with weight > 0 (register_as_weights, shm_proxy.py:642-648),
+   * alias indices are positions in that active list (node.c:449-460 as_indexes) */
+  int n_act = 0, act[LBSIM_MAX_SERVERS];
+  float w_act[LBSIM_MAX_SERVERS], odd[LBSIM_MAX_SERVERS];
+  int32_t alias[LBSIM_MAX_SERVERS];
+  if (policy == LBSIM_POLICY_ALIAS) {
+    for (int s = 0; s < S; ++s)
+      if (w[s] > 0.0f) { act[n_act] = s; w_act[n_act] = w[s]; ++n_act; }
+    double odd64[LBSIM_MAX_SERVERS];
+    oracle_gen_alias(w_act, n_act, odd64, alias);
+    for (int k = 0; k < n_act; ++k) odd[k] = (float)odd64[k];
+  }
 
   while (o->next_arr[b] < o->dt_us) {
     const int32_t ta = o->next_arr[b];
@@ -463,7 +512,18 @@ static void sim_step(env_ctx* e, const float* w) {
       sc[s] = score_of(policy, cnt[s], den[s]);
     }
     int chosen = -1;
-    if (policy == LBSIM_POLICY_SED2 || policy == LBSIM_POLICY_LSQ2) {
+    if (policy == LBSIM_POLICY_ALIAS) {
+      /* node.c:442-460: rand_num = U * n, bucket = (int)rand_num, alias if the fraction exceeds
+       * odd[bucket]; U = 24 bits of the arrival's hash word (never 1, unlike rand()/RAND_MAX).
+       * A full server drops the flow (ALIAS has no eligibility test). */
+      if (n_act > 0) {
+        const float rn = (float)(o->next_u2[b] >> 8) * 5.9604644775390625e-8f * (float)n_act;
+        int bucket = (int)rn;
+        if (bucket > n_act - 1) bucket = n_act - 1;
+        const int k = (rn - (float)bucket) > odd[bucket] ? alias[bucket] : bucket;
+        if (cnt[act[k]] < Q) chosen = act[k];
+      }
+    } else if (policy == LBSIM_POLICY_SED2 || policy == LBSIM_POLICY_LSQ2) {
       /* node.c:409-417 / 433-441: two candidates, keep the second only if strictly better */
       const int h1 = (int)(((uint64_t)o->next_u2[b] * (uint64_t)S) >> 32);
       const int h2 = (int)(((uint64_t)o->next_u3[b] * (uint64_t)S) >> 32);

@@ -17,7 +17,7 @@ Reference entry points exercised (paths relative to the reference root):
   LoadBalanceEnv.reset/step bookkeeping env.py:186-286
   gen_alias                            src/lb/shm_proxy.py:127-146 (weights -> alias table)
 
-Usage:  python tests/golden/gen_golden.py [--reference /root/reference]
+Usage:  python tests/golden/gen_golden.py [--reference /root/reference] [--only alias]
 """
 import argparse
 import json
@@ -142,10 +142,54 @@ def reward_cases(rng):
     return groups
 
 
+# ------------------------------------------------------------------ alias tables
+def alias_cases(rng):
+    """Weight vectors as the env produces them (float32 action weights, all > 0): random, the
+    discrete levels, ties with the mean, one dominant server, n = 1..16."""
+    cases = []
+    for n in range(1, 17):
+        for _ in range(6):
+            cases.append(rng.uniform(0.1, 10.0, n).astype(np.float32))
+        cases.append(rng.choice(np.array([1.0, 1.5, 2.0], np.float32), n))
+        cases.append(np.full(n, 1.5, np.float32))
+    cases += [np.array(w, np.float32) for w in (
+        [1, 1, 1, 1, 2, 2, 2],            # SURVEY §8a a13 worked example
+        [0.1] * 15 + [10.0], [10.0] + [0.1] * 15, [1, 2, 3, 4], [4, 3, 2, 1],
+        [1, 1, 1, 5], [0.1, 0.1, 10, 10], [2, 2, 2, 6], [1.5, 1.0, 2.0, 1.5])]
+    return cases
+
+
+def alias_goldens(root, rng):
+    """gen_alias (src/lb/shm_proxy.py:127-146) imported in place; the module reads
+    ./shm_layout.json at import time, hence the chdir."""
+    import importlib
+    lb = os.path.join(root, "src/lb")
+    cwd = os.getcwd()
+    sys.path.insert(0, lb)
+    os.chdir(lb)
+    try:
+        shm_proxy = importlib.import_module("shm_proxy")
+    finally:
+        os.chdir(cwd)
+    out = []
+    for w in alias_cases(rng):
+        weights = [float(x) for x in w]  # python floats of the float32 weights
+        tab = shm_proxy.gen_alias(weights)
+        out.append({"weights": weights, "odd": [float(a[0]) for a in tab],
+                    "alias": [int(a[1]) for a in tab]})
+    with open(os.path.join(HERE, "alias.json"), "w") as fh:
+        json.dump({"source": "src/lb/shm_proxy.py:127-146 gen_alias", "cases": out}, fh)
+    print(f"wrote alias.json ({len(out)} tables)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
+    ap.add_argument("--only", choices=["alias"], default=None)
     args = ap.parse_args()
+    if args.only == "alias":
+        alias_goldens(args.reference, np.random.default_rng(20260110))
+        return
     reservoir, rewards, refenv = import_reference(args.reference)
     rng = np.random.default_rng(20260109)
 
@@ -243,6 +287,7 @@ def main():
     with open(os.path.join(HERE, "env_plumbing.json"), "w") as fh:
         json.dump(plumb, fh, indent=1)
     print("wrote reservoir_features.npz, rewards.npz, env_plumbing.json")
+    alias_goldens(args.reference, np.random.default_rng(20260110))
 
 
 if __name__ == "__main__":

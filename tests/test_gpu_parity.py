@@ -74,6 +74,43 @@ def test_reward_kernel_matches_reference(lib, oracle_mod, golden_dir, S):
                                        rtol=tol, atol=0)
 
 
+def test_alias_tables_kernel_matches_reference(lib, oracle_mod, golden_dir):
+    """The per-step ALIAS table build (dynamics_kernel's build_alias) against the reference
+    gen_alias (src/lb/shm_proxy.py:127-146): odd as the float32 the reference packs, alias index
+    exact, on every golden row (padded rows of equal S share one launch)."""
+    import json
+    cases = json.load(open(os.path.join(golden_dir, "alias.json")))["cases"]
+    for S in sorted({len(c["weights"]) for c in cases}):
+        rows = [c for c in cases if len(c["weights"]) == S]
+        w = dev(np.array([c["weights"] for c in rows], np.float32))
+        n = len(rows)
+        odd = torch.empty((n, S), dtype=torch.float32, device="cuda:0")
+        ali = torch.empty((n, S), dtype=torch.int32, device="cuda:0")
+        act = torch.empty((n, S), dtype=torch.int32, device="cuda:0")
+        assert lib.load().lbsim_alias_tables(w.data_ptr(), n, S, odd.data_ptr(), ali.data_ptr(),
+                                             act.data_ptr(), None) == 0
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(odd.cpu().numpy(),
+                                      np.array([c["odd"] for c in rows], np.float32))
+        np.testing.assert_array_equal(ali.cpu().numpy(), np.array([c["alias"] for c in rows]))
+        np.testing.assert_array_equal(act.cpu().numpy(), np.tile(np.arange(S), (n, 1)))
+    # rows with non-positive weights: the active list skips them (register_as_weights)
+    w = np.array([[0.0, 2.0, 0.0, 1.0], [0.0, 0.0, 0.0, 0.0], [3.0, -1.0, 1.0, 1.0]], np.float32)
+    odd = torch.empty((3, 4), dtype=torch.float32, device="cuda:0")
+    ali = torch.empty((3, 4), dtype=torch.int32, device="cuda:0")
+    act = torch.empty((3, 4), dtype=torch.int32, device="cuda:0")
+    assert lib.load().lbsim_alias_tables(dev(w).data_ptr(), 3, 4, odd.data_ptr(), ali.data_ptr(),
+                                         act.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    for r in range(3):
+        keep = np.flatnonzero(w[r] > 0)
+        o, a = oracle_mod.gen_alias(w[r, keep])
+        np.testing.assert_array_equal(act.cpu().numpy()[r, :len(keep)], keep)
+        np.testing.assert_array_equal(odd.cpu().numpy()[r, :len(keep)], o.astype(np.float32))
+        np.testing.assert_array_equal(ali.cpu().numpy()[r, :len(keep)], a)
+        assert (act.cpu().numpy()[r, len(keep):] == -1).all()
+
+
 # ------------------------------------------------------------------ the simulator
 CONFIGS = [
     dict(B=257, S=4, kw={}),
@@ -91,6 +128,10 @@ CONFIGS = [
     # slow servers, 5 s steps: flows wait > 2^25 us (33 s), so observe takes the two-pass sort
     dict(B=48, S=4, kw={"server_rates": [1.0, 1.0, 1.5, 2.0], "arrival_rate": 20.0,
                         "step_interval": 5.0, "queue_capacity": 64}),
+    # ALIAS (node.c:442-460 over gen_alias): continuous weights; discrete with a zero level, so
+    # servers drop out of the active list and all-zero rows drop every arrival
+    dict(B=100, S=6, kw={"assign_policy": "alias", "action_type": "continuous"}),
+    dict(B=80, S=4, kw={"assign_policy": "alias", "discrete_weights": [0.0, 1.0, 3.0]}),
 ]
 
 

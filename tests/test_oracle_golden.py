@@ -122,3 +122,29 @@ def test_algorithm_r_acceptance_rate(oracle_mod):
                   for e in range(20000))
         p = 128 / (count + 1)
         assert abs(acc / 20000 - p) < 5 * math.sqrt(p * (1 - p) / 20000) + 1e-4
+
+
+def test_gen_alias_matches_reference(oracle_mod, golden_dir):
+    """oracle_gen_alias == the reference gen_alias (src/lb/shm_proxy.py:127-146) bit for bit in
+    float64, on 137 weight vectors (n = 1..16, ties with the mean, the SURVEY §8a example)."""
+    import json
+    cases = json.load(open(os.path.join(golden_dir, "alias.json")))["cases"]
+    assert len(cases) > 100
+    for c in cases:
+        odd, alias = oracle_mod.gen_alias(np.array(c["weights"], np.float32))
+        np.testing.assert_array_equal(odd, np.array(c["odd"], np.float64))
+        np.testing.assert_array_equal(alias, np.array(c["alias"], np.int32))
+
+
+def test_alias_pick_frequencies(oracle_mod):
+    """The ALIAS rule (node.c:449-460) over a gen_alias table picks server i with probability
+    ~ w_i / sum(w) (gen_alias's 1e-6 epsilons aside)."""
+    w = np.array([1.0, 1.0, 1.0, 1.0, 2.0, 2.0, 2.0], np.float32)
+    odd, alias = oracle_mod.gen_alias(w)
+    odd = odd.astype(np.float32)
+    u = np.random.default_rng(0).integers(0, 2**32, 400000, dtype=np.uint64).astype(np.uint32)
+    rn = (u >> 8).astype(np.float32) * np.float32(5.9604644775390625e-8) * np.float32(len(w))
+    bucket = np.minimum(rn.astype(np.int32), len(w) - 1)
+    pick = np.where(rn - bucket.astype(np.float32) > odd[bucket], alias[bucket], bucket)
+    freq = np.bincount(pick, minlength=len(w)) / len(u)
+    np.testing.assert_allclose(freq, w / w.sum(), atol=3e-3)
