@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--servers", type=int, default=4)
     ap.add_argument("--seed", type=int, default=20260109)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--trace", default=None,
+                    help="replay data/traces/<name>.npz (e.g. poisson_for_loop_rate_500: configs[2])")
+    ap.add_argument("--policy", default="sed", help="sed | sed2 | lsq | lsq2 | alias")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
@@ -119,8 +122,12 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     B, S = args.batch, args.servers
+    tr = None
+    if args.trace:
+        from marllb_amd import trace
+        tr = trace.builtin(args.trace)
     env = VecLoadBalanceEnv(B, S, device=dev, seed=args.seed, env_id_offset=shard.env_id_offset,
-                            autoreset=True, max_steps=10000)
+                            autoreset=True, max_steps=10000, assign_policy=args.policy, trace=tr)
     env.reset()
     gen = torch.Generator(device=dev)
     gen.manual_seed(args.seed + rank)
@@ -152,7 +159,8 @@ def main():
         value = lbdist.throughput(shard, args.steps, elapsed)
         names = ["dynamics_kernel", "observe_kernel"]
         avg = {names[i]: ms[i] / max(1, cnt[i]) for i in range(2)}
-        abytes = algorithmic_bytes(S, ARRIVAL_RATE * STEP_INTERVAL)
+        rate = tr.rate if tr is not None else ARRIVAL_RATE
+        abytes = algorithmic_bytes(S, rate * STEP_INTERVAL)
         per_kernel = {}
         for k in names:
             ab_k = abytes[k] * B
@@ -173,12 +181,16 @@ def main():
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32/int32 (f64 reward)",
-            "data": "synthetic: Philox4x32-10 Poisson arrivals lambda=400/s, Exp(1) work, "
-                    "mu=lambda/(0.8 S) per server, random discrete policy",
-            "config": {"workload": "LB env random-policy rollout, 4 servers (BASELINE configs[1] "
-                                   "rollout at the north-star batch)",
+            "data": ("synthetic: Philox4x32-10 Poisson arrivals lambda=400/s, Exp(1) work, "
+                     "mu=lambda/(0.8 S) per server, random discrete policy") if tr is None else
+                    (f"trace replay {tr.name} ({tr.rows} rows, {tr.rate:.1f}/s; per-env offset "
+                     "gid*7919), mu=rate/(0.8 S), random discrete policy"),
+            "config": {"workload": ("LB env random-policy rollout, 4 servers (BASELINE configs[1] "
+                                    "rollout at the north-star batch)") if tr is None else
+                                   f"LB env trace replay, {S} servers (BASELINE configs[2])",
+                       "assign_policy": args.policy,
                        "envs_per_gpu": B, "servers": S, "global_batch": world * B,
-                       "step_interval_s": 0.25, "assign_policy": "sed", "autoreset": True,
+                       "step_interval_s": 0.25, "autoreset": True,
                        "parallelism": f"env-shard x{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

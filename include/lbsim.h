@@ -73,7 +73,9 @@ enum lbsim_assign_policy {
   LBSIM_POLICY_ALIAS = 4
 };
 
-enum lbsim_arrival_source { LBSIM_ARRIVAL_POISSON = 0 };
+/* POISSON: exponential gaps of mean 1/arrival_rate, Exp(1) work.  TRACE: replay of an arrival
+ * trace set with lbsim_set_trace (data/trace/poisson_for_loop/rate_N.csv). */
+enum lbsim_arrival_source { LBSIM_ARRIVAL_POISSON = 0, LBSIM_ARRIVAL_TRACE = 1 };
 
 /*
  * POD configuration.  Mirrors the LoadBalanceEnv kwargs (env.py:71-87) plus the simulator knobs
@@ -98,7 +100,8 @@ typedef struct lbsim_config {
   int32_t normalize_obs;     /* running mean/std normalisation    env.py:85,450-470   */
   int32_t assign_policy;     /* lbsim_assign_policy, default SED                             */
   int32_t arrival_source;    /* lbsim_arrival_source, default POISSON                        */
-  float arrival_rate;        /* lambda, flows/s per env, default 400 (poisson_for_loop)      */
+  float arrival_rate;        /* lambda, flows/s per env, default 400 (poisson_for_loop);     */
+                             /* TRACE: informational (the trace sets the rate)               */
   float server_rate[LBSIM_MAX_SERVERS]; /* mu_s, flows/s each server can serve (Exp work)   */
   float decay_factor;        /* reservoir decay, default 0.9          reservoir.py:106       */
   int32_t queue_capacity;    /* Q: max flows in flight per server (1..64), default 32       */
@@ -189,6 +192,15 @@ int lbsim_reservoir_features(const float* values, const uint32_t* ts_ms, const u
  * every step -> odd_out[n, S] (float32, as packed into shm.h alias_t), alias_out[n, S] (position
  * in the row's active list), active_out[n, S] (server of each active position; -1 past the end).
  * Entries past a row's active count are (1, 0, -1). */
+/* Arrival trace for arrival_source == TRACE (the TRACE counterpart of the Poisson draw in
+ * env.py's simulation; rows of replay_fork_io.py:95-121's `time<TAB>query` CSV): gap_us[rows]
+ * (us since the previous row; row 0: the wrap-around gap) and work[rows] (service demand in mean-1
+ * units, row N / mean N), device pointers, copied into the handle.  Env gid in episode e replays
+ * rows (gid * 7919 + (e - 1) * 1000003 + k) mod rows for its k-th arrival.  Must precede the
+ * first lbsim_reset of a TRACE handle; setting it again takes effect at the next reset. */
+int lbsim_set_trace(lbsim_t* h, const uint32_t* gap_us, const float* work, int64_t rows,
+                    void* stream);
+
 int lbsim_alias_tables(const float* weights, int64_t n, int S, float* odd_out, int32_t* alias_out,
                        int32_t* active_out, void* stream);
 

@@ -20,6 +20,7 @@ MAX_DISCRETE = 8
 
 OK, EINVAL, ENOMEM, EDEVICE, ESHAPE, ENOTSUP = 0, -1, -2, -3, -4, -5
 ACTION_DISCRETE, ACTION_CONTINUOUS = 0, 1
+ARRIVAL_POISSON, ARRIVAL_TRACE = 0, 1
 DTYPE_I32, DTYPE_I64, DTYPE_F32 = 0, 1, 2
 METRICS = ["jain", "variance", "std", "cv", "max", "min", "product", "range", "gini"]
 POLICIES = ["sed", "sed2", "lsq", "lsq2", "alias"]
@@ -95,6 +96,7 @@ _SIGNATURES = {
     "lbsim_step_outputs_size": (ctypes.c_size_t, []),
     "lbsim_episode_stats": (ctypes.c_int, [_P, _P, _P, _P]),
     "lbsim_reward": (ctypes.c_int, [ctypes.POINTER(LbsimConfig), _P, ctypes.c_int64, _P, _P]),
+    "lbsim_set_trace": (ctypes.c_int, [_P, _P, _P, ctypes.c_int64, _P]),
     "lbsim_alias_tables": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int, _P, _P, _P, _P]),
     "lbsim_reservoir_features": (ctypes.c_int, [_P, _P, _P, ctypes.c_int64, ctypes.c_float, _P,
                                                 _P]),

@@ -32,6 +32,7 @@ struct lbsim {
   DevState st;
   SimParams prm;
   std::vector<void*> allocs;
+  void* trace_buf = nullptr;  // gap_us[rows] then work[rows]
   bool initialised;  // a full reset has been issued
   std::string err;
 };
@@ -100,7 +101,8 @@ int validate(const lbsim_config_t* c, char* msg, size_t n) {
   if (c->max_steps < 1) return bad("max_steps must be >= 1");
   if (c->assign_policy < LBSIM_POLICY_SED || c->assign_policy > LBSIM_POLICY_ALIAS)
     return bad("unknown assign_policy %d", c->assign_policy);
-  if (c->arrival_source != LBSIM_ARRIVAL_POISSON) return bad("unknown arrival_source");
+  if (c->arrival_source != LBSIM_ARRIVAL_POISSON && c->arrival_source != LBSIM_ARRIVAL_TRACE)
+    return bad("unknown arrival_source");
   if (!(c->arrival_rate >= 0.1f) || !(c->arrival_rate <= 1.0e6f))
     return bad("arrival_rate must be in [0.1, 1e6] flows/s");
   for (int s = 0; s < c->num_servers; ++s)
@@ -139,6 +141,8 @@ void derive_params(const lbsim_config_t& c, SimParams& p) {
   p.reward_field = c.reward_field;
   p.decay_c = (float)(std::log2((double)c.decay_factor) / 1000.0);
   p.normalize = c.normalize_obs ? 1 : 0;
+  p.trace = c.arrival_source == LBSIM_ARRIVAL_TRACE ? 1 : 0;
+  p.trace_rows = 0;
 }
 
 // State sections in snapshot order.
@@ -208,8 +212,12 @@ template <int MAXS, int MODE, int POLICY>
 void launch_dyn(lbsim_t* h, const void* action, int dtype, int32_t* assign, const uint8_t* mask,
                 hipStream_t stream) {
   const dim3 block(64), grid((unsigned)((h->B + 63) / 64));
-  hipLaunchKernelGGL((dynamics_kernel<MAXS, MODE, POLICY>), grid, block, 0, stream, h->st, h->prm,
-                     action, dtype, assign, mask);
+  if (h->prm.trace)
+    hipLaunchKernelGGL((dynamics_kernel<MAXS, MODE, POLICY, true>), grid, block, 0, stream, h->st,
+                       h->prm, action, dtype, assign, mask);
+  else
+    hipLaunchKernelGGL((dynamics_kernel<MAXS, MODE, POLICY, false>), grid, block, 0, stream,
+                       h->st, h->prm, action, dtype, assign, mask);
 }
 
 template <int MAXS, int MODE>
@@ -352,6 +360,7 @@ int lbsim_destroy(lbsim_t* h) {
   {
     DeviceGuard g(h->device);
     for (void* p : h->allocs) (void)hipFree(p);
+    if (h->trace_buf) (void)hipFree(h->trace_buf);
     for (hipEvent_t e : h->prof.ev) (void)hipEventDestroy(e);
   }
   delete h;
@@ -376,6 +385,8 @@ int lbsim_seed(lbsim_t* h, uint64_t seed) {
 int lbsim_reset(lbsim_t* h, const uint8_t* env_mask, float* obs_out, void* stream) {
   if (h == nullptr) return LBSIM_EINVAL;
   if (obs_out == nullptr) return fail(h, LBSIM_EINVAL, "obs_out is NULL");
+  if (h->prm.trace && h->prm.trace_rows == 0)
+    return fail(h, LBSIM_EINVAL, "arrival_source TRACE: call lbsim_set_trace before lbsim_reset");
   DeviceGuard g(h->device);
   const hipStream_t s = (hipStream_t)stream;
   int rc = launch_dynamics(h, nullptr, 0, nullptr, env_mask, kModeReset, s);
@@ -442,6 +453,37 @@ int lbsim_reward(const lbsim_config_t* cfg, const float* obs, int64_t n, float* 
                      (hipStream_t)stream, obs, n, cfg->num_servers, cfg->reward_metric,
                      cfg->reward_field, reward_out);
   return hipGetLastError() == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
+}
+
+int lbsim_set_trace(lbsim_t* h, const uint32_t* gap_us, const float* work, int64_t rows,
+                    void* stream) {
+  if (h == nullptr) return LBSIM_EINVAL;
+  if (!h->prm.trace) return fail(h, LBSIM_EINVAL, "lbsim_set_trace needs arrival_source TRACE");
+  if (gap_us == nullptr || work == nullptr || rows < 1 || rows > (int64_t)0x7FFFFFFF)
+    return fail(h, LBSIM_EINVAL, "trace: need device gap_us/work and 1 <= rows < 2^31");
+  DeviceGuard g(h->device);
+  const hipStream_t s = (hipStream_t)stream;
+  if (hipStreamSynchronize(s) != hipSuccess) return fail(h, LBSIM_EDEVICE, "stream sync failed");
+  if (h->trace_buf) {
+    (void)hipFree(h->trace_buf);
+    h->trace_buf = nullptr;
+    h->prm.trace_rows = 0;
+  }
+  const size_t n = (size_t)rows;
+  if (hipMalloc(&h->trace_buf, n * 8) != hipSuccess) {
+    h->trace_buf = nullptr;
+    return fail(h, LBSIM_ENOMEM, "hipMalloc(%zu) failed", n * 8);
+  }
+  uint32_t* g_dev = (uint32_t*)h->trace_buf;
+  float* w_dev = (float*)(g_dev + n);
+  if (hipMemcpyAsync(g_dev, gap_us, n * 4, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(w_dev, work, n * 4, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return fail(h, LBSIM_EDEVICE, "trace copy failed");
+  h->st.trace_gap = g_dev;
+  h->st.trace_work = w_dev;
+  h->prm.trace_rows = (uint32_t)rows;
+  return LBSIM_OK;
 }
 
 int lbsim_alias_tables(const float* weights, int64_t n, int S, float* odd_out, int32_t* alias_out,

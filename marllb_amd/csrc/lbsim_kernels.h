@@ -59,6 +59,10 @@ struct DevState {
   // running normalisation [B*S*11] (nullptr when disabled)
   double* norm_mean;
   double* norm_std;
+  // arrival trace (TRACE source; nullptr otherwise), shared by all envs: us gap before each row,
+  // mean-1 work of each row
+  const uint32_t* trace_gap;
+  const float* trace_work;
 };
 
 struct SimParams {
@@ -79,7 +83,20 @@ struct SimParams {
   int32_t reward_field;
   float decay_c;  // log2(decay_factor) / 1000, per integer millisecond of age
   int32_t normalize;
+  int32_t trace;          // 1: arrivals replay the trace (LBSIM_ARRIVAL_TRACE)
+  uint32_t trace_rows;
 };
+
+constexpr uint32_t kTraceEnvStride = 7919u;        // SURVEY §8d C3 per-env offset
+constexpr uint32_t kTraceEpisodeStride = 1000003u;  // next episode, another window
+
+// Trace row of arrival k of env gid in episode `episode` (>= 1).
+__device__ __forceinline__ uint32_t trace_row(const SimParams& p, uint32_t gid, uint32_t episode,
+                                              uint32_t k) {
+  const uint64_t v = (uint64_t)gid * kTraceEnvStride +
+                     (uint64_t)(episode - 1u) * kTraceEpisodeStride + (uint64_t)k;
+  return (uint32_t)(v % (uint64_t)p.trace_rows);
+}
 
 // ================================================================ dynamics (one lane = one env)
 
@@ -112,6 +129,11 @@ struct LaneState {
   float next_work;
   uint32_t u2, u3, arr_idx, episode, clock, dropped;
   uint32_t gid;
+  // TRACE: row of arrival arr_idx + 1 and its prefetched gap / work (loaded an arrival ahead so
+  // the event loop never waits on the trace)
+  uint32_t row;
+  int32_t pf_gap;
+  float pf_work;
 };
 
 struct Lds {
@@ -222,11 +244,30 @@ __device__ __forceinline__ void arrival_from_draw(const SimParams& p, const u32x
 }
 
 template <int MAXS>
-__device__ __forceinline__ void draw_arrival(const SimParams& p, LaneState<MAXS>& L,
-                                             int32_t t_prev) {
+__device__ __forceinline__ void draw_arrival(const DevState& st, const SimParams& p,
+                                             LaneState<MAXS>& L, int32_t t_prev) {
   const u32x4 d = philox4x32_10(u32x4{L.arr_idx, L.gid, L.episode, kStreamArrival << 24},
                                 p.key0, p.key1);
-  arrival_from_draw(p, d, t_prev, L.next_arr, L.next_work, L.u2, L.u3);
+  if (p.trace) {
+    const uint32_t r = trace_row(p, L.gid, L.episode, L.arr_idx);
+    L.next_arr = t_prev + (int32_t)st.trace_gap[r];
+    L.next_work = st.trace_work[r];
+    L.u2 = d.z;
+    L.u3 = d.w;
+  } else {
+    arrival_from_draw(p, d, t_prev, L.next_arr, L.next_work, L.u2, L.u3);
+  }
+}
+
+// TRACE: position the prefetch at arrival arr_idx + 1 (kernel entry).
+template <int MAXS>
+__device__ __forceinline__ void trace_prefetch(const DevState& st, const SimParams& p,
+                                               LaneState<MAXS>& L) {
+  if (p.trace) {
+    L.row = trace_row(p, L.gid, L.episode, L.arr_idx + 1u);
+    L.pf_gap = (int32_t)st.trace_gap[L.row];
+    L.pf_work = st.trace_work[L.row];
+  }
 }
 
 // Kernel entry: per-server state from HBM; the first WL entries of every queue into LDS.
@@ -295,7 +336,7 @@ __device__ __forceinline__ void clear_servers(const SimParams& p, LaneState<MAXS
 // completions are processed in t_complete order before any arrival at the same or a later time —
 // the order the oracle (server by server) produces — so every reservoir sees the same insert
 // sequence and the state is bit-identical.
-template <int MAXS, int POLICY>
+template <int MAXS, int POLICY, bool TRACE>
 __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
                                          LaneState<MAXS>& L, uint32_t b, const float (&w)[MAXS],
                                          const Lds& l) {
@@ -473,7 +514,19 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     int32_t na;
     float nw;
     uint32_t nu2, nu3;
-    arrival_from_draw(p, d, ta, na, nw, nu2, nu3);
+    if constexpr (TRACE) {  // the prefetched row; the next prefetch is issued one arrival ahead
+      na = ta + L.pf_gap;
+      nw = L.pf_work;
+      nu2 = d.z;
+      nu3 = d.w;
+      if (arr) {
+        L.row = (L.row + 1u == p.trace_rows) ? 0u : L.row + 1u;
+        L.pf_gap = (int32_t)st.trace_gap[L.row];
+        L.pf_work = st.trace_work[L.row];
+      }
+    } else {
+      arrival_from_draw(p, d, ta, na, nw, nu2, nu3);
+    }
     L.next_arr = arr ? na : L.next_arr;
     L.next_work = arr ? nw : L.next_work;
     L.u2 = arr ? nu2 : L.u2;
@@ -557,8 +610,9 @@ __device__ __forceinline__ float action_weight(const SimParams& p, const void* a
 }
 
 // MODE is a template parameter so step and reset launches are separate kernels in profiles.
-// POLICY is a template parameter: each assignment rule gets its own straight-line event loop.
-template <int MAXS, int MODE, int POLICY>
+// POLICY and TRACE (arrival source) are template parameters: each combination gets its own
+// straight-line event loop.
+template <int MAXS, int MODE, int POLICY, bool TRACE>
 __global__ void __launch_bounds__(64)
     dynamics_kernel(DevState st, SimParams p, const void* action, int action_dtype,
                     int32_t* assign_out, const uint8_t* reset_mask) {
@@ -578,12 +632,13 @@ __global__ void __launch_bounds__(64)
     L.clock = 0u;
     L.dropped = 0u;
     L.arr_idx = 0u;
-    draw_arrival<MAXS>(p, L, 0);
+    draw_arrival<MAXS>(st, p, L, 0);
+    trace_prefetch<MAXS>(st, p, L);
     clear_servers<MAXS>(p, L, l);
     float w1[MAXS];
 #pragma unroll
     for (int s = 0; s < MAXS; ++s) w1[s] = 1.0f;
-    for (int k = 0; k < p.warmup_steps; ++k) sim_step<MAXS, POLICY>(st, p, L, b, w1, l);
+    for (int k = 0; k < p.warmup_steps; ++k) sim_step<MAXS, POLICY, TRACE>(st, p, L, b, w1, l);
     st.ep_step[b] = 0;
     st.ep_return[b] = 0.0;
     store_servers<MAXS>(st, p, L, b, l, nullptr);
@@ -596,12 +651,13 @@ __global__ void __launch_bounds__(64)
     L.next_work = st.next_work[b];
     L.u2 = st.next_u2[b];
     L.u3 = st.next_u3[b];
+    trace_prefetch<MAXS>(st, p, L);
     load_servers<MAXS>(st, p, L, b, l);
     float w[MAXS];
 #pragma unroll
     for (int s = 0; s < MAXS; ++s)
       w[s] = (s < S) ? action_weight(p, action, action_dtype, (size_t)b * S + (size_t)s) : 1.0f;
-    sim_step<MAXS, POLICY>(st, p, L, b, w, l);
+    sim_step<MAXS, POLICY, TRACE>(st, p, L, b, w, l);
     store_servers<MAXS>(st, p, L, b, l, assign_out);
   }
   st.episode[b] = L.episode;

@@ -98,10 +98,12 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
                 env_id_offset: int = 0, arrival_rate: float = 400.0,
                 server_rates: Optional[List[float]] = None, load: float = 0.8,
                 queue_capacity: int = 32, warmup_steps: int = 8, decay_factor: float = 0.9,
-                assign_policy: str = "sed") -> _lib.LbsimConfig:
+                assign_policy: str = "sed", trace=None) -> _lib.LbsimConfig:
     """Build and validate an lbsim_config_t from reference-style kwargs.
 
     server_rates defaults to identical servers at utilisation `load`: mu = rate / (load * S).
+    trace (marllb_amd.trace.Trace): replay its arrivals (LBSIM_ARRIVAL_TRACE); its empirical rate
+    replaces arrival_rate.  The arrays themselves go to the handle (Handle.set_trace).
     """
     if reward_metric not in _lib.METRICS:  # rewards.py:321-323
         raise ValueError(f"Unsupported metric: {reward_metric}. Supported: {_lib.METRICS}")
@@ -131,6 +133,9 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
     cfg.max_steps = int(max_steps)
     cfg.normalize_obs = 1 if normalize_obs else 0
     cfg.assign_policy = _lib.POLICIES.index(assign_policy)
+    if trace is not None:
+        cfg.arrival_source = _lib.ARRIVAL_TRACE
+        arrival_rate = float(trace.rate)
     cfg.arrival_rate = float(arrival_rate)
     if server_rates is None:
         server_rates = [float(arrival_rate) / (float(load) * num_servers)] * num_servers
@@ -180,6 +185,17 @@ class Handle:
     def load_state(self, data: bytes) -> None:
         self.check(self.lib.lbsim_set_state(self.h, data, len(data)))
 
+    def set_trace(self, trace) -> None:
+        """Copy a marllb_amd.trace.Trace to the device and install it (lbsim_set_trace)."""
+        torch = _torch()
+        dev = torch.device("cuda", self.device_index)
+        gap = torch.from_numpy(trace.gap_us.view(np.int32)).to(dev)
+        work = torch.from_numpy(trace.work).to(dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        self.check(self.lib.lbsim_set_trace(self.h, ctypes.c_void_p(gap.data_ptr()),
+                                            ctypes.c_void_p(work.data_ptr()), trace.rows,
+                                            ctypes.c_void_p(stream)))
+
 
 class VecLoadBalanceEnv:
     """num_envs independent LoadBalanceEnv instances stepped together on one GPU.
@@ -198,12 +214,15 @@ class VecLoadBalanceEnv:
         self.device_index = _device_index(device)
         self.device = torch.device("cuda", self.device_index)
         self.cfg = make_config(num_envs, num_servers, **kwargs)
+        self.trace = kwargs.get("trace")
         self.num_envs = int(num_envs)
         self.num_servers = int(num_servers)
         self.action_type = "discrete" if self.cfg.action_type == _lib.ACTION_DISCRETE else "continuous"
         self.autoreset = autoreset
         self.keep_terminal_obs = keep_terminal_obs
         self.handle = Handle(self.cfg, self.device_index)
+        if self.trace is not None:
+            self.handle.set_trace(self.trace)
         self._reset_done = False
         # upper bound on every env's episode step since the last full reset: while it is below
         # max_steps no env can be done, so the masked auto-reset launch is provably a no-op

@@ -55,6 +55,7 @@ def load() -> ctypes.CDLL:
         "oracle_step": (ctypes.c_int, [_P, _P, ctypes.c_int, _P, _P, _P, _P]),
         "oracle_episode_stats": (None, [_P, _P, _P]),
         "oracle_normalize": (None, [_P, ctypes.c_int, _P, _P, _P, _P]),
+        "oracle_set_trace": (ctypes.c_int, [_P, _P, _P, ctypes.c_long]),
         "oracle_gen_alias": (None, [_P, ctypes.c_int, _P, _P]),
         "oracle_algr_slot": (ctypes.c_long, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                              ctypes.c_uint32, _P]),
@@ -113,7 +114,7 @@ def rewards(obs: np.ndarray, metric: int, field: int, f64: bool = False) -> np.n
 class OracleEnv:
     """B envs of the CPU restatement with the same config struct and state layout as liblbsim."""
 
-    def __init__(self, cfg, threads: int = 1):
+    def __init__(self, cfg, threads: int = 1, trace=None):
         self.lib = load()
         self.cfg = cfg
         self.B, self.S = cfg.num_envs, cfg.num_servers
@@ -121,6 +122,13 @@ class OracleEnv:
         if not self.h:
             raise MemoryError("oracle_create failed")
         self.lib.oracle_set_threads(self.h, threads)
+        if trace is not None:
+            self.set_trace(trace)
+
+    def set_trace(self, trace):
+        gap = np.ascontiguousarray(trace.gap_us, np.uint32)
+        work = np.ascontiguousarray(trace.work, np.float32)
+        assert self.lib.oracle_set_trace(self.h, ptr(gap), ptr(work), len(gap)) == 0
 
     def close(self):
         if self.h:

@@ -296,6 +296,8 @@ typedef struct oracle {
   uint32_t* res_fct; uint32_t* res_dur; /* integer microseconds; value = (float)us * 1e-6f */
   uint32_t* res_ts;
   double* norm_mean; double* norm_std;
+  /* TRACE arrivals (lbsim_set_trace semantics): us gap before each row, mean-1 work */
+  uint32_t* trace_gap; float* trace_work; uint32_t trace_rows;
 } oracle_t;
 
 static void derive(oracle_t* o) {
@@ -344,8 +346,23 @@ oracle_t* oracle_create(const lbsim_config_t* cfg) {
 
 void oracle_destroy(oracle_t* o) {
   if (!o) return;
+  free(o->trace_gap);
+  free(o->trace_work);
   free(o->buf);
   free(o);
+}
+
+/* The trace replayed when cfg.arrival_source == TRACE (host copies). */
+int oracle_set_trace(oracle_t* o, const uint32_t* gap_us, const float* work, long rows) {
+  if (rows < 1) return -1;
+  free(o->trace_gap);
+  free(o->trace_work);
+  o->trace_gap = (uint32_t*)malloc((size_t)rows * 4);
+  o->trace_work = (float*)malloc((size_t)rows * 4);
+  memcpy(o->trace_gap, gap_us, (size_t)rows * 4);
+  memcpy(o->trace_work, work, (size_t)rows * 4);
+  o->trace_rows = (uint32_t)rows;
+  return 0;
 }
 
 void oracle_set_threads(oracle_t* o, int n) { o->threads = n < 1 ? 1 : n; }
@@ -474,9 +491,18 @@ static void draw_arrival(env_ctx* e, int32_t t_prev) {
   const uint32_t ctr[4] = {o->arr_idx[b], e->gid, o->episode[b], 1u << 24};
   uint32_t d[4];
   oracle_philox(ctr, o->key, d);
-  const int32_t gap = (int32_t)(-oracle_logf(u01(d[0])) * o->mean_gap_us);
-  o->next_arr[b] = t_prev + gap;
-  o->next_work[b] = -oracle_logf(u01(d[1]));
+  if (o->cfg.arrival_source == LBSIM_ARRIVAL_TRACE) {
+    /* row (gid * 7919 + (episode - 1) * 1000003 + k) mod rows of the k-th arrival */
+    const uint64_t v = (uint64_t)e->gid * 7919u + (uint64_t)(o->episode[b] - 1u) * 1000003u +
+                       (uint64_t)o->arr_idx[b];
+    const uint32_t r = (uint32_t)(v % (uint64_t)o->trace_rows);
+    o->next_arr[b] = t_prev + (int32_t)o->trace_gap[r];
+    o->next_work[b] = o->trace_work[r];
+  } else {
+    const int32_t gap = (int32_t)(-oracle_logf(u01(d[0])) * o->mean_gap_us);
+    o->next_arr[b] = t_prev + gap;
+    o->next_work[b] = -oracle_logf(u01(d[1]));
+  }
   o->next_u2[b] = d[2];
   o->next_u3[b] = d[3];
 }
@@ -680,6 +706,7 @@ static void reset_env(oracle_t* o, size_t b) {
 
 int oracle_reset(oracle_t* o, const uint8_t* mask, float* obs_out) {
   const long B = o->B;
+  if (o->cfg.arrival_source == LBSIM_ARRIVAL_TRACE && o->trace_rows == 0) return -2;
 #pragma omp parallel for schedule(dynamic, 16) num_threads(o->threads)
   for (long b = 0; b < B; ++b) {
     if (mask && !mask[b]) continue;

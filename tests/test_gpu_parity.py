@@ -132,7 +132,22 @@ CONFIGS = [
     # servers drop out of the active list and all-zero rows drop every arrival
     dict(B=100, S=6, kw={"assign_policy": "alias", "action_type": "continuous"}),
     dict(B=80, S=4, kw={"assign_policy": "alias", "discrete_weights": [0.0, 1.0, 3.0]}),
+    # TRACE arrivals (configs[2] shape, small B): the converted rate_500 trace, and a 37-row
+    # synthetic trace that every env wraps around many times per episode
+    dict(B=64, S=8, kw={"trace": "builtin"}),
+    dict(B=50, S=4, kw={"trace": "short", "assign_policy": "sed2", "step_interval": 0.5}),
 ]
+
+
+def resolve_kw(kw):
+    """CONFIGS entries name traces; build them here (module import stays cheap)."""
+    from marllb_amd import trace
+    kw = dict(kw)
+    if kw.get("trace") == "builtin":
+        kw["trace"] = trace.builtin()
+    elif kw.get("trace") == "short":
+        kw["trace"] = trace.synthetic(37, 300.0, seed=7)
+    return kw
 
 
 def _actions(rng, B, S, cfgkw):
@@ -156,10 +171,10 @@ def _compare_state(h_gpu, ora, B, S, Q, norm):
 def test_simulator_bit_exact_vs_oracle(lib, oracle_mod, case):
     from marllb_amd.env import VecLoadBalanceEnv, make_config
     c = CONFIGS[case]
-    B, S, kw = c["B"], c["S"], dict(c["kw"])
+    B, S, kw = c["B"], c["S"], resolve_kw(c["kw"])
     kw.setdefault("seed", 1000 + case)
     env = VecLoadBalanceEnv(B, S, device="cuda:0", autoreset=False, **kw)
-    ora = oracle_mod.OracleEnv(make_config(B, S, **kw), threads=4)
+    ora = oracle_mod.OracleEnv(make_config(B, S, **kw), threads=4, trace=kw.get("trace"))
     Q, norm = env.cfg.queue_capacity, bool(env.cfg.normalize_obs)
     obs_g = env.reset().cpu().numpy()
     obs_o = ora.reset()
@@ -240,3 +255,35 @@ def test_full_size_properties(lib, oracle_mod):
     np.testing.assert_array_equal(obs[off:off + n].cpu().numpy(), oo)
     np.testing.assert_array_equal(rew[off:off + n].cpu().numpy(), ro)
     assert st["dropped"].sum() == 0
+
+
+def test_full_size_trace_replay_c3(lib, oracle_mod):
+    """BASELINE configs[2]: 65536 envs x 8 servers replaying data/trace poisson_for_loop
+    rate_500 (the Wikipedia-trace stand-in).  Arrival conservation against the
+    trace rows, and the oracle on a slice of the same global ids, bit-exact."""
+    from marllb_amd import trace
+    from marllb_amd.env import VecLoadBalanceEnv, make_config
+    tr = trace.builtin()
+    B, S, steps = 65536, 8, 4
+    env = VecLoadBalanceEnv(B, S, device="cuda:0", seed=11, autoreset=False, trace=tr)
+    env.reset()
+    rng = np.random.default_rng(3)
+    acts = [rng.integers(0, 3, (B, S)) for _ in range(steps)]
+    tot = torch.zeros(B, dtype=torch.int64, device="cuda:0")
+    for a in acts:
+        obs, rew, done, info = env.step(torch.from_numpy(a), assign_counts=True)
+        tot += info["assign_counts"].sum(1)
+        assert torch.isfinite(obs).all() and not done.any()
+    st = statelayout.parse(env.handle.state_bytes(), B, S, env.cfg.queue_capacity, False)
+    # arrivals since reset = rows consumed from each env's offset (warm-up included)
+    arrived = tot + torch.from_numpy(st["dropped"].astype(np.int64)).cuda()
+    idx = torch.from_numpy(st["arr_idx"].astype(np.int64)).cuda()
+    assert bool((arrived <= idx).all())
+    off, n = 30000, 256
+    ora = oracle_mod.OracleEnv(make_config(n, S, seed=11, env_id_offset=off, trace=tr),
+                               threads=8, trace=tr)
+    ora.reset()
+    for a in acts:
+        oo, ro, _, _ = ora.step(np.ascontiguousarray(a[off:off + n]))
+    np.testing.assert_array_equal(obs[off:off + n].cpu().numpy(), oo)
+    np.testing.assert_array_equal(rew[off:off + n].cpu().numpy(), ro)

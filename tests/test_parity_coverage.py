@@ -10,7 +10,7 @@ import pytest
 from tests import statelayout
 
 pytest.importorskip("torch")
-from tests.test_gpu_parity import CONFIGS, _actions  # noqa: E402
+from tests.test_gpu_parity import CONFIGS, _actions, resolve_kw  # noqa: E402
 
 PACK_LIMIT = (1 << 25) - 1
 
@@ -22,10 +22,10 @@ def window(S):
 def run_case(oracle_mod, case, steps=12):
     from marllb_amd.env import make_config
     c = CONFIGS[case]
-    B, S, kw = c["B"], c["S"], dict(c["kw"])
+    B, S, kw = c["B"], c["S"], resolve_kw(c["kw"])
     kw.setdefault("seed", 1000 + case)
     cfg = make_config(B, S, **kw)
-    ora = oracle_mod.OracleEnv(cfg, threads=4)
+    ora = oracle_mod.OracleEnv(cfg, threads=4, trace=kw.get("trace"))
     ora.reset()
     rng = np.random.default_rng(case)
     max_q = 0
