@@ -192,6 +192,13 @@ int lbsim_reservoir_features(const float* values, const uint32_t* ts_ms, const u
  * every step -> odd_out[n, S] (float32, as packed into shm.h alias_t), alias_out[n, S] (position
  * in the row's active list), active_out[n, S] (server of each active position; -1 past the end).
  * Entries past a row's active count are (1, 0, -1). */
+/* Stateless: problem-05 per-agent observations (multi_agent_env.py:152-188) of n flattened
+ * (S, 11) observations (device pointers), num_agents * servers_per_agent == S.  Agent a gets the
+ * 4-value slices of the flattened obs for its servers -- flat[4 a k : 4 (a+1) k], the wrapper's
+ * `server_features_per_server = 4` -- then flat[4 S :]: out[n, A, 4 k + 7 S] (128 at 4 x 4). */
+int lbsim_agent_obs(const float* obs, int64_t n, int S, int num_agents, int servers_per_agent,
+                    float* out, void* stream);
+
 /* Arrival trace for arrival_source == TRACE (the TRACE counterpart of the Poisson draw in
  * env.py's simulation; rows of replay_fork_io.py:95-121's `time<TAB>query` CSV): gap_us[rows]
  * (us since the previous row; row 0: the wrap-around gap) and work[rows] (service demand in mean-1

@@ -486,6 +486,19 @@ int lbsim_set_trace(lbsim_t* h, const uint32_t* gap_us, const float* work, int64
   return LBSIM_OK;
 }
 
+int lbsim_agent_obs(const float* obs, int64_t n, int S, int num_agents, int servers_per_agent,
+                    float* out, void* stream) {
+  if (n < 0 || S < 1 || S > LBSIM_MAX_SERVERS || num_agents < 1 || servers_per_agent < 1 ||
+      num_agents * servers_per_agent != S)
+    return LBSIM_EINVAL;
+  if (n == 0) return LBSIM_OK;
+  if (!obs || !out) return LBSIM_EINVAL;
+  const int64_t total = n * num_agents * (4 * servers_per_agent + 7 * S);
+  hipLaunchKernelGGL(agent_obs_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, obs, n, S, num_agents, servers_per_agent, out);
+  return hipGetLastError() == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
+}
+
 int lbsim_alias_tables(const float* weights, int64_t n, int S, float* odd_out, int32_t* alias_out,
                        int32_t* active_out, void* stream) {
   if (n < 0 || S < 1 || S > LBSIM_MAX_SERVERS) return LBSIM_EINVAL;

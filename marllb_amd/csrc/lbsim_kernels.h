@@ -1274,6 +1274,21 @@ __global__ void __launch_bounds__(64)
   }
 }
 
+// problem-05 per-agent observations (multi_agent_env.py:152-188) of n flattened (S, 11) obs:
+// agent a sees 4-value slices of the flattened obs for its servers [a k, (a+1) k) -- flat
+// [4 a k, 4 (a+1) k), the wrapper's `server_features_per_server = 4` -- followed by flat[4 S:].
+__global__ void __launch_bounds__(256)
+    agent_obs_kernel(const float* obs, int64_t n, int S, int A, int k, float* out) {
+  const int D = 4 * k + 7 * S;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * A * D) return;
+  const int64_t b = i / ((int64_t)A * D);
+  const int r = (int)(i - b * A * D);
+  const int a = r / D, j = r - a * D;
+  const int src = j < 4 * k ? 4 * k * a + j : 4 * S + (j - 4 * k);
+  out[i] = obs[b * S * NF + src];
+}
+
 __global__ void __launch_bounds__(256)
     reward_kernel(const float* obs, int64_t n, int S, int metric, int field, float* out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -411,7 +411,9 @@ class LoadBalanceEnv:
         raw = info_t["raw_obs"][0].cpu().numpy()
         reward = float(rew_t[0].item())
         obs_dict = self._array_to_dict(raw)
-        self.last_observation = obs_dict
+        # the reference sets last_observation only in SHM mode (env.py:201,249); problem-05's
+        # get_state() relies on it staying None in simulation (multi_agent_env.py:249-254)
+        self._last_obs_dict = obs_dict
         self.episode_rewards.append(reward)
         self.episode_return += reward
         done = self.current_step >= self.max_steps
@@ -430,8 +432,8 @@ class LoadBalanceEnv:
             print(f"\n{'=' * 60}")
             print(f"Step: {self.current_step}/{self.max_steps}")
             print(f"Episode Return: {self.episode_return:.4f}")
-            if self.last_observation:
-                obs_dict = self.last_observation
+            obs_dict = self.last_observation or getattr(self, "_last_obs_dict", None)
+            if obs_dict:
                 active = obs_dict.get("active_servers", [])
                 stats = obs_dict.get("server_stats", {})
                 print(f"Active Servers: {active}")

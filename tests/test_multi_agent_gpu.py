@@ -1,0 +1,79 @@
+"""problem-05 multi-agent facade (SURVEY §8a a15, §0.6 contract) on the GPU simulator."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test run without a HIP device")
+
+
+def test_single_env_reference_io():
+    """Shapes and values the reference wrapper actually produces: 128-dim float64
+    agent obs built from 4-value slices, 74-dim state, replicated global reward."""
+    from marllb_amd import MultiAgentLoadBalanceEnv
+    env = MultiAgentLoadBalanceEnv(num_agents=4, servers_per_agent=4, max_steps=10, seed=3)
+    assert (env.obs_dim, env.declared_obs_dim, env.state_dim) == (128, 20, 74)
+    obs = env.reset()
+    assert len(obs) == 4 and all(o.shape == (128,) and o.dtype == np.float64 for o in obs)
+    st = env.get_state()
+    assert st.shape == (74,) and np.all(st[:72] == 0) and st[72] == 0.0 and st[73] == 4
+    acts = [np.array([0.5, 1.0, 2.0, 4.0], np.float32) for _ in range(4)]
+    obs, rew, done, info = env.step(acts)
+    assert len(rew) == 4 and len(set(rew)) == 1 and not done
+    for a in range(4):  # own slice flat[16a:16a+16], shared tail flat[64:]
+        np.testing.assert_array_equal(obs[a][16:], obs[0][16:])
+    loads = np.array(info["server_loads"])
+    np.testing.assert_array_equal(obs[0][0:4:4], loads[0:1])  # flat[0] = server 0 n_flow_on
+    assert env.get_state()[72] == pytest.approx(0.1)
+    assert len(info["server_loads"]) == 16
+
+
+def test_scalar_agent_actions_and_local_rewards():
+    """FIX 1 (one value per agent is broadcast) and FIX 2 (server_loads, local Jain)."""
+    from marllb_amd import MultiAgentLoadBalanceEnv
+    a = MultiAgentLoadBalanceEnv(num_agents=4, servers_per_agent=4, action_type="discrete",
+                                 max_steps=10, seed=5, global_reward=False)
+    b = MultiAgentLoadBalanceEnv(num_agents=4, servers_per_agent=4, action_type="discrete",
+                                 max_steps=10, seed=5, global_reward=False)
+    a.reset()
+    b.reset()
+    oa, ra, _, ia = a.step([0, 1, 2, 1])
+    ob, rb, _, ib = b.step([[0] * 4, [1] * 4, [2] * 4, [1] * 4])
+    for x, y in zip(oa, ob):
+        np.testing.assert_array_equal(x, y)
+    assert ra == rb and len(ra) == 4
+    for ag in range(4):
+        loads = ia["server_loads"][4 * ag:4 * ag + 4]
+        s = sum(loads)
+        want = 0.0 if s == 0 else s * s / (4 * sum(x * x for x in loads) + 1e-8)
+        assert ra[ag] == pytest.approx(want)
+
+
+def test_vec_agent_obs_kernel_and_actions():
+    """lbsim_agent_obs equals the wrapper's slicing; (B,A), (B,A,k) and (B,S) actions agree."""
+    from marllb_amd import VecMultiAgentLoadBalanceEnv
+    B, A, k = 256, 4, 4
+    envs = [VecMultiAgentLoadBalanceEnv(B, A, k, device="cuda:0", seed=9,
+                                        action_type="discrete") for _ in range(3)]
+    obs0 = [e.reset() for e in envs]
+    assert obs0[0].shape == (B, A, 128)
+    assert torch.equal(obs0[0], obs0[1])
+    a = torch.randint(0, 3, (B, A), device="cuda:0")
+    o1, r1, d1, i1 = envs[0].step(a)
+    o2, _, _, _ = envs[1].step(a.unsqueeze(2).expand(B, A, k))
+    o3, _, _, _ = envs[2].step(a.repeat_interleave(k, dim=1))
+    assert torch.equal(o1, o2) and torch.equal(o1, o3)
+    # the wrapper's slicing of the underlying (B, 16, 11) obs
+    raw = envs[0].vec.step(a.repeat_interleave(k, dim=1))[0]
+    flat = raw.reshape(B, -1)
+    want = torch.cat([flat[:, :64].reshape(B, A, 16),
+                      flat[:, 64:].unsqueeze(1).expand(B, A, 112)], dim=2)
+    assert torch.equal(envs[0].agent_obs(raw), want)
+    st = envs[0].get_state()
+    assert st.shape == (B, 74) and torch.all(st[:, -1] == 4)
+    assert r1.shape == (B, A) and torch.all(r1 == r1[:, :1])

@@ -1,0 +1,59 @@
+"""On-GPU policy / mixer networks (marllb_amd/policies.py) against the reference modules' outputs
+(tests/golden/nets.npz, made by tests/golden/gen_nets.py from problem-04 networks.py and
+problem-05 agent_network.py / mixing_network.py).  fp32; tolerance 1e-5 (abs + rel)."""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from marllb_amd.policies import AgentQNet, GRUPolicy, QMixer, load_prefixed  # noqa: E402
+
+TOL = dict(rtol=1e-5, atol=1e-5)
+
+
+@pytest.fixture(scope="module")
+def g(golden_dir):
+    return np.load(os.path.join(golden_dir, "nets.npz"))
+
+
+def nets(g, device):
+    pol = load_prefixed(GRUPolicy(88, 8, 256, 128), g, "policy").to(device)
+    q = load_prefixed(AgentQNet(128, 3, 128, 64), g, "agentq").to(device)
+    mix = load_prefixed(QMixer(4, 74, 32, 64), g, "mixer").to(device)
+    return pol, q, mix
+
+
+def check(g, device):
+    pol, q, mix = nets(g, device)
+    t = lambda k: torch.from_numpy(g[k]).to(device)  # noqa: E731
+    with torch.no_grad():
+        mean, log_std, h1 = pol(t("policy_x"), t("policy_h"))
+        _, _, det, _ = pol.sample(t("policy_x"), t("policy_h"))
+        qv, hq1 = q(t("agentq_obs"), t("agentq_h"))
+        qtot = mix(t("mixer_qs"), t("mixer_state"))
+    np.testing.assert_allclose(mean.cpu().numpy(), g["policy_mean"], **TOL)
+    np.testing.assert_allclose(log_std.cpu().numpy(), g["policy_log_std"], **TOL)
+    np.testing.assert_allclose(h1.cpu().numpy(), g["policy_h1"], **TOL)
+    np.testing.assert_allclose(det.cpu().numpy(), g["policy_det_action"], **TOL)
+    np.testing.assert_allclose(qv.cpu().numpy(), g["agentq_q"], **TOL)
+    np.testing.assert_allclose(hq1.cpu().numpy(), g["agentq_h1"], **TOL)
+    np.testing.assert_allclose(qtot.cpu().numpy(), g["mixer_qtot"], **TOL)
+
+
+def test_mirrors_match_reference_cpu(g):
+    check(g, "cpu")
+
+
+def test_reference_state_dict_names(g):
+    """A reference checkpoint loads unchanged: identical parameter names and shapes."""
+    pol, q, mix = nets(g, "cpu")
+    for prefix, m in (("policy", pol), ("agentq", q), ("mixer", mix)):
+        names = {k[len(prefix) + 1:] for k in g.files if k.startswith(prefix + ".")}
+        assert names == set(m.state_dict())
+
+
+@pytest.mark.gpu
+def test_mirrors_match_reference_gpu(g):
+    check(g, "cuda:0")
