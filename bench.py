@@ -51,8 +51,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=65536, help="envs per GPU")
-    ap.add_argument("--servers", type=int, default=4)
+    ap.add_argument("--batch", type=int, default=None,
+                    help="envs per GPU (default 65536; qmix 8192)")
+    ap.add_argument("--servers", type=int, default=None,
+                    help="servers per env (default 4; sac-gru 8; qmix 4 agents x 4)")
+    ap.add_argument("--workload", choices=["rollout", "sac-gru", "qmix"], default="rollout",
+                    help="rollout: random policy (configs[1] at the north-star batch); sac-gru: "
+                         "problem-04 actor on GPU (configs[3]); qmix: problem-05 agents + "
+                         "mixer on GPU (configs[4])")
     ap.add_argument("--seed", type=int, default=20260109)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--trace", default=None,
@@ -110,6 +116,10 @@ def main():
     from marllb_amd import dist as lbdist
     from marllb_amd.env import VecLoadBalanceEnv
 
+    if args.batch is None:
+        args.batch = 8192 if args.workload == "qmix" else 65536
+    if args.servers is None:
+        args.servers = {"rollout": 4, "sac-gru": 8, "qmix": 16}[args.workload]
     shard = lbdist.from_env(args.batch)
     world, rank = shard.world, shard.rank
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -126,15 +136,39 @@ def main():
     if args.trace:
         from marllb_amd import trace
         tr = trace.builtin(args.trace)
-    env = VecLoadBalanceEnv(B, S, device=dev, seed=args.seed, env_id_offset=shard.env_id_offset,
-                            autoreset=True, max_steps=10000, assign_policy=args.policy, trace=tr)
-    env.reset()
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(args.seed + rank)
+    common = dict(device=dev, seed=args.seed, env_id_offset=shard.env_id_offset, autoreset=True,
+                  assign_policy=args.policy, trace=tr)
+    torch.manual_seed(args.seed)  # network init (random weights of the reference architecture)
+    if args.workload == "rollout":
+        env = VecLoadBalanceEnv(B, S, max_steps=10000, **common)
+        env.reset()
+        handle = env.handle
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(args.seed + rank)
 
-    def one_step():
-        a = torch.randint(0, 3, (B, S), device=dev, dtype=torch.int64, generator=gen)
-        env.step(a)
+        def one_step():
+            a = torch.randint(0, 3, (B, S), device=dev, dtype=torch.int64, generator=gen)
+            env.step(a)
+    elif args.workload == "sac-gru":
+        from marllb_amd.rollout import SACGRURollout
+        env = VecLoadBalanceEnv(B, S, action_type="continuous", max_steps=10000, **common)
+        ro = SACGRURollout(env, seed=args.seed + rank)
+        handle = env.handle
+
+        def one_step():
+            ro.step()
+    else:
+        from marllb_amd.multi_agent import VecMultiAgentLoadBalanceEnv
+        from marllb_amd.rollout import QMIXRollout
+        if S % 4:
+            raise SystemExit("qmix workload: servers must be 4 agents x k")
+        env = VecMultiAgentLoadBalanceEnv(B, 4, S // 4, action_type="discrete", max_steps=100,
+                                          **common)
+        ro = QMIXRollout(env, seed=args.seed + rank)
+        handle = env.vec.handle
+
+        def one_step():
+            ro.step()
 
     for _ in range(args.warmup):
         one_step()
@@ -142,7 +176,7 @@ def main():
     if world > 1:
         dist.barrier()
     lib = _lib.load()
-    env.handle.check(lib.lbsim_profile_begin(env.handle.h, 4 * args.steps + 8))
+    handle.check(lib.lbsim_profile_begin(handle.h, 4 * args.steps + 8))
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_step()
@@ -152,7 +186,7 @@ def main():
         dist.barrier()
     ms = (ctypes.c_double * 4)()
     cnt = (ctypes.c_int64 * 4)()
-    env.handle.check(lib.lbsim_profile_end(env.handle.h, ms, cnt))
+    handle.check(lib.lbsim_profile_end(handle.h, ms, cnt))
     elapsed = lbdist.max_over_ranks(t1 - t0, dev)
 
     if rank == 0:
@@ -198,7 +232,19 @@ def main():
                          "avg_launch_ms": avg[dom],
                          "kernel_avg_ms": avg, "kernels": per_kernel},
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if args.workload != "rollout":
+            out["config"]["workload"] = {
+                "sac-gru": f"problem-04 SAC-GRU actor (GRU {S * 11}->128, fc 128->256, heads "
+                           f"256->{S}) sampling continuous weights on the GPU each step, "
+                           f"{S} servers (BASELINE configs[3] per GPU)",
+                "qmix": f"problem-05 QMIX: 4 agents x {S // 4} servers, per-agent GRU "
+                        f"Q-networks (obs {4 * (S // 4) + 7 * S}) epsilon-greedy + mixing network "
+                        "(state 74) on the GPU each step (BASELINE configs[4] per GPU)"}[
+                            args.workload]
+            out["data"] = out["data"].replace("random discrete policy",
+                                              "random-init network policy")
+            out["policy_ms_per_step"] = out["ms_per_step"] - sum(avg.values())
+        if world == 1 and not args.no_cpu_baseline and args.workload == "rollout":
             out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
         print(json.dumps(out), flush=True)
     env.close()

@@ -1,0 +1,85 @@
+"""Policy-in-the-loop rollouts on one GPU: the networks of problem-04 / problem-05 drive the batched
+simulator with no host round trip (BASELINE configs[3] and configs[4]).
+
+SACGRURollout  problem-04 Trainer's acting loop (trainer.py:96-126): flattened (S*11) state ->
+               PolicyNetwork.sample (GRU hidden state resident, (1, B, 128)) -> continuous weights
+               -> env.step; hidden state of finished envs zeroed (init_hidden at episode start).
+QMIXRollout    problem-05 QMIXAgent.select_actions (qmix_agent.py:138-178) over the multi-agent
+               facade: per-agent GRU Q-networks, epsilon-greedy argmax, one int per agent, then
+               the mixing network on the chosen Q-values and the global state (qmix_agent.py:110).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+
+from .env import VecLoadBalanceEnv
+from .multi_agent import VecMultiAgentLoadBalanceEnv
+from .policies import AgentQNet, GRUPolicy, QMixer
+
+
+class SACGRURollout:
+    def __init__(self, env: VecLoadBalanceEnv, policy: Optional[GRUPolicy] = None,
+                 deterministic: bool = False, seed: int = 0):
+        self.env = env
+        S = env.num_servers
+        self.policy = (policy or GRUPolicy(S * 11, S, 256, 128)).to(env.device).eval()
+        self.deterministic = deterministic
+        self.gen = torch.Generator(device=env.device)
+        self.gen.manual_seed(seed)
+        self.hidden = torch.zeros(1, env.num_envs, self.policy.gru_dim, device=env.device)
+        self.obs = env.reset()
+
+    @torch.no_grad()
+    def step(self):
+        B = self.env.num_envs
+        state = self.obs.reshape(B, -1)
+        mean, log_std, h1 = self.policy(state, self.hidden)
+        if self.deterministic:
+            action = self.policy.squash(mean)
+        else:
+            eps = torch.randn(mean.shape, device=mean.device, generator=self.gen)
+            action = self.policy.squash(mean + log_std.exp() * eps)
+        obs, rew, done, info = self.env.step(action)
+        self.hidden = h1 * (~done).view(1, B, 1).to(h1.dtype)
+        self.obs = obs
+        return rew, done, info
+
+
+class QMIXRollout:
+    def __init__(self, env: VecMultiAgentLoadBalanceEnv, agents: Optional[List[AgentQNet]] = None,
+                 mixer: Optional[QMixer] = None, n_actions: int = 3, epsilon: float = 0.05,
+                 seed: int = 0):
+        self.env = env
+        A, dev = env.num_agents, env.device
+        self.agents = [(agents[a] if agents else AgentQNet(env.obs_dim, n_actions, 128, 64))
+                       .to(dev).eval() for a in range(A)]
+        self.mixer = (mixer or QMixer(A, env.state_dim, 32, 64)).to(dev).eval()
+        self.epsilon = epsilon
+        self.n_actions = n_actions
+        self.gen = torch.Generator(device=dev)
+        self.gen.manual_seed(seed)
+        self.hidden = [torch.zeros(1, env.num_envs, a.gru_dim, device=dev) for a in self.agents]
+        self.obs = env.reset()
+
+    @torch.no_grad()
+    def step(self):
+        B, A = self.env.num_envs, self.env.num_agents
+        state = self.env.get_state()
+        qs, acts = [], []
+        for a, net in enumerate(self.agents):
+            q, self.hidden[a] = net(self.obs[:, a], self.hidden[a])
+            greedy = q.argmax(dim=1)
+            rnd = torch.randint(0, self.n_actions, (B,), device=q.device, generator=self.gen)
+            explore = torch.rand(B, device=q.device, generator=self.gen) < self.epsilon
+            act = torch.where(explore, rnd, greedy)
+            qs.append(q.gather(1, act.unsqueeze(1)))
+            acts.append(act)
+        actions = torch.stack(acts, dim=1)
+        q_tot = self.mixer(torch.cat(qs, dim=1), state)
+        obs, rewards, done, info = self.env.step(actions)
+        keep = (~done).view(1, B, 1).float()
+        self.hidden = [h * keep for h in self.hidden]
+        self.obs = obs
+        return q_tot, rewards, done, info
