@@ -45,8 +45,15 @@ def main():
     f, w = load(a.dir, "fetch"), load(a.dir, "write")
     sq = {**load(a.dir, "sq1"), **load(a.dir, "sq2")}
     S = a.servers
-    step = {"dynamics_kernel": f"dynamics_kernel<{4 if S <= 4 else 8 if S <= 8 else 16}, 0>",
-            "observe_kernel": f"observe_kernel<{4 if S <= 4 else 8 if S <= 8 else 16}, 0>"}
+    m = 4 if S <= 4 else 8 if S <= 8 else 16
+    # step-mode launches: dynamics_kernel<MAXS, 0, POLICY, TRACE>, observe_kernel<MAXS, 0>
+    prefixes = {"dynamics_kernel": f"dynamics_kernel<{m}, 0", "observe_kernel": f"observe_kernel<{m}, 0"}
+
+    def match(agg, prefix):
+        names = sorted({k for k, _ in agg if k.startswith(prefix)})
+        return names[0] if names else prefix
+
+    step = {n: match(load(a.dir, "fetch"), pfx) for n, pfx in prefixes.items()}
     out = {"batch": a.batch, "servers": S, "fetch_calibration": fetch_factor,
            "write_calibration": write_factor, "bytes_per_launch": {}, "detail": {}}
     for name, kname in step.items():
