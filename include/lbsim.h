@@ -199,6 +199,27 @@ int lbsim_reservoir_features(const float* values, const uint32_t* ts_ms, const u
 int lbsim_agent_obs(const float* obs, int64_t n, int S, int num_agents, int servers_per_agent,
                     float* out, void* stream);
 
+/* Policy-network epilogues (device pointers, row-major), used between hipBLASLt GEMMs by
+ * marllb_amd/policies.py for problem-04 PolicyNetwork (networks.py:82-146) and problem-05
+ * AgentQNetwork (agent_network.py:63-87):
+ *  lbsim_gru_gates: torch.nn.GRU cell from gi = x W_ih^T + b_ih, gh = h W_hh^T + b_hh ([B, 3H],
+ *    gates r, z, n): h_out = (1 - z) n + z h, r = sig(gi_r + gh_r), z = sig(gi_z + gh_z),
+ *    n = tanh(gi_n + r gh_n).
+ *  lbsim_sac_head: y = [B, 2A] = [mean | log_std]: log_std clamped to [min, max]; action =
+ *    tanh(mean) (deterministic) or tanh(mean + exp(log_std) eps), eps ~ N(0,1) from Philox
+ *    (key = seed, counter = (row, step, a, 3 << 24)); times scale plus bias.  log_std_out optional. */
+int lbsim_gru_gates(const float* gi, const float* gh, const float* h, float* h_out, int64_t B,
+                    int H, void* stream);
+int lbsim_sac_head(const float* y, int64_t B, int A, float log_std_min, float log_std_max,
+                   float action_scale, float action_bias, int deterministic, uint64_t seed,
+                   uint32_t step, float* action_out, float* log_std_out, void* stream);
+/* QMIX mixing tail (mixing_network.py:96-116) after the hypernetwork GEMMs, per env b:
+ *  hidden_e = elu(b1[b,e] + sum_a q[b,a] |w1[b, a E + e]|), q_tot[b] = sum_e hidden_e |w2[b,e]| + b2[b]
+ * (row strides *_ld in floats, so the outputs of one concatenated GEMM can be passed directly). */
+int lbsim_qmix_tail(const float* q, const float* w1, int64_t w1_ld, const float* b1,
+                    int64_t b1_ld, const float* w2, int64_t w2_ld, const float* b2, int64_t b2_ld,
+                    int64_t B, int A, int E, float* q_tot, void* stream);
+
 /* Arrival trace for arrival_source == TRACE (the TRACE counterpart of the Poisson draw in
  * env.py's simulation; rows of replay_fork_io.py:95-121's `time<TAB>query` CSV): gap_us[rows]
  * (us since the previous row; row 0: the wrap-around gap) and work[rows] (service demand in mean-1

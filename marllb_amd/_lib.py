@@ -96,6 +96,13 @@ _SIGNATURES = {
     "lbsim_step_outputs_size": (ctypes.c_size_t, []),
     "lbsim_episode_stats": (ctypes.c_int, [_P, _P, _P, _P]),
     "lbsim_reward": (ctypes.c_int, [ctypes.POINTER(LbsimConfig), _P, ctypes.c_int64, _P, _P]),
+    "lbsim_gru_gates": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int64, ctypes.c_int, _P]),
+    "lbsim_sac_head": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int, ctypes.c_float,
+                                      ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_int,
+                                      ctypes.c_uint64, ctypes.c_uint32, _P, _P, _P]),
+    "lbsim_qmix_tail": (ctypes.c_int, [_P, _P, ctypes.c_int64, _P, ctypes.c_int64, _P,
+                                       ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64,
+                                       ctypes.c_int, ctypes.c_int, _P, _P]),
     "lbsim_agent_obs": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, _P, _P]),
     "lbsim_set_trace": (ctypes.c_int, [_P, _P, _P, ctypes.c_int64, _P]),

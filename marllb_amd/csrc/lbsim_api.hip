@@ -14,6 +14,7 @@
 
 #include "../../include/lbsim.h"
 #include "lbsim_kernels.h"
+#include "lbsim_nets.h"
 
 using namespace lbk;
 
@@ -496,6 +497,41 @@ int lbsim_agent_obs(const float* obs, int64_t n, int S, int num_agents, int serv
   const int64_t total = n * num_agents * (4 * servers_per_agent + 7 * S);
   hipLaunchKernelGGL(agent_obs_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, obs, n, S, num_agents, servers_per_agent, out);
+  return hipGetLastError() == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
+}
+
+int lbsim_gru_gates(const float* gi, const float* gh, const float* h, float* h_out, int64_t B,
+                    int H, void* stream) {
+  if (B < 0 || H < 1 || (B > 0 && (!gi || !gh || !h || !h_out))) return LBSIM_EINVAL;
+  if (B == 0) return LBSIM_OK;
+  const int64_t n = B * H;
+  hipLaunchKernelGGL(gru_gates_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, gi, gh, h, h_out, B, H);
+  return hipGetLastError() == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
+}
+
+int lbsim_sac_head(const float* y, int64_t B, int A, float log_std_min, float log_std_max,
+                   float action_scale, float action_bias, int deterministic, uint64_t seed,
+                   uint32_t step, float* action_out, float* log_std_out, void* stream) {
+  if (B < 0 || A < 1 || (B > 0 && (!y || !action_out))) return LBSIM_EINVAL;
+  if (B == 0) return LBSIM_OK;
+  const int64_t n = B * A;
+  hipLaunchKernelGGL(sac_head_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, y, B, A, log_std_min, log_std_max, action_scale,
+                     action_bias, deterministic, (uint32_t)(seed & 0xFFFFFFFFull),
+                     (uint32_t)(seed >> 32), step, action_out, log_std_out);
+  return hipGetLastError() == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
+}
+
+int lbsim_qmix_tail(const float* q, const float* w1, int64_t w1_ld, const float* b1,
+                    int64_t b1_ld, const float* w2, int64_t w2_ld, const float* b2, int64_t b2_ld,
+                    int64_t B, int A, int E, float* q_tot, void* stream) {
+  if (B < 0 || A < 1 || E < 1) return LBSIM_EINVAL;
+  if (B == 0) return LBSIM_OK;
+  if (!q || !w1 || !b1 || !w2 || !b2 || !q_tot) return LBSIM_EINVAL;
+  hipLaunchKernelGGL(qmix_tail_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, q, w1, w1_ld, b1, b1_ld, w2, w2_ld, b2, b2_ld, B, A, E,
+                     q_tot);
   return hipGetLastError() == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
 }
 

@@ -134,3 +134,132 @@ def load_prefixed(module: nn.Module, arrays, prefix: str) -> nn.Module:
           if k.startswith(prefix + ".")}
     module.load_state_dict(sd)
     return module
+
+
+# ---------------------------------------------------------------------------- fused inference
+# A step of a GRU + MLP network as hipBLASLt GEMMs (torch.addmm / baddbmm, ReLU as the GEMM
+# epilogue) with every elementwise stage in our HIP kernels (csrc/lbsim_nets.h): 5 launches per
+# step instead of MIOpen's generic RNN path.  Inference only (no autograd); the torch modules above
+# are the fp32 reference these are tested against.
+
+def _lib_and_stream(device):
+    import ctypes
+
+    from . import _lib
+    lib = _lib.load()
+    return lib, ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _ptr(t: torch.Tensor):
+    import ctypes
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _linear_relu(x, w, b):
+    """x @ w.T + b with ReLU fused into the GEMM epilogue when torch exposes it."""
+    f = getattr(torch, "_addmm_activation", None)
+    if f is not None:
+        return f(b, x, w.t())
+    return torch.relu_(torch.addmm(b, x, w.t()))
+
+
+class FusedGRUPolicy:
+    """GRUPolicy.forward + sample for inference on the GPU (networks.py:82-146)."""
+
+    def __init__(self, policy: GRUPolicy, seed: int = 0):
+        g = policy.gru
+        self.p = policy
+        self.w_ih, self.b_ih = g.weight_ih_l0.detach(), g.bias_ih_l0.detach()
+        self.w_hh, self.b_hh = g.weight_hh_l0.detach(), g.bias_hh_l0.detach()
+        self.w1, self.b1 = policy.fc1.weight.detach(), policy.fc1.bias.detach()
+        self.wh = torch.cat([policy.fc_mean.weight, policy.fc_logstd.weight]).detach().contiguous()
+        self.bh = torch.cat([policy.fc_mean.bias, policy.fc_logstd.bias]).detach().contiguous()
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.step_no = 0
+
+    @torch.no_grad()
+    def __call__(self, state: torch.Tensor, hidden: torch.Tensor, deterministic: bool = False):
+        """state (B, I), hidden (B, H) -> action (B, A), hidden_new (B, H), log_std (B, A)."""
+        from . import _lib
+        B, A, H = state.shape[0], self.p.action_dim, self.p.gru_dim
+        lib, stream = _lib_and_stream(state.device)
+        gi = torch.addmm(self.b_ih, state, self.w_ih.t())
+        gh = torch.addmm(self.b_hh, hidden, self.w_hh.t())
+        h1 = torch.empty_like(hidden)
+        _lib.check(lib.lbsim_gru_gates(_ptr(gi), _ptr(gh), _ptr(hidden), _ptr(h1), B, H, stream))
+        y = torch.addmm(self.bh, _linear_relu(h1, self.w1, self.b1), self.wh.t())
+        action = torch.empty((B, A), dtype=torch.float32, device=state.device)
+        log_std = torch.empty_like(action)
+        _lib.check(lib.lbsim_sac_head(
+            _ptr(y), B, A, float(self.p.log_std_min), float(self.p.log_std_max),
+            float(self.p.action_scale), float(self.p.action_bias), int(deterministic), self.seed,
+            self.step_no & 0xFFFFFFFF, _ptr(action), _ptr(log_std), stream))
+        self.step_no += 1
+        return action, h1, log_std
+
+
+class FusedAgentQNets:
+    """A problem-05 AgentQNetworks (one per agent) evaluated together: per layer one batched GEMM
+    over the stacked agent weights, GRU gates in lbsim_gru_gates."""
+
+    def __init__(self, agents):
+        st = lambda f: torch.stack([f(a).detach() for a in agents]).contiguous()  # noqa: E731
+        self.A = len(agents)
+        self.H = agents[0].gru_dim
+        self.w_ih = st(lambda a: a.gru.weight_ih_l0.t())  # (A, I, 3H)
+        self.b_ih = st(lambda a: a.gru.bias_ih_l0).unsqueeze(1)
+        self.w_hh = st(lambda a: a.gru.weight_hh_l0.t())
+        self.b_hh = st(lambda a: a.gru.bias_hh_l0).unsqueeze(1)
+        self.w1, self.b1 = st(lambda a: a.fc1.weight.t()), st(lambda a: a.fc1.bias).unsqueeze(1)
+        self.w2, self.b2 = st(lambda a: a.fc2.weight.t()), st(lambda a: a.fc2.bias).unsqueeze(1)
+        self.w3, self.b3 = st(lambda a: a.fc3.weight.t()), st(lambda a: a.fc3.bias).unsqueeze(1)
+
+    @torch.no_grad()
+    def __call__(self, obs: torch.Tensor, hidden: torch.Tensor):
+        """obs (A, B, I), hidden (A, B, H) -> q (A, B, n_actions), hidden_new (A, B, H)."""
+        from . import _lib
+        A, B, H = obs.shape[0], obs.shape[1], self.H
+        lib, stream = _lib_and_stream(obs.device)
+        gi = torch.baddbmm(self.b_ih, obs, self.w_ih)
+        gh = torch.baddbmm(self.b_hh, hidden, self.w_hh)
+        h1 = torch.empty_like(hidden)
+        _lib.check(lib.lbsim_gru_gates(_ptr(gi), _ptr(gh), _ptr(hidden), _ptr(h1), A * B, H,
+                                       stream))
+        x = torch.relu_(torch.baddbmm(self.b1, h1, self.w1))
+        x = torch.relu_(torch.baddbmm(self.b2, x, self.w2))
+        return torch.baddbmm(self.b3, x, self.w3), h1
+
+
+class FusedQMixer:
+    """QMixer.forward: the four hypernetwork first layers as one GEMM on the state, the second
+    layers as GEMMs, then abs / bmm / elu / bmm per env in lbsim_qmix_tail."""
+
+    def __init__(self, mixer: QMixer):
+        m = mixer
+        self.A, self.E = m.num_agents, m.mixing_embed_dim
+        firsts = [m.hyper_w1[0], m.hyper_b1[0], m.hyper_w2[0], m.hyper_b2[0]]
+        self.w0 = torch.cat([l.weight for l in firsts]).detach().contiguous()
+        self.b0 = torch.cat([l.bias for l in firsts]).detach().contiguous()
+        he = m.hypernet_embed_dim
+        self.cuts = [he, he + self.E, 2 * he + self.E, 3 * he + self.E]
+        self.w1, self.bw1 = m.hyper_w1[2].weight.detach(), m.hyper_w1[2].bias.detach()
+        self.w2, self.bw2 = m.hyper_w2[2].weight.detach(), m.hyper_w2[2].bias.detach()
+        self.wb2, self.bb2 = m.hyper_b2[2].weight.detach(), m.hyper_b2[2].bias.detach()
+
+    @torch.no_grad()
+    def __call__(self, agent_qs: torch.Tensor, state: torch.Tensor) -> torch.Tensor:
+        from . import _lib
+        B = agent_qs.shape[0]
+        lib, stream = _lib_and_stream(state.device)
+        z = torch.addmm(self.b0, state, self.w0.t())  # [hw1 | b1 | hw2 | hb2] pre-activation
+        c0, c1, c2, c3 = self.cuts
+        b1 = z[:, c0:c1]                               # hyper_b1 has no ReLU
+        w1 = torch.addmm(self.bw1, torch.relu(z[:, :c0]), self.w1.t())
+        w2 = torch.addmm(self.bw2, torch.relu(z[:, c1:c2]), self.w2.t())
+        b2 = torch.addmm(self.bb2, torch.relu(z[:, c2:c3]), self.wb2.t())
+        q_tot = torch.empty((B, 1), dtype=torch.float32, device=state.device)
+        qs = agent_qs.contiguous()
+        _lib.check(lib.lbsim_qmix_tail(_ptr(qs), _ptr(w1), w1.stride(0), _ptr(b1), b1.stride(0),
+                                       _ptr(w2), w2.stride(0), _ptr(b2), b2.stride(0), B, self.A,
+                                       self.E, _ptr(q_tot), stream))
+        return q_tot

@@ -16,15 +16,18 @@ import torch
 
 from .env import VecLoadBalanceEnv
 from .multi_agent import VecMultiAgentLoadBalanceEnv
-from .policies import AgentQNet, GRUPolicy, QMixer
+from .policies import AgentQNet, FusedAgentQNets, FusedGRUPolicy, FusedQMixer, GRUPolicy, QMixer
 
 
 class SACGRURollout:
     def __init__(self, env: VecLoadBalanceEnv, policy: Optional[GRUPolicy] = None,
-                 deterministic: bool = False, seed: int = 0):
+                 deterministic: bool = False, seed: int = 0, fused: bool = True):
         self.env = env
         S = env.num_servers
         self.policy = (policy or GRUPolicy(S * 11, S, 256, 128)).to(env.device).eval()
+        # fused: hipBLASLt GEMMs + lbsim_gru_gates / lbsim_sac_head (noise from Philox);
+        # unfused: the torch module (noise from torch's generator)
+        self.fused = FusedGRUPolicy(self.policy, seed=seed) if fused else None
         self.deterministic = deterministic
         self.gen = torch.Generator(device=env.device)
         self.gen.manual_seed(seed)
@@ -35,12 +38,16 @@ class SACGRURollout:
     def step(self):
         B = self.env.num_envs
         state = self.obs.reshape(B, -1)
-        mean, log_std, h1 = self.policy(state, self.hidden)
-        if self.deterministic:
-            action = self.policy.squash(mean)
+        if self.fused is not None:
+            action, h, _ = self.fused(state, self.hidden[0], self.deterministic)
+            h1 = h.unsqueeze(0)
         else:
-            eps = torch.randn(mean.shape, device=mean.device, generator=self.gen)
-            action = self.policy.squash(mean + log_std.exp() * eps)
+            mean, log_std, h1 = self.policy(state, self.hidden)
+            if self.deterministic:
+                action = self.policy.squash(mean)
+            else:
+                eps = torch.randn(mean.shape, device=mean.device, generator=self.gen)
+                action = self.policy.squash(mean + log_std.exp() * eps)
         obs, rew, done, info = self.env.step(action)
         self.hidden = h1 * (~done).view(1, B, 1).to(h1.dtype)
         self.obs = obs
@@ -50,7 +57,7 @@ class SACGRURollout:
 class QMIXRollout:
     def __init__(self, env: VecMultiAgentLoadBalanceEnv, agents: Optional[List[AgentQNet]] = None,
                  mixer: Optional[QMixer] = None, n_actions: int = 3, epsilon: float = 0.05,
-                 seed: int = 0):
+                 seed: int = 0, fused: bool = True):
         self.env = env
         A, dev = env.num_agents, env.device
         self.agents = [(agents[a] if agents else AgentQNet(env.obs_dim, n_actions, 128, 64))
@@ -61,12 +68,28 @@ class QMIXRollout:
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(seed)
         self.hidden = [torch.zeros(1, env.num_envs, a.gru_dim, device=dev) for a in self.agents]
+        self.fused = (FusedAgentQNets(self.agents), FusedQMixer(self.mixer)) if fused else None
+        if fused:
+            self.hidden = torch.zeros(A, env.num_envs, self.agents[0].gru_dim, device=dev)
         self.obs = env.reset()
 
     @torch.no_grad()
     def step(self):
         B, A = self.env.num_envs, self.env.num_agents
         state = self.env.get_state()
+        if self.fused is not None:
+            nets, mixer = self.fused
+            q, self.hidden = nets(self.obs.transpose(0, 1).contiguous(), self.hidden)  # (A, B, n)
+            greedy = q.argmax(dim=2)
+            rnd = torch.randint(0, self.n_actions, (A, B), device=q.device, generator=self.gen)
+            explore = torch.rand((A, B), device=q.device, generator=self.gen) < self.epsilon
+            act = torch.where(explore, rnd, greedy)
+            chosen = q.gather(2, act.unsqueeze(2)).squeeze(2).t().contiguous()  # (B, A)
+            q_tot = mixer(chosen, state)
+            obs, rewards, done, info = self.env.step(act.t())
+            self.hidden = self.hidden * (~done).view(1, B, 1).float()
+            self.obs = obs
+            return q_tot, rewards, done, info
         qs, acts = [], []
         for a, net in enumerate(self.agents):
             q, self.hidden[a] = net(self.obs[:, a], self.hidden[a])

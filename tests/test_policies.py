@@ -57,3 +57,41 @@ def test_reference_state_dict_names(g):
 @pytest.mark.gpu
 def test_mirrors_match_reference_gpu(g):
     check(g, "cuda:0")
+
+
+@pytest.mark.gpu
+def test_fused_inference_matches_modules_gpu(g):
+    """The fused forms (hipBLASLt GEMMs + lbsim_gru_gates / lbsim_sac_head / lbsim_qmix_tail)
+    against the torch modules on the reference weights, fp32, 1e-5."""
+    from marllb_amd.policies import FusedAgentQNets, FusedGRUPolicy, FusedQMixer
+    dev = "cuda:0"
+    pol, q, mix = nets(g, dev)
+    t = lambda k: torch.from_numpy(g[k]).to(dev)  # noqa: E731
+    x, h = t("policy_x"), t("policy_h")
+    with torch.no_grad():
+        mean, log_std, h1 = pol(x, h)
+        act, fh1, fls = FusedGRUPolicy(pol)(x, h[0].contiguous(), deterministic=True)
+    np.testing.assert_allclose(act.cpu().numpy(), g["policy_det_action"], **TOL)
+    np.testing.assert_allclose(fh1.cpu().numpy(), g["policy_h1"][0], **TOL)
+    np.testing.assert_allclose(fls.cpu().numpy(), g["policy_log_std"], **TOL)
+    # stochastic: tanh(mean + std * eps) stays in (-1, 1), reproducible per (seed, step)
+    a1, _, _ = FusedGRUPolicy(pol, seed=5)(x, h[0].contiguous())
+    a2, _, _ = FusedGRUPolicy(pol, seed=5)(x, h[0].contiguous())
+    assert torch.equal(a1, a2) and bool((a1.abs() <= 1).all())
+    assert not torch.equal(a1, act)
+    # 4 agents with different weights through one batched pass
+    agents = [load_prefixed(AgentQNet(128, 3, 128, 64), g, "agentq").to(dev) for _ in range(4)]
+    with torch.no_grad():
+        for k, a in enumerate(agents[1:], 1):
+            for p in a.parameters():
+                p.mul_(1.0 + 0.1 * k)
+    obs = torch.randn(4, 64, 128, device=dev)
+    hid = torch.randn(4, 64, 64, device=dev) * 0.5
+    fq, fh = FusedAgentQNets(agents)(obs, hid)
+    for a, net in enumerate(agents):
+        with torch.no_grad():
+            rq, rh = net(obs[a], hid[a:a + 1])
+        np.testing.assert_allclose(fq[a].cpu().numpy(), rq.cpu().numpy(), **TOL)
+        np.testing.assert_allclose(fh[a].cpu().numpy(), rh[0].cpu().numpy(), **TOL)
+    fq = FusedQMixer(mix)(t("mixer_qs"), t("mixer_state"))
+    np.testing.assert_allclose(fq.cpu().numpy(), g["mixer_qtot"], **TOL)
