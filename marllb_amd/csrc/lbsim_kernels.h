@@ -763,15 +763,18 @@ __device__ __forceinline__ T pairwise8(int n, int j, F term) {
 // groups hit distinct banks.
 constexpr int KP = K + 8;
 
-template <int MAXS>
+// Scratch of one chunk of up to 4 servers (observe_env walks an env's servers in chunks, so the LDS
+// footprint -- and the occupancy -- is the same at S = 4, 8 and 16).
+constexpr int kObsChunk = 4;
+
 struct ObsScratch {
+  static constexpr int MAXS = kObsChunk;
   uint32_t vals[2 * MAXS][KP];  // reservoir r = 2s (fct) / 2s+1 (duration), slot order; then
                                 // sorted, transposed: sorted position p at (p & 15) * 8 + (p >> 4)
   float wts[MAXS][KP];          // decay weights of server s (shared by its two reservoirs)
   int n[2 * MAXS];             // valid slots per reservoir
   float mean[2 * MAXS], sd[2 * MAXS], md[2 * MAXS], p90[2 * MAXS], p90d[2 * MAXS];
   double swt[MAXS], svw[2 * MAXS];
-  float obs[MAXS * NF];
   uint8_t perm[8][K];           // two-pass sort: slot at each position after the first pass
 };
 
@@ -848,13 +851,14 @@ __device__ __forceinline__ float sample_value(uint32_t raw) {
 // us << 7 | slot must stay below the 0xFFFFFFFF filler of empty slots.
 constexpr uint32_t kPackLimit = (1u << 25) - 1u;
 
-// The 11-column observation of one env (features.py:256-286) into sc.obs, S servers.
-// Slot-order sums follow numpy exactly (reservoir.py:143-155); order statistics come from the
-// sorted keys (reservoir.py:144, 165-196).  All values >= 0, so float bits order like floats.
-template <int MAXS, bool US>
-__device__ __forceinline__ void observe_env(const DevState& st, const SimParams& p, size_t b,
-                                            ObsScratch<MAXS>& sc, int lane) {
-  const int S = p.S;
+// The 11-column observation rows (features.py:256-286) of servers [s_base, s_base + S), S <= 4,
+// of env b into obs_out.  Slot-order sums follow numpy exactly (reservoir.py:143-155); order
+// statistics come from the sorted keys (reservoir.py:144, 165-196).
+template <bool US>
+__device__ __forceinline__ void observe_chunk(const DevState& st, const SimParams& p, size_t b,
+                                              int s_base, int S, ObsScratch& sc, float* obs_out,
+                                              int lane) {
+  const size_t srow = b * (size_t)p.S + (size_t)s_base;  // first (env, server) of the chunk
   const int R = 2 * S;
   const int g = lane >> 3, j = lane & 7;
   // ---- phase 1: reservoirs into LDS, decay weights relative to each server's newest sample.
@@ -865,7 +869,7 @@ __device__ __forceinline__ void observe_env(const DevState& st, const SimParams&
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int s = s0 + u;
-      const size_t sb = b * (size_t)S + (size_t)(s < S ? s : 0);
+      const size_t sb = srow + (size_t)(s < S ? s : 0);
       const uint32_t rc = s < S ? st.res_count[sb] : 0u;
       nn[u] = rc < (uint32_t)K ? (int)rc : K;
 #pragma unroll
@@ -1058,15 +1062,28 @@ __device__ __forceinline__ void observe_env(const DevState& st, const SimParams&
     const int s = e / NF, c = e - s * NF;
     float v;
     if (c == 0) {
-      v = (float)(st.hc[b * (size_t)S + (size_t)s] >> 16);
+      v = (float)(st.hc[srow + (size_t)s] >> 16);
     } else {
       const int r = 2 * s + (c >= 6 ? 1 : 0);
       const int f = (c - 1) % 5;
       v = f == 0 ? sc.mean[r] : f == 1 ? sc.p90[r] : f == 2 ? sc.sd[r] : f == 3 ? sc.md[r] : sc.p90d[r];
     }
-    sc.obs[e] = v;
+    obs_out[s_base * NF + e] = v;
   }
   __syncthreads();
+}
+
+// The (S, 11) observation of env b into obs_out, 4 servers at a time.
+template <int MAXS, bool US>
+__device__ __forceinline__ void observe_env(const DevState& st, const SimParams& p, size_t b,
+                                            ObsScratch& sc, float* obs_out, int lane) {
+  if constexpr (MAXS <= kObsChunk) {
+    observe_chunk<US>(st, p, b, 0, p.S, sc, obs_out, lane);
+  } else {
+    for (int s0 = 0; s0 < p.S; s0 += kObsChunk)
+      observe_chunk<US>(st, p, b, s0, p.S - s0 < kObsChunk ? p.S - s0 : kObsChunk, sc, obs_out,
+                        lane);
+  }
 }
 
 // ================================================================ reward (rewards.py)
@@ -1167,10 +1184,10 @@ struct ObsOutputs {
   double* ep_ret;
 };
 
-// Waves per SIMD the LDS footprint allows (ObsScratch: 8 / 15 / 29 KB); at S <= 4 this caps
-// the kernel at 96 VGPRs.
+// Waves per SIMD the LDS footprint allows (ObsScratch of one 4-server chunk, ~8 KB at every S);
+// caps the kernel at 96 VGPRs.
 template <int MAXS>
-constexpr int kObsWaves = MAXS <= 4 ? 5 : (MAXS <= 8 ? 3 : 2);
+constexpr int kObsWaves = MAXS <= kObsChunk ? 5 : 4;
 
 template <int MAXS, int MODE>
 __global__ void __launch_bounds__(64, kObsWaves<MAXS>)
@@ -1179,10 +1196,10 @@ __global__ void __launch_bounds__(64, kObsWaves<MAXS>)
   const size_t b = blockIdx.x;
   const int lane = threadIdx.x;
   if (mode == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
-  __shared__ ObsScratch<MAXS> sc;
+  __shared__ ObsScratch sc;
+  __shared__ float s_obs[MAXS * NF];
   const int S = p.S;
-  observe_env<MAXS, true>(st, p, b, sc, lane);
-  const float* s_obs = sc.obs;
+  observe_env<MAXS, true>(st, p, b, sc, s_obs, lane);
 
   if (mode == kModeStep && lane == 0) {
     const double r = reward_of(s_obs, S, p.reward_metric, p.reward_field);
@@ -1232,7 +1249,8 @@ __global__ void __launch_bounds__(64)
                     float decay_c, float* out) {
   const int64_t r0 = (int64_t)blockIdx.x * 4;
   const int lane = threadIdx.x;
-  __shared__ ObsScratch<4> sc;
+  __shared__ ObsScratch sc;
+  __shared__ float fobs[4 * NF];
   const int S = (int)(n - r0 < 4 ? n - r0 : 4);
   DevState st{};
   st.res_fct = reinterpret_cast<uint32_t*>(const_cast<float*>(values)) + r0 * K;
@@ -1246,10 +1264,10 @@ __global__ void __launch_bounds__(64)
   p.S = S;
   p.decay_c = decay_c;
   __syncthreads();
-  observe_env<4, false>(st, p, 0, sc, lane);
+  observe_env<4, false>(st, p, 0, sc, fobs, lane);
   for (int e = lane; e < S * 5; e += 64) {
     const int s = e / 5, f = e - s * 5;
-    out[(r0 + s) * 5 + f] = sc.obs[s * NF + 1 + f];
+    out[(r0 + s) * 5 + f] = fobs[s * NF + 1 + f];
   }
 }
 
