@@ -126,10 +126,16 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("for --gpus N > 1 launch with torch.distributed.run --nproc-per-node N")
+    # one process per GPU; LBSIM_DIST_BACKEND=gloo rehearses several ranks on fewer GPUs
+    backend = os.environ.get("LBSIM_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     B, S = args.batch, args.servers
     tr = None
@@ -187,7 +193,7 @@ def main():
     ms = (ctypes.c_double * 4)()
     cnt = (ctypes.c_int64 * 4)()
     handle.check(lib.lbsim_profile_end(handle.h, ms, cnt))
-    elapsed = lbdist.max_over_ranks(t1 - t0, dev)
+    elapsed = lbdist.max_over_ranks(t1 - t0, dev if backend == "nccl" else None)
 
     if rank == 0:
         value = lbdist.throughput(shard, args.steps, elapsed)
