@@ -161,7 +161,7 @@ std::vector<Section> sections(lbsim_t* h) {
       {(void**)&s.clock, B * 4},      {(void**)&s.ep_step, B * 4},   {(void**)&s.dropped, B * 4},
       {(void**)&s.norm_count, B * 4}, {(void**)&s.ep_return, B * 8}, {(void**)&s.hc, BS * 4},
       {(void**)&s.last_tc, BS * 4},   {(void**)&s.res_count, BS * 4}, {(void**)&s.ring, BSQ * 8},
-      {(void**)&s.res_fct, BSK * 4},  {(void**)&s.res_dur, BSK * 4}, {(void**)&s.res_ts, BSK * 4},
+      {(void**)&s.res, BSK * 12},
   };
   if (h->cfg.normalize_obs) {
     v.push_back({(void**)&s.norm_mean, BS * NF * 8});

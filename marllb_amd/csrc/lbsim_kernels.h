@@ -53,9 +53,11 @@ struct DevState {
   int2* ring;
   // reservoirs [B*S*K]; flow completion time / duration samples in integer microseconds (the
   // feature value of a sample is (float)us * 1e-6f seconds, us_to_seconds)
-  uint32_t* res_fct;
-  uint32_t* res_dur;
-  uint32_t* res_ts;     // sample time, integer ms since episode start
+  uint3* res;           // [B*S*K] slot records {fct us, duration us, timestamp ms}: an insert is
+                        // one 12-B store (one partial line, not three), observe reads dwordx3
+  // stateless features API only: caller's separate value / timestamp arrays [n*K]
+  const uint32_t* feat_vals;
+  const uint32_t* feat_ts;
   // running normalisation [B*S*11] (nullptr when disabled)
   double* norm_mean;
   double* norm_std;
@@ -454,9 +456,8 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     }
     if (comp && slot >= 0) {
       const uint32_t r = (b0 + (uint32_t)smin) * (uint32_t)K + (uint32_t)slot;
-      st.res_fct[r] = (uint32_t)(tc - h_ta);
-      st.res_dur[r] = (uint32_t)(tc - start_c);
-      st.res_ts[r] = base_ms + (base_rem + (uint32_t)tc) / 1000u;
+      st.res[r] = make_uint3((uint32_t)(tc - h_ta), (uint32_t)(tc - start_c),
+                             base_ms + (base_rem + (uint32_t)tc) / 1000u);
     }
     // rare: the queue is longer than the window; bring entry WL-1 (after this pop) into LDS
     if (comp && c_cnt - 1 >= WL) {
@@ -876,9 +877,16 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
       for (int h = 0; h < 2; ++h) {
         const int slot = lane + 64 * h;
         const bool v = slot < nn[u];
-        f[u][h] = v ? st.res_fct[sb * K + slot] : 0u;
-        d[u][h] = v ? st.res_dur[sb * K + slot] : 0u;
-        t[u][h] = v ? st.res_ts[sb * K + slot] : 0u;
+        if constexpr (US) {  // simulator: one 12-B record per slot
+          const uint3 rec = v ? st.res[sb * K + slot] : make_uint3(0u, 0u, 0u);
+          f[u][h] = rec.x;
+          d[u][h] = rec.y;
+          t[u][h] = rec.z;
+        } else {  // features API: one value array serves as both "fct" and "duration"
+          f[u][h] = v ? st.feat_vals[sb * K + slot] : 0u;
+          d[u][h] = f[u][h];
+          t[u][h] = v ? st.feat_ts[sb * K + slot] : 0u;
+        }
       }
     }
 #pragma unroll
@@ -1253,9 +1261,8 @@ __global__ void __launch_bounds__(64)
   __shared__ float fobs[4 * NF];
   const int S = (int)(n - r0 < 4 ? n - r0 : 4);
   DevState st{};
-  st.res_fct = reinterpret_cast<uint32_t*>(const_cast<float*>(values)) + r0 * K;
-  st.res_dur = st.res_fct;
-  st.res_ts = const_cast<uint32_t*>(ts) + r0 * K;
+  st.feat_vals = reinterpret_cast<const uint32_t*>(values) + r0 * K;
+  st.feat_ts = ts + r0 * K;
   st.res_count = const_cast<uint32_t*>(counts) + r0;
   __shared__ uint32_t hc0[4];
   if (lane < 4) hc0[lane] = 0;

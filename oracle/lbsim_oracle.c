@@ -293,8 +293,9 @@ typedef struct oracle {
   double* ep_return;
   uint32_t* hc; int32_t* last_tc; uint32_t* res_count;
   int32_t* ring; /* [B*S*Q][2] = {t_complete, t_arrival} */
-  uint32_t* res_fct; uint32_t* res_dur; /* integer microseconds; value = (float)us * 1e-6f */
-  uint32_t* res_ts;
+  /* reservoir slot records [B*S*K][3] = {fct us, duration us, timestamp ms}; the feature value
+   * of a sample is (float)us * 1e-6f */
+  uint32_t* res;
   double* norm_mean; double* norm_std;
   /* TRACE arrivals (lbsim_set_trace semantics): us gap before each row, mean-1 work */
   uint32_t* trace_gap; float* trace_work; uint32_t trace_rows;
@@ -320,7 +321,7 @@ oracle_t* oracle_create(const lbsim_config_t* cfg) {
   o->threads = 1;
   const size_t B = o->B, BS = (size_t)o->B * o->S, BSQ = BS * o->Q, BSK = BS * K;
   const size_t sz[] = {B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4,
-                       B * 8, BS * 4, BS * 4, BS * 4, BSQ * 8, BSK * 4, BSK * 4, BSK * 4,
+                       B * 8, BS * 4, BS * 4, BS * 4, BSQ * 8, BSK * 12,
                        cfg->normalize_obs ? BS * NF * 8 : 0, cfg->normalize_obs ? BS * NF * 8 : 0};
   size_t total = 0;
   for (size_t i = 0; i < sizeof(sz) / sizeof(sz[0]); ++i) total += sz[i];
@@ -333,8 +334,7 @@ oracle_t* oracle_create(const lbsim_config_t* cfg) {
                    (void**)&o->clock, (void**)&o->ep_step, (void**)&o->dropped,
                    (void**)&o->norm_count, (void**)&o->ep_return, (void**)&o->hc,
                    (void**)&o->last_tc, (void**)&o->res_count, (void**)&o->ring,
-                   (void**)&o->res_fct, (void**)&o->res_dur, (void**)&o->res_ts,
-                   (void**)&o->norm_mean, (void**)&o->norm_std};
+                   (void**)&o->res, (void**)&o->norm_mean, (void**)&o->norm_std};
   for (size_t i = 0; i < sizeof(sz) / sizeof(sz[0]); ++i) {
     *ptrs[i] = sz[i] ? (void*)p : NULL;
     p += sz[i];
@@ -457,9 +457,9 @@ static void reservoir_add(env_ctx* e, int s, uint32_t fct, uint32_t dur, uint32_
   }
   if (slot >= 0) {
     const size_t r = sb * K + (size_t)slot;
-    o->res_fct[r] = fct;
-    o->res_dur[r] = dur;
-    o->res_ts[r] = ts_ms;
+    o->res[3 * r + 0] = fct;
+    o->res[3 * r + 1] = dur;
+    o->res[3 * r + 2] = ts_ms;
   }
   if (c != 0xFFFFFFFFu) o->res_count[sb] = c + 1u;
 }
@@ -654,11 +654,13 @@ static void observe(oracle_t* o, size_t b, float* obs_out, float* reward_out, ui
     const int n = rc < (uint32_t)K ? (int)rc : K;
     float w[K];
     uint64_t wq[K];
-    slot_weights(o->res_ts + sb * K, n, o->decay_c, w, wq);
+    uint32_t ts[K];
+    for (int i = 0; i < n; ++i) ts[i] = o->res[3 * (sb * K + (size_t)i) + 2];
+    slot_weights(ts, n, o->decay_c, w, wq);
     float ff[5], fd[5], vf[K], vd[K];
     for (int i = 0; i < n; ++i) {
-      vf[i] = us_to_seconds(o->res_fct[sb * K + i]);
-      vd[i] = us_to_seconds(o->res_dur[sb * K + i]);
+      vf[i] = us_to_seconds(o->res[3 * (sb * K + (size_t)i) + 0]);
+      vd[i] = us_to_seconds(o->res[3 * (sb * K + (size_t)i) + 1]);
     }
     features_one(vf, w, wq, n, ff);
     features_one(vd, w, wq, n, fd);

@@ -11,8 +11,7 @@ def sections(B, S, Q, normalize):
            ("clock", np.uint32, B), ("ep_step", np.int32, B), ("dropped", np.uint32, B),
            ("norm_count", np.int32, B), ("ep_return", np.float64, B), ("hc", np.uint32, BS),
            ("last_tc", np.int32, BS), ("res_count", np.uint32, BS), ("ring", np.int32, BS * Q * 2),
-           ("res_fct", np.uint32, BS * K), ("res_dur", np.uint32, BS * K),
-           ("res_ts", np.uint32, BS * K)]
+           ("res", np.uint32, BS * K * 3)]
     if normalize:
         out += [("norm_mean", np.float64, BS * NF), ("norm_std", np.float64, BS * NF)]
     return out
@@ -25,6 +24,8 @@ def parse(buf: bytes, B, S, Q, normalize):
         d[name] = np.frombuffer(buf[off:off + nb], dtype=dt)
         off += nb
     assert off == len(buf), (off, len(buf))
+    rec = d["res"].reshape(-1, 3)  # slot records {fct us, duration us, timestamp ms}
+    d["res_fct"], d["res_dur"], d["res_ts"] = rec[:, 0], rec[:, 1], rec[:, 2]
     return d
 
 
