@@ -65,6 +65,8 @@ def parse():
                     help="replay data/traces/<name>.npz (e.g. poisson_for_loop_rate_500: configs[2])")
     ap.add_argument("--policy", default="sed", help="sed | sed2 | lsq | lsq2 | alias")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dyn-mapping", default="auto", choices=["auto", "env", "server"],
+                    help="dynamics kernel mapping: one lane per env / per server (same results)")
     return ap.parse_args()
 
 
@@ -143,7 +145,7 @@ def main():
         from marllb_amd import trace
         tr = trace.builtin(args.trace)
     common = dict(device=dev, seed=args.seed, env_id_offset=shard.env_id_offset, autoreset=True,
-                  assign_policy=args.policy, trace=tr)
+                  assign_policy=args.policy, trace=tr, dyn_mapping=args.dyn_mapping)
     torch.manual_seed(args.seed)  # network init (random weights of the reference architecture)
     if args.workload == "rollout":
         env = VecLoadBalanceEnv(B, S, max_steps=10000, **common)
@@ -231,7 +233,7 @@ def main():
                        "assign_policy": args.policy,
                        "envs_per_gpu": B, "servers": S, "global_batch": world * B,
                        "step_interval_s": 0.25, "autoreset": True,
-                       "parallelism": f"env-shard x{world}"},
+                       "parallelism": f"env-shard x{world}", "dyn_mapping": args.dyn_mapping},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "algorithmic_bytes_per_launch": ab,

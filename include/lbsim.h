@@ -77,6 +77,14 @@ enum lbsim_assign_policy {
  * trace set with lbsim_set_trace (data/trace/poisson_for_loop/rate_N.csv). */
 enum lbsim_arrival_source { LBSIM_ARRIVAL_POISSON = 0, LBSIM_ARRIVAL_TRACE = 1 };
 
+/* Dynamics-kernel mapping; every choice produces the same bits.  AUTO picks SERVER_PER_LANE when
+ * one lane per env would leave most of the GPU's SIMDs idle (small batches). */
+enum lbsim_dyn_mapping {
+  LBSIM_DYN_AUTO = 0,
+  LBSIM_DYN_ENV_PER_LANE = 1,    /* one lane = one env (large batches)                      */
+  LBSIM_DYN_SERVER_PER_LANE = 2  /* pow2(S) lanes = one env, one lane per server            */
+};
+
 /*
  * POD configuration.  Mirrors the LoadBalanceEnv kwargs (env.py:71-87) plus the simulator knobs
  * the reference leaves implicit.  Fill with lbsim_config_default() and override.
@@ -106,7 +114,8 @@ typedef struct lbsim_config {
   float decay_factor;        /* reservoir decay, default 0.9          reservoir.py:106       */
   int32_t queue_capacity;    /* Q: max flows in flight per server (1..64), default 32       */
   int32_t warmup_steps;      /* simulated steps run inside reset() with weights 1.0         */
-  int32_t reserved[8];
+  int32_t dyn_mapping;       /* lbsim_dyn_mapping: how envs map onto lanes (results identical) */
+  int32_t reserved[7];
 } lbsim_config_t;
 
 typedef struct lbsim lbsim_t; /* opaque handle */

@@ -21,6 +21,7 @@ MAX_DISCRETE = 8
 OK, EINVAL, ENOMEM, EDEVICE, ESHAPE, ENOTSUP = 0, -1, -2, -3, -4, -5
 ACTION_DISCRETE, ACTION_CONTINUOUS = 0, 1
 ARRIVAL_POISSON, ARRIVAL_TRACE = 0, 1
+DYN_MAPPINGS = ("auto", "env", "server")  # lbsim_dyn_mapping
 DTYPE_I32, DTYPE_I64, DTYPE_F32 = 0, 1, 2
 METRICS = ["jain", "variance", "std", "cv", "max", "min", "product", "range", "gini"]
 POLICIES = ["sed", "sed2", "lsq", "lsq2", "alias"]
@@ -51,7 +52,8 @@ class LbsimConfig(ctypes.Structure):
         ("decay_factor", ctypes.c_float),
         ("queue_capacity", ctypes.c_int32),
         ("warmup_steps", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 8),
+        ("dyn_mapping", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 7),
     ]
 
 

@@ -14,6 +14,7 @@
 
 #include "../../include/lbsim.h"
 #include "lbsim_kernels.h"
+#include "lbsim_dyn_group.h"
 #include "lbsim_nets.h"
 
 using namespace lbk;
@@ -29,6 +30,7 @@ struct lbsim {
   lbsim_config_t cfg;
   Profiler prof;
   int device;
+  int simds;  // SIMDs of the device (CUs x 4): the env-per-lane mapping fills them at B >= 64·simds
   int B, S, Q;
   DevState st;
   SimParams prm;
@@ -114,6 +116,8 @@ int validate(const lbsim_config_t* c, char* msg, size_t n) {
   if (c->queue_capacity < 1 || c->queue_capacity > 64)
     return bad("queue_capacity must be in [1, 64]");
   if (c->warmup_steps < 0 || c->warmup_steps > 100000) return bad("warmup_steps out of range");
+  if (c->dyn_mapping < LBSIM_DYN_AUTO || c->dyn_mapping > LBSIM_DYN_SERVER_PER_LANE)
+    return bad("unknown dyn_mapping %d", c->dyn_mapping);
   return LBSIM_OK;
 #undef bad
 }
@@ -221,24 +225,54 @@ void launch_dyn(lbsim_t* h, const void* action, int dtype, int32_t* assign, cons
                        h->st, h->prm, action, dtype, assign, mask);
 }
 
+// server per lane: G = MAXS lanes per env, 64 / G envs per wave
+template <int MAXS, int MODE, int POLICY>
+void launch_dyn_group(lbsim_t* h, const void* action, int dtype, int32_t* assign,
+                      const uint8_t* mask, hipStream_t stream) {
+  constexpr int epw = 64 / MAXS;
+  const dim3 block(64), grid((unsigned)((h->B + epw - 1) / epw));
+  if (h->prm.trace)
+    hipLaunchKernelGGL((dynamics_group_kernel<MAXS, MODE, POLICY, true>), grid, block, 0, stream,
+                       h->st, h->prm, action, dtype, assign, mask);
+  else
+    hipLaunchKernelGGL((dynamics_group_kernel<MAXS, MODE, POLICY, false>), grid, block, 0, stream,
+                       h->st, h->prm, action, dtype, assign, mask);
+}
+
+template <int MAXS, int MODE, int POLICY>
+void launch_dyn_map(lbsim_t* h, bool group, const void* action, int dtype, int32_t* assign,
+                    const uint8_t* mask, hipStream_t stream) {
+  if (group) launch_dyn_group<MAXS, MODE, POLICY>(h, action, dtype, assign, mask, stream);
+  else launch_dyn<MAXS, MODE, POLICY>(h, action, dtype, assign, mask, stream);
+}
+
 template <int MAXS, int MODE>
-void launch_dyn_policy(lbsim_t* h, const void* action, int dtype, int32_t* assign,
+void launch_dyn_policy(lbsim_t* h, bool g, const void* action, int dtype, int32_t* assign,
                        const uint8_t* mask, hipStream_t stream) {
   switch (h->prm.policy) {
-    case LBSIM_POLICY_SED: launch_dyn<MAXS, MODE, 0>(h, action, dtype, assign, mask, stream); break;
-    case LBSIM_POLICY_SED2: launch_dyn<MAXS, MODE, 1>(h, action, dtype, assign, mask, stream); break;
-    case LBSIM_POLICY_LSQ: launch_dyn<MAXS, MODE, 2>(h, action, dtype, assign, mask, stream); break;
-    case LBSIM_POLICY_LSQ2: launch_dyn<MAXS, MODE, 3>(h, action, dtype, assign, mask, stream); break;
-    default: launch_dyn<MAXS, MODE, 4>(h, action, dtype, assign, mask, stream); break;
+    case LBSIM_POLICY_SED: launch_dyn_map<MAXS, MODE, 0>(h, g, action, dtype, assign, mask, stream); break;
+    case LBSIM_POLICY_SED2: launch_dyn_map<MAXS, MODE, 1>(h, g, action, dtype, assign, mask, stream); break;
+    case LBSIM_POLICY_LSQ: launch_dyn_map<MAXS, MODE, 2>(h, g, action, dtype, assign, mask, stream); break;
+    case LBSIM_POLICY_LSQ2: launch_dyn_map<MAXS, MODE, 3>(h, g, action, dtype, assign, mask, stream); break;
+    default: launch_dyn_map<MAXS, MODE, 4>(h, g, action, dtype, assign, mask, stream); break;
   }
+}
+
+// Mapping choice (LBSIM_DYN_AUTO): one lane per env while that gives at least half as many waves
+// as the device has SIMDs; below, one lane per server.
+bool server_per_lane(const lbsim_t* h) {
+  if (h->cfg.dyn_mapping == LBSIM_DYN_ENV_PER_LANE) return false;
+  if (h->cfg.dyn_mapping == LBSIM_DYN_SERVER_PER_LANE) return true;
+  return (int64_t)(h->B + 63) / 64 < (int64_t)h->simds / 2;
 }
 
 template <int MODE>
 void launch_dynamics_t(lbsim_t* h, const void* action, int dtype, int32_t* assign,
                        const uint8_t* mask, hipStream_t stream) {
-  if (h->S <= 4) launch_dyn_policy<4, MODE>(h, action, dtype, assign, mask, stream);
-  else if (h->S <= 8) launch_dyn_policy<8, MODE>(h, action, dtype, assign, mask, stream);
-  else launch_dyn_policy<16, MODE>(h, action, dtype, assign, mask, stream);
+  const bool g = server_per_lane(h);
+  if (h->S <= 4) launch_dyn_policy<4, MODE>(h, g, action, dtype, assign, mask, stream);
+  else if (h->S <= 8) launch_dyn_policy<8, MODE>(h, g, action, dtype, assign, mask, stream);
+  else launch_dyn_policy<16, MODE>(h, g, action, dtype, assign, mask, stream);
 }
 
 int launch_dynamics(lbsim_t* h, const void* action, int dtype, int32_t* assign,
@@ -324,6 +358,11 @@ int lbsim_create(const lbsim_config_t* cfg, int device, lbsim_t** out) {
   lbsim_t* h = new lbsim_t();
   h->cfg = *cfg;
   h->device = device;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      cus < 1)
+    cus = 256;
+  h->simds = 4 * cus;
   h->B = cfg->num_envs;
   h->S = cfg->num_servers;
   h->Q = cfg->queue_capacity;

@@ -1,0 +1,390 @@
+// lbsim_dyn_group.h — dynamics with one LANE per SERVER, for batches too small to fill the chip
+// with one lane per env.
+//
+// dynamics_kernel (lbsim_kernels.h) gives each env one lane, so a batch of B envs is B/64 waves:
+// 4096 envs (BASELINE configs[1]) are 64 waves on 1024 SIMDs, 8192 × 16-server envs (configs[4]
+// per GPU) 128.  Here an env is a group of G = pow2 >= S lanes, lane s owning server s; the wave
+// holds 64/G envs and the grid is B·G/64 waves.  Same event sequence, same arithmetic, same state
+// layout as dynamics_kernel, so the two mappings are interchangeable between
+// launches and bit-identical to the oracle.
+//
+// Per event, the group agrees on the event with DPP reductions inside a 16-lane row (no LDS):
+//   earliest completion: min over head_tc (quad_perm / row_half_mirror / row_mirror), lowest
+//     server among ties from a ballot;
+//   SED / LSQ choice: the reference's scan "start at the hashed server h, replace on a strictly
+//     lower score" equals: h (or the first eligible server when h is full) if its score is the
+//     minimum or NaN, else the lowest eligible server holding the minimum — one min reduction and
+//     two ballots;
+//   SED2 / LSQ2: the two candidates' scores broadcast by OR-reducing a one-hot word.
+// Each lane runs the event's Philox block with its own counter: for a completion only the owning
+// lane's reservoir draw is used, for an arrival every lane draws the same block.  Per-server fields
+// are plain registers (one server per lane); the queue window lives in LDS [slot][lane].
+#pragma once
+
+#include "lbsim_kernels.h"
+
+namespace lbk {
+
+constexpr int kGroupWL = 8;  // LDS queue window per server: 64 lanes x 8 x 8 B = 4 KiB per wave
+
+// Reductions over the aligned G-lane group (G <= 16: one DPP row).  Lanes read only within their
+// group, so groups that left the event loop (inactive lanes) are never read.
+template <int G>
+__device__ __forceinline__ int32_t group_min_i32(int32_t v) {
+  int32_t o = (int32_t)dpp_u32<0xB1>((uint32_t)v);  // quad_perm [1,0,3,2]
+  v = o < v ? o : v;
+  if constexpr (G >= 4) { o = (int32_t)dpp_u32<0x4E>((uint32_t)v); v = o < v ? o : v; }
+  if constexpr (G >= 8) { o = (int32_t)dpp_u32<0x141>((uint32_t)v); v = o < v ? o : v; }
+  if constexpr (G >= 16) { o = (int32_t)dpp_u32<0x140>((uint32_t)v); v = o < v ? o : v; }
+  return v;
+}
+// NaN-free inputs (the caller maps NaN to +inf)
+template <int G>
+__device__ __forceinline__ float group_min_f32(float v) {
+  float o = __uint_as_float(dpp_u32<0xB1>(__float_as_uint(v)));
+  v = o < v ? o : v;
+  if constexpr (G >= 4) { o = __uint_as_float(dpp_u32<0x4E>(__float_as_uint(v))); v = o < v ? o : v; }
+  if constexpr (G >= 8) { o = __uint_as_float(dpp_u32<0x141>(__float_as_uint(v))); v = o < v ? o : v; }
+  if constexpr (G >= 16) { o = __uint_as_float(dpp_u32<0x140>(__float_as_uint(v))); v = o < v ? o : v; }
+  return v;
+}
+template <int G>
+__device__ __forceinline__ uint32_t group_or(uint32_t v) {
+  v |= dpp_u32<0xB1>(v);
+  if constexpr (G >= 4) v |= dpp_u32<0x4E>(v);
+  if constexpr (G >= 8) v |= dpp_u32<0x141>(v);
+  if constexpr (G >= 16) v |= dpp_u32<0x140>(v);
+  return v;
+}
+// This lane's group's bits of a wave ballot.
+template <int G>
+__device__ __forceinline__ uint32_t group_bits(uint64_t m, int gbase) {
+  return (uint32_t)(m >> gbase) & (uint32_t)((1u << G) - 1u);
+}
+
+// The server this lane owns (fields of DESIGN.md §4, in registers).
+struct SrvLane {
+  int32_t cnt, head_tc, head, lh, tail, last, assigned;
+  uint32_t rcnt;
+  float score, scale;
+  double den;
+  bool act;  // s < S
+};
+
+// ALIAS table of the group in LDS: word f of active position k at [f][gbase + k].  Every lane of
+// the group builds the same table (same values to the same words).
+struct GroupAliasTab {
+  int32_t* t;
+  int gbase;
+  __device__ int32_t& operator()(int f, int k) const { return t[f * 64 + gbase + k]; }
+};
+
+template <int G, int POLICY, bool TRACE>
+__device__ __forceinline__ void sim_step_group(const DevState& st, const SimParams& p,
+                                               LaneState<1>& E, SrvLane& V, uint32_t b, int s,
+                                               int gbase, float w_own, const float (&wall)[G],
+                                               int2* win, int32_t* atab) {
+  constexpr int WL = kGroupWL;
+  const int S = p.S, Q = p.Q;
+  const int32_t dt = p.dt_us;
+  const uint64_t base_us = (uint64_t)E.clock * (uint64_t)dt;
+  const uint32_t base_ms = (uint32_t)(base_us / 1000u);
+  const uint32_t base_rem = (uint32_t)(base_us - (uint64_t)base_ms * 1000u);
+  constexpr bool two_choice = (POLICY == 1 || POLICY == 3);
+  constexpr bool alias = POLICY == kPolicyAlias;
+  const uint32_t sb = b * (uint32_t)S + (uint32_t)s;  // valid when V.act
+  const GroupAliasTab tab{atab, gbase};
+  int n_alias = 0;
+  if constexpr (alias) {
+    n_alias = build_alias<G>(wall, S, tab);
+  } else if (V.act) {
+    V.den = (double)w_own + 1e-9;
+    V.score = policy_score(POLICY, V.cnt, V.den);
+  }
+  auto wslot = [&](int i) -> int2* { return win + i * 64 + (gbase + s); };
+  for (;;) {
+    // ---- which event: earliest completion of the group (ties: lowest server) vs next arrival
+    const int32_t key = (V.act && V.cnt > 0) ? V.head_tc : 0x7FFFFFFF;
+    const int32_t tmin = group_min_i32<G>(key);
+    const uint32_t tb = group_bits<G>(__ballot(key == tmin && tmin != 0x7FFFFFFF), gbase);
+    const int smin = tb ? __builtin_ctz(tb) : -1;
+    const bool arrival_due = E.next_arr < dt;
+    const int32_t horizon = arrival_due ? E.next_arr : dt;
+    const bool comp = smin >= 0 && tmin <= horizon;
+    const bool arr = !comp && arrival_due;
+    if (!comp && !arr) break;
+
+    // ---- arrival: choose a server (node.c:388-441); full servers are not eligible
+    const int32_t ta = E.next_arr;
+    const bool elig = V.act && V.cnt < Q;
+    const uint32_t em = group_bits<G>(__ballot(elig), gbase);
+    int chosen = -1;
+    if constexpr (alias) {
+      if (n_alias > 0) {
+        const int a = alias_pick(tab, n_alias, E.u2);
+        chosen = ((em >> a) & 1u) ? a : -1;
+      }
+    } else if constexpr (two_choice) {
+      const int h1 = (int)(((uint64_t)E.u2 * (uint64_t)S) >> 32);
+      const int h2 = (int)(((uint64_t)E.u3 * (uint64_t)S) >> 32);
+      const uint32_t bits = __float_as_uint(V.score);
+      const float s1 = __uint_as_float(group_or<G>(s == h1 ? bits : 0u));
+      const float s2 = __uint_as_float(group_or<G>(s == h2 ? bits : 0u));
+      const bool ok1 = (em >> h1) & 1u, ok2 = (em >> h2) & 1u;
+      chosen = (ok1 && ok2) ? ((s2 < s1) ? h2 : h1) : (ok1 ? h1 : (ok2 ? h2 : -1));
+    } else {
+      const int h = (int)(((uint64_t)E.u2 * (uint64_t)S) >> 32);
+      const int c0 = ((em >> h) & 1u) ? h : (em ? __builtin_ctz(em) : -1);
+      const bool num = elig && V.score == V.score;
+      const float m = group_min_f32<G>(num ? V.score : __uint_as_float(0x7f800000u));
+      const uint32_t tie = group_bits<G>(__ballot(num && V.score == m), gbase);
+      const uint32_t nan = group_bits<G>(__ballot(V.score != V.score), gbase);
+      chosen = c0 < 0 ? -1 : ((((tie | nan) >> c0) & 1u) ? c0 : (tie ? __builtin_ctz(tie) : -1));
+    }
+    const bool push = arr && chosen >= 0;
+    E.dropped += (arr && chosen < 0) ? 1u : 0u;
+    const int cs = comp ? smin : (push ? chosen : -1);
+    const bool mine = s == cs;
+
+    // ---- the event's Philox block: this lane's reservoir draw, or the next arrival's draw
+    const u32x4 ctr = comp
+        ? u32x4{V.rcnt >> 1, E.gid, E.episode, (kStreamReservoir << 24) | (uint32_t)s}
+        : u32x4{E.arr_idx + 1u, E.gid, E.episode, kStreamArrival << 24};
+    const u32x4 d = philox4x32_10(ctr, p.key0, p.key1);
+
+    // ---- completion (lbhash.h:116-124, 131-135) + Algorithm R (reservoir.py:64-85)
+    const int32_t tc = tmin;
+    const int32_t h_ta = wslot(V.lh)->y;
+    const int32_t start_c = h_ta > V.last ? h_ta : V.last;
+    const int h_next = (V.head + 1 == Q) ? 0 : V.head + 1;
+    const int lh_next = (V.lh + 1 == WL) ? 0 : V.lh + 1;
+    int slot;
+    {
+      const uint32_t cres = V.rcnt;
+      const uint32_t hi = (cres & 1u) ? d.w : d.y;
+      const uint32_t lo = (cres & 1u) ? d.z : d.x;
+      const uint64_t j = mulhi64_by_u33(hi, lo, (uint64_t)cres + 1u);
+      slot = cres < (uint32_t)K ? (int)cres : (j < (uint64_t)K ? (int)j : -1);
+    }
+    if (comp && mine && slot >= 0) {
+      st.res[sb * (uint32_t)K + (uint32_t)slot] =
+          make_uint3((uint32_t)(tc - h_ta), (uint32_t)(tc - start_c),
+                     base_ms + (base_rem + (uint32_t)tc) / 1000u);
+    }
+    if (comp && mine && V.cnt - 1 >= WL) {  // rare: refill window entry WL-1 from the ring
+      int pw = h_next + WL - 1;
+      pw = pw >= Q ? pw - Q : pw;
+      *wslot(V.lh) = st.ring[sb * (uint32_t)Q + (uint32_t)pw];
+      __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+    }
+    const int32_t nxt_tc = wslot(lh_next)->x;
+
+    // ---- arrival: FIFO service starts when the server's last queued flow ends
+    const int32_t start_a = V.cnt > 0 ? (V.tail > ta ? V.tail : ta) : ta;
+    int32_t svc = (int32_t)(E.next_work * V.scale);
+    svc = svc < 1 ? 1 : svc;
+    const int32_t tc_a = start_a + svc;
+    if (push && mine) {
+      const int2 e = make_int2(tc_a, ta);
+      if (V.cnt < WL) {
+        int li = V.lh + V.cnt;
+        li = li >= WL ? li - WL : li;
+        *wslot(li) = e;
+      } else {
+        int pos = V.head + V.cnt;
+        pos = pos >= Q ? pos - Q : pos;
+        st.ring[sb * (uint32_t)Q + (uint32_t)pos] = e;
+      }
+    }
+
+    // ---- write back the changed server (the owning lane)
+    if (mine) {
+      const int32_t n_cs = comp ? V.cnt - 1 : V.cnt + 1;
+      if (comp) {
+        V.rcnt = V.rcnt != 0xFFFFFFFFu ? V.rcnt + 1u : V.rcnt;
+        V.last = tc;
+        V.head = h_next;
+        V.lh = lh_next;
+        V.head_tc = nxt_tc;
+      } else {
+        V.tail = tc_a;
+        V.assigned += 1;
+        V.head_tc = V.cnt == 0 ? tc_a : V.head_tc;
+      }
+      V.cnt = n_cs;
+      V.score = policy_score(POLICY, n_cs, V.den);
+    }
+
+    // ---- next arrival (identical in every lane of the group)
+    int32_t na;
+    float nw;
+    uint32_t nu2, nu3;
+    if constexpr (TRACE) {
+      na = ta + E.pf_gap;
+      nw = E.pf_work;
+      nu2 = d.z;
+      nu3 = d.w;
+      if (arr) {
+        E.row = (E.row + 1u == p.trace_rows) ? 0u : E.row + 1u;
+        E.pf_gap = (int32_t)st.trace_gap[E.row];
+        E.pf_work = st.trace_work[E.row];
+      }
+    } else {
+      arrival_from_draw(p, d, ta, na, nw, nu2, nu3);
+    }
+    E.next_arr = arr ? na : E.next_arr;
+    E.next_work = arr ? nw : E.next_work;
+    E.u2 = arr ? nu2 : E.u2;
+    E.u3 = arr ? nu3 : E.u3;
+    E.arr_idx += arr ? 1u : 0u;
+  }
+
+  // ---- rebase to the next step's start (this lane's server)
+  E.next_arr -= dt;
+  if (V.act) {
+    for (int i = 0; i < WL && i < V.cnt; ++i) {
+      int li = V.lh + i;
+      li = li >= WL ? li - WL : li;
+      int2* e = wslot(li);
+      e->x -= dt;
+      e->y -= dt;
+    }
+    int pos = V.head + WL;
+    if (pos >= Q) pos -= Q;
+    for (int i = WL; i < V.cnt; ++i) {
+      int2 e = st.ring[sb * (uint32_t)Q + (uint32_t)pos];
+      e.x -= dt;
+      e.y -= dt;
+      st.ring[sb * (uint32_t)Q + (uint32_t)pos] = e;
+      pos = (pos + 1 == Q) ? 0 : pos + 1;
+    }
+    V.head_tc -= dt;
+    V.tail -= dt;
+    V.last = (V.last < kLastNone + dt) ? kLastNone : V.last - dt;
+  }
+  E.clock += 1u;
+}
+
+template <int G, int MODE, int POLICY, bool TRACE>
+__global__ void __launch_bounds__(64)
+    dynamics_group_kernel(DevState st, SimParams p, const void* action, int action_dtype,
+                          int32_t* assign_out, const uint8_t* reset_mask) {
+  static_assert(G == 2 || G == 4 || G == 8 || G == 16, "group = one DPP row or a part of it");
+  constexpr int WL = kGroupWL;
+  constexpr bool alias = POLICY == kPolicyAlias;
+  __shared__ int2 win[WL * 64];
+  __shared__ int32_t atab[alias ? 2 * 64 : 1];
+  const int lane = (int)threadIdx.x;
+  const int s = lane & (G - 1);
+  const int gbase = lane & ~(G - 1);
+  const uint32_t b = blockIdx.x * (uint32_t)(64 / G) + (uint32_t)(lane / G);
+  if (b >= (uint32_t)p.B) return;  // whole groups leave together
+  const int S = p.S, Q = p.Q;
+  if (MODE == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
+
+  LaneState<1> E;
+  E.gid = p.env_id_offset + b;
+  SrvLane V;
+  V.act = s < S;
+  V.scale = p.svc_scale[0];
+#pragma unroll
+  for (int k = 1; k < G; ++k) V.scale = (k == s) ? p.svc_scale[k] : V.scale;
+  V.den = 1.0;
+  V.score = 0.f;
+  V.assigned = 0;
+  V.lh = 0;
+  const uint32_t sb = b * (uint32_t)S + (uint32_t)s;
+  float wall[G];
+  float w_own = 1.0f;
+
+  if (MODE == kModeReset) {
+    E.episode = st.episode[b] + 1u;
+    E.clock = 0u;
+    E.dropped = 0u;
+    E.arr_idx = 0u;
+    draw_arrival<1>(st, p, E, 0);
+    trace_prefetch<1>(st, p, E);
+    V.cnt = 0;
+    V.head_tc = 0;
+    V.head = 0;
+    V.tail = 0;
+    V.last = kLastNone;
+    V.rcnt = 0u;
+#pragma unroll
+    for (int k = 0; k < G; ++k) wall[k] = 1.0f;
+    for (int k = 0; k < p.warmup_steps; ++k)
+      sim_step_group<G, POLICY, TRACE>(st, p, E, V, b, s, gbase, 1.0f, wall, win, atab);
+    if (s == 0) {
+      st.ep_step[b] = 0;
+      st.ep_return[b] = 0.0;
+    }
+  } else {
+    E.episode = st.episode[b];
+    E.clock = st.clock[b];
+    E.dropped = st.dropped[b];
+    E.arr_idx = st.arr_idx[b];
+    E.next_arr = st.next_arr[b];
+    E.next_work = st.next_work[b];
+    E.u2 = st.next_u2[b];
+    E.u3 = st.next_u3[b];
+    trace_prefetch<1>(st, p, E);
+    V.cnt = 0;
+    V.head_tc = 0;
+    V.head = 0;
+    V.tail = 0;
+    V.last = kLastNone;
+    V.rcnt = 0u;
+    if (V.act) {
+      const uint32_t hc = st.hc[sb];
+      V.head = (int)(hc & 0xFFFFu);
+      V.cnt = (int32_t)(hc >> 16);
+      V.last = st.last_tc[sb];
+      V.rcnt = st.res_count[sb];
+      for (int i = 0; i < WL && i < V.cnt; ++i) {
+        int pos = V.head + i;
+        if (pos >= Q) pos -= Q;
+        win[i * 64 + lane] = st.ring[sb * (uint32_t)Q + (uint32_t)pos];
+      }
+      if (V.cnt > 0) {
+        int tp = V.head + V.cnt - 1;
+        if (tp >= Q) tp -= Q;
+        V.tail = st.ring[sb * (uint32_t)Q + (uint32_t)tp].x;
+        V.head_tc = st.ring[sb * (uint32_t)Q + (uint32_t)V.head].x;
+      }
+      w_own = action_weight(p, action, action_dtype, (size_t)sb);
+    }
+    if constexpr (alias) {
+#pragma unroll
+      for (int k = 0; k < G; ++k)
+        wall[k] = k < S ? action_weight(p, action, action_dtype, (size_t)b * S + (size_t)k) : 1.0f;
+    }
+    sim_step_group<G, POLICY, TRACE>(st, p, E, V, b, s, gbase, w_own, wall, win, atab);
+  }
+
+  // ---- this lane's server back to HBM (window into the ring), then the env words (lane 0)
+  if (V.act) {
+    for (int i = 0; i < WL && i < V.cnt; ++i) {
+      int pos = V.head + i;
+      if (pos >= Q) pos -= Q;
+      int li = V.lh + i;
+      li = li >= WL ? li - WL : li;
+      st.ring[sb * (uint32_t)Q + (uint32_t)pos] = win[li * 64 + lane];
+    }
+    st.hc[sb] = (uint32_t)V.head | ((uint32_t)V.cnt << 16);
+    st.last_tc[sb] = V.last;
+    st.res_count[sb] = V.rcnt;
+    if (MODE != kModeReset && assign_out != nullptr) assign_out[sb] = V.assigned;
+  }
+  if (s == 0) {
+    st.episode[b] = E.episode;
+    st.clock[b] = E.clock;
+    st.dropped[b] = E.dropped;
+    st.arr_idx[b] = E.arr_idx;
+    st.next_arr[b] = E.next_arr;
+    st.next_work[b] = E.next_work;
+    st.next_u2[b] = E.u2;
+    st.next_u3[b] = E.u3;
+  }
+}
+
+}  // namespace lbk

@@ -185,22 +185,23 @@ __device__ __forceinline__ T sel(const T (&a)[MAXS], int i) {
 // avg = sum / (n + 1e-6), p = w / (avg + 1e-6), small / big generators in index order, a big
 // reduced below 1 becomes the next small).  Stored per active position k in the lane's den
 // fields: F_DEN_LO = odd (f32 bits, the alias_t float), F_DEN_HI = alias | server << 8.
+// `tab(f, k)` is the table word f (0: odd, 1: alias | server << 8) of active position k.
 // Returns the active count.
-template <int MAXS>
-__device__ int build_alias(const float (&w)[MAXS], int S, const Lds& l) {
+template <int MAXS, typename Tab>
+__device__ int build_alias(const float (&w)[MAXS], int S, Tab tab) {
   int n = 0;
   double sum = 0.0;
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) {
     if (s < S && w[s] > 0.0f) {
-      fld<MAXS>(l, F_DEN_LO, n) = (int32_t)0x3f800000;  // (1, 0)
-      fld<MAXS>(l, F_DEN_HI, n) = s << 8;
+      tab(0, n) = (int32_t)0x3f800000;  // (1, 0)
+      tab(1, n) = s << 8;
       sum += (double)w[s];
       ++n;
     }
   }
   const double avg = sum / ((double)n + 1e-6);
-  auto wk = [&](int k) { return (double)sel<MAXS>(w, fld<MAXS>(l, F_DEN_HI, k) >> 8); };
+  auto wk = [&](int k) { return (double)sel<MAXS>(w, tab(1, k) >> 8); };
   int si = 0, bi = 0, sk = -1, bk = -1;
   double sp = 0.0, bp = 0.0;
   auto next_small = [&]() {
@@ -214,8 +215,8 @@ __device__ int build_alias(const float (&w)[MAXS], int S, const Lds& l) {
   next_small();
   next_big();
   while (bk >= 0 && sk >= 0) {
-    fld<MAXS>(l, F_DEN_LO, sk) = (int32_t)__float_as_uint((float)sp);
-    fld<MAXS>(l, F_DEN_HI, sk) = (fld<MAXS>(l, F_DEN_HI, sk) & ~0xFF) | bk;
+    tab(0, sk) = (int32_t)__float_as_uint((float)sp);
+    tab(1, sk) = (tab(1, sk) & ~0xFF) | bk;
     bp = bp - (1.0 - sp);
     if (bp < 1.0) { sk = bk; sp = bp; next_big(); } else { next_small(); }
   }
@@ -224,15 +225,22 @@ __device__ int build_alias(const float (&w)[MAXS], int S, const Lds& l) {
 
 // ALIAS pick for an arrival with hash word u: rand_num = U * n (U = 24 bits of u, in [0, 1)),
 // bucket = (int)rand_num, the alias if rand_num - bucket > odd[bucket] (node.c:449-460).
-template <int MAXS>
-__device__ __forceinline__ int alias_pick(const Lds& l, int n, uint32_t u) {
+template <typename Tab>
+__device__ __forceinline__ int alias_pick(Tab tab, int n, uint32_t u) {
   const float rn = (float)(u >> 8) * 5.9604644775390625e-8f * (float)n;
   int bucket = (int)rn;
   bucket = bucket > n - 1 ? n - 1 : bucket;
-  const float odd = __uint_as_float((uint32_t)fld<MAXS>(l, F_DEN_LO, bucket));
-  const int k = (rn - (float)bucket) > odd ? (fld<MAXS>(l, F_DEN_HI, bucket) & 0xFF) : bucket;
-  return fld<MAXS>(l, F_DEN_HI, k) >> 8;
+  const float odd = __uint_as_float((uint32_t)tab(0, bucket));
+  const int k = (rn - (float)bucket) > odd ? (tab(1, bucket) & 0xFF) : bucket;
+  return tab(1, k) >> 8;
 }
+
+// The per-lane kernel keeps the table in the lane's den fields.
+template <int MAXS>
+struct FieldAliasTab {
+  const Lds& l;
+  __device__ int32_t& operator()(int f, int k) const { return fld<MAXS>(l, F_DEN_LO + f, k); }
+};
 
 // Arrival draw for one arrival index: gap to it, its work, its two hash words.
 __device__ __forceinline__ void arrival_from_draw(const SimParams& p, const u32x4& d,
@@ -354,7 +362,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
   const uint32_t b0 = b * (uint32_t)S;
   int n_alias = 0;
   if constexpr (alias) {
-    n_alias = build_alias<MAXS>(w, S, l);
+    n_alias = build_alias<MAXS>(w, S, FieldAliasTab<MAXS>{l});
   } else {
 #pragma unroll
     for (int s = 0; s < MAXS; ++s) {
@@ -387,7 +395,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     int chosen = -1;
     if constexpr (alias) {  // full server: the flow is dropped (ALIAS has no eligibility test)
       if (n_alias > 0) {
-        const int a = alias_pick<MAXS>(l, n_alias, L.u2);
+        const int a = alias_pick(FieldAliasTab<MAXS>{l}, n_alias, L.u2);
         chosen = sel<MAXS>(L.cnt, a) < Q ? a : -1;
       }
     } else if constexpr (two_choice) {  // SED2 / LSQ2: two candidates, keep the second if strictly better
@@ -1290,7 +1298,7 @@ __global__ void __launch_bounds__(64)
   float w[MAX_S];
 #pragma unroll
   for (int s = 0; s < MAX_S; ++s) w[s] = s < S ? weights[r * S + s] : 0.0f;
-  const int na = build_alias<MAX_S>(w, S, l);
+  const int na = build_alias<MAX_S>(w, S, FieldAliasTab<MAX_S>{l});
   for (int k = 0; k < S; ++k) {
     const bool v = k < na;
     odd_out[r * S + k] = v ? __uint_as_float((uint32_t)fld<MAX_S>(l, F_DEN_LO, k)) : 1.0f;

@@ -101,12 +101,15 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
                 env_id_offset: int = 0, arrival_rate: float = 400.0,
                 server_rates: Optional[List[float]] = None, load: float = 0.8,
                 queue_capacity: int = 32, warmup_steps: int = 8, decay_factor: float = 0.9,
-                assign_policy: str = "sed", trace=None) -> _lib.LbsimConfig:
+                assign_policy: str = "sed", trace=None,
+                dyn_mapping: str = "auto") -> _lib.LbsimConfig:
     """Build and validate an lbsim_config_t from reference-style kwargs.
 
     server_rates defaults to identical servers at utilisation `load`: mu = rate / (load * S).
     trace (marllb_amd.trace.Trace): replay its arrivals (LBSIM_ARRIVAL_TRACE); its empirical rate
     replaces arrival_rate.  The arrays themselves go to the handle (Handle.set_trace).
+    dyn_mapping: "auto" | "env" (one lane per env) | "server" (one lane per server): how the
+    dynamics kernel lays envs onto lanes; results are identical, only speed differs.
     """
     if reward_metric not in _lib.METRICS:  # rewards.py:321-323
         raise ValueError(f"Unsupported metric: {reward_metric}. Supported: {_lib.METRICS}")
@@ -149,6 +152,9 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
     cfg.decay_factor = float(decay_factor)
     cfg.queue_capacity = int(queue_capacity)
     cfg.warmup_steps = int(warmup_steps)
+    if dyn_mapping not in _lib.DYN_MAPPINGS:
+        raise ValueError(f"Unknown dyn_mapping: {dyn_mapping}. Supported: {_lib.DYN_MAPPINGS}")
+    cfg.dyn_mapping = _lib.DYN_MAPPINGS.index(dyn_mapping)
     _lib.validate(cfg)
     return cfg
 

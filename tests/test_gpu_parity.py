@@ -167,13 +167,15 @@ def _compare_state(h_gpu, ora, B, S, Q, norm):
     np.testing.assert_array_equal(statelayout.live_ring(g, B, S, Q), statelayout.live_ring(o, B, S, Q))
 
 
+@pytest.mark.parametrize("mapping", ["env", "server"])
 @pytest.mark.parametrize("case", range(len(CONFIGS)))
-def test_simulator_bit_exact_vs_oracle(lib, oracle_mod, case):
+def test_simulator_bit_exact_vs_oracle(lib, oracle_mod, case, mapping):
+    """Both dynamics mappings (one lane per env / one lane per server) against the oracle."""
     from marllb_amd.env import VecLoadBalanceEnv, make_config
     c = CONFIGS[case]
     B, S, kw = c["B"], c["S"], resolve_kw(c["kw"])
     kw.setdefault("seed", 1000 + case)
-    env = VecLoadBalanceEnv(B, S, device="cuda:0", autoreset=False, **kw)
+    env = VecLoadBalanceEnv(B, S, device="cuda:0", autoreset=False, dyn_mapping=mapping, **kw)
     ora = oracle_mod.OracleEnv(make_config(B, S, **kw), threads=4, trace=kw.get("trace"))
     Q, norm = env.cfg.queue_capacity, bool(env.cfg.normalize_obs)
     obs_g = env.reset().cpu().numpy()
