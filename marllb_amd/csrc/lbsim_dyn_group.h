@@ -67,7 +67,7 @@ struct SrvLane {
   int32_t cnt, head_tc, head, lh, tail, last, assigned;
   uint32_t rcnt;
   float score, scale;
-  double den;
+  double den, rcp;
   bool act;  // s < S
 };
 
@@ -99,6 +99,7 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
     n_alias = build_alias<G>(wall, S, tab);
   } else if (V.act) {
     V.den = (double)w_own + 1e-9;
+    V.rcp = 1.0 / V.den;
     V.score = policy_score(POLICY, V.cnt, V.den);
   }
   auto wslot = [&](int i) -> int2* { return win + i * 64 + (gbase + s); };
@@ -212,7 +213,7 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
         V.head_tc = V.cnt == 0 ? tc_a : V.head_tc;
       }
       V.cnt = n_cs;
-      V.score = policy_score(POLICY, n_cs, V.den);
+      V.score = policy_score_r(POLICY, n_cs, V.den, V.rcp);
     }
 
     // ---- next arrival (identical in every lane of the group)
@@ -290,6 +291,7 @@ __global__ void __launch_bounds__(64)
 #pragma unroll
   for (int k = 1; k < G; ++k) V.scale = (k == s) ? p.svc_scale[k] : V.scale;
   V.den = 1.0;
+  V.rcp = 1.0;
   V.score = 0.f;
   V.assigned = 0;
   V.lh = 0;

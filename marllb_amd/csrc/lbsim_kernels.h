@@ -119,7 +119,9 @@ struct Win {
 // Per-server fields touched only by the server an event changes live in LDS, lane-major
 // ([field][server][lane], conflict-free): one ds_read/ds_write per field per event instead of an
 // S-way register select chain.  cnt / head_tc / score stay in registers (scanned every event).
-enum SrvField { F_HEAD = 0, F_LH, F_TAIL, F_LAST, F_RCNT, F_ASSIGNED, F_DEN_LO, F_DEN_HI, F_NUM };
+enum SrvField {
+  F_HEAD = 0, F_LH, F_TAIL, F_LAST, F_RCNT, F_ASSIGNED, F_DEN_LO, F_DEN_HI, F_RCP_LO, F_RCP_HI, F_NUM
+};
 
 template <int MAXS>
 struct LaneState {
@@ -169,6 +171,24 @@ __device__ __forceinline__ float policy_score(int policy, int32_t cnt, double de
   if (policy == 2 /*LSQ*/ || policy == 3 /*LSQ2*/) return (float)cnt;
   if (policy == kPolicyAlias) return 0.0f;
   return (float)((double)(cnt + 1) / den);
+}
+
+// The same score inside the event loop, with rcp = 1 / den computed once per step: (cnt + 1) / den
+// correctly rounded as q0 = c·rcp, q = q0 + fma(−q0, den, c)·rcp (Markstein's corrected quotient:
+// bit-identical to the division for every finite non-zero den — checked over every 7th float
+// weight in [2^-10, 2^10) × c = 1..65 and 2e8 random weights, tools/markstein_check.c).  den = 0,
+// ±inf or NaN make q NaN and take the division.  3 f64 ops instead of the ~12 of a division.
+__device__ __forceinline__ float policy_score_r(int policy, int32_t cnt, double den, double rcp) {
+  if (policy == 2 /*LSQ*/ || policy == 3 /*LSQ2*/) return (float)cnt;
+  if (policy == kPolicyAlias) return 0.0f;
+  const double c = (double)(cnt + 1);
+  const double q0 = c * rcp;
+  double q = fma(fma(-q0, den, c), rcp, q0);
+  if (q != q) {  // rare: a real branch (the asm keeps the division from being speculated)
+    asm volatile("");
+    q = c / den;
+  }
+  return (float)q;
 }
 
 template <int MAXS, typename T>
@@ -368,8 +388,11 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     for (int s = 0; s < MAXS; ++s) {
       if (s < S) {
         const double den = (double)w[s] + 1e-9;
+        const double rcp = 1.0 / den;
         fld<MAXS>(l, F_DEN_LO, s) = (int32_t)__double2loint(den);
         fld<MAXS>(l, F_DEN_HI, s) = (int32_t)__double2hiint(den);
+        fld<MAXS>(l, F_RCP_LO, s) = (int32_t)__double2loint(rcp);
+        fld<MAXS>(l, F_RCP_HI, s) = (int32_t)__double2hiint(rcp);
         L.score[s] = policy_score(POLICY, L.cnt[s], den);
       }
     }
@@ -442,6 +465,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     const int32_t c_last = fld<MAXS>(l, F_LAST, csi);
     const uint32_t cres = (uint32_t)fld<MAXS>(l, F_RCNT, csi);
     const double c_den = den_of<MAXS>(l, csi);
+    const double c_rcp = __hiloint2double(fld<MAXS>(l, F_RCP_HI, csi), fld<MAXS>(l, F_RCP_LO, csi));
 
     // ---- the one Philox block of this event (Algorithm R draw, or the next arrival's draw)
     const u32x4 ctr = comp
@@ -499,7 +523,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
 
     // ---- write back the changed server
     const int32_t n_cs = comp ? c_cnt - 1 : c_cnt + 1;
-    const float sc_new = policy_score(POLICY, n_cs, c_den);
+    const float sc_new = policy_score_r(POLICY, n_cs, c_den, c_rcp);
     if (comp) {
       fld<MAXS>(l, F_RCNT, csi) = (int32_t)(cres != 0xFFFFFFFFu ? cres + 1u : cres);
       fld<MAXS>(l, F_LAST, csi) = tc;
