@@ -195,6 +195,7 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
         int pos = V.head + V.cnt;
         pos = pos >= Q ? pos - Q : pos;
         st.ring[sb * (uint32_t)Q + (uint32_t)pos] = e;
+        asm volatile("");  // no flat store (see dynamics_kernel)
       }
     }
 

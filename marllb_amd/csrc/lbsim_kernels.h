@@ -120,7 +120,9 @@ struct Win {
 // ([field][server][lane], conflict-free): one ds_read/ds_write per field per event instead of an
 // S-way register select chain.  cnt / head_tc / score stay in registers (scanned every event).
 enum SrvField {
-  F_HEAD = 0, F_LH, F_TAIL, F_LAST, F_RCNT, F_ASSIGNED, F_DEN_LO, F_DEN_HI, F_RCP_LO, F_RCP_HI, F_NUM
+  F_HEAD = 0, F_LH, F_TAIL, F_LAST, F_RCNT, F_ASSIGNED, F_DEN_LO, F_DEN_HI, F_RCP_LO, F_RCP_HI,
+  F_SCALE,  // service-time scale (us per unit work) of the server, f32 bits
+  F_NUM
 };
 
 template <int MAXS>
@@ -381,6 +383,9 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
   constexpr bool alias = POLICY == kPolicyAlias;
   const uint32_t b0 = b * (uint32_t)S;
   int n_alias = 0;
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s)
+    if (s < S) fld<MAXS>(l, F_SCALE, s) = (int32_t)__float_as_uint(p.svc_scale[s]);
   if constexpr (alias) {
     n_alias = build_alias<MAXS>(w, S, FieldAliasTab<MAXS>{l});
   } else {
@@ -466,6 +471,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     const uint32_t cres = (uint32_t)fld<MAXS>(l, F_RCNT, csi);
     const double c_den = den_of<MAXS>(l, csi);
     const double c_rcp = __hiloint2double(fld<MAXS>(l, F_RCP_HI, csi), fld<MAXS>(l, F_RCP_LO, csi));
+    const float c_scale = __uint_as_float((uint32_t)fld<MAXS>(l, F_SCALE, csi));
 
     // ---- the one Philox block of this event (Algorithm R draw, or the next arrival's draw)
     const u32x4 ctr = comp
@@ -501,9 +507,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     const int32_t nxt_tc = qslot<MAXS>(l, csi, lh_next)->x;  // next head (valid if cnt > 1)
 
     // ---- arrival: FIFO service starts when the server's last queued flow ends
-    float a_scale = 0.f;
-#pragma unroll
-    for (int s = 0; s < MAXS; ++s) a_scale = (s == chosen) ? p.svc_scale[s] : a_scale;
+    const float a_scale = c_scale;  // csi is the chosen server whenever the flow is pushed
     const int32_t start_a = c_cnt > 0 ? (c_tail > ta ? c_tail : ta) : ta;
     int32_t svc = (int32_t)(L.next_work * a_scale);
     svc = svc < 1 ? 1 : svc;
@@ -518,6 +522,9 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
         int pos = c_head + c_cnt;
         pos = pos >= Q ? pos - Q : pos;
         st.ring[(b0 + (uint32_t)csi) * (uint32_t)Q + (uint32_t)pos] = e;
+        // keeps the compiler from sinking the two stores' common half into one flat (generic
+        // pointer) store, which counts in lgkmcnt too: every LDS wait would then wait on it
+        asm volatile("");
       }
     }
 
@@ -532,7 +539,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     }
     if (push) {
       fld<MAXS>(l, F_TAIL, csi) = tc_a;
-      fld<MAXS>(l, F_ASSIGNED, csi) += 1;
+      atomicAdd(&fld<MAXS>(l, F_ASSIGNED, csi), 1);  // ds_add_u32: no read-back, no wait
     }
     const int32_t new_head_tc = comp ? nxt_tc : tc_a;
 #pragma unroll
