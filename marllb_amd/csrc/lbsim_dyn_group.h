@@ -28,32 +28,53 @@ namespace lbk {
 constexpr int kGroupWL = 8;  // LDS queue window per server: 64 lanes x 8 x 8 B = 4 KiB per wave
 
 // Reductions over the aligned G-lane group (G <= 16: one DPP row).  Lanes read only within their
-// group, so groups that left the event loop (inactive lanes) are never read.
+// group, so groups that left the event loop (inactive lanes) are never read.  mov_dpp with
+// bound_ctrl and full masks lets the DPP combiner fold each step into one v_min/v_or with a DPP
+// source; the event selection runs its two reductions interleaved (no wait states between a
+// step's write and the next step's DPP read).
+template <int CTRL>
+__device__ __forceinline__ uint32_t gdpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+// NaN-free f32 <-> int32 with the same order (-0 just below +0; the callers compare the result
+// back as a float, so +-0 stay equal there)
+__device__ __forceinline__ int32_t f32_key(float x) {
+  const int32_t b = (int32_t)__float_as_uint(x);
+  return b ^ ((b >> 31) & 0x7FFFFFFF);
+}
+__device__ __forceinline__ float key_f32(int32_t k) {
+  return __uint_as_float((uint32_t)(k ^ ((k >> 31) & 0x7FFFFFFF)));
+}
+template <int CTRL>
+__device__ __forceinline__ void gmin_step(int32_t& a, int32_t& b) {
+  const int32_t oa = (int32_t)gdpp<CTRL>((uint32_t)a);
+  const int32_t ob = (int32_t)gdpp<CTRL>((uint32_t)b);
+  a = oa < a ? oa : a;
+  b = ob < b ? ob : b;
+}
+// min over the group of two ints, interleaved
+template <int G>
+__device__ __forceinline__ void group_min2(int32_t& a, int32_t& b) {
+  gmin_step<0xB1>(a, b);                          // quad_perm [1,0,3,2]
+  if constexpr (G >= 4) gmin_step<0x4E>(a, b);    // quad_perm [2,3,0,1]
+  if constexpr (G >= 8) gmin_step<0x141>(a, b);   // row_half_mirror
+  if constexpr (G >= 16) gmin_step<0x140>(a, b);  // row_mirror
+}
 template <int G>
 __device__ __forceinline__ int32_t group_min_i32(int32_t v) {
-  int32_t o = (int32_t)dpp_u32<0xB1>((uint32_t)v);  // quad_perm [1,0,3,2]
+  int32_t o = (int32_t)gdpp<0xB1>((uint32_t)v);
   v = o < v ? o : v;
-  if constexpr (G >= 4) { o = (int32_t)dpp_u32<0x4E>((uint32_t)v); v = o < v ? o : v; }
-  if constexpr (G >= 8) { o = (int32_t)dpp_u32<0x141>((uint32_t)v); v = o < v ? o : v; }
-  if constexpr (G >= 16) { o = (int32_t)dpp_u32<0x140>((uint32_t)v); v = o < v ? o : v; }
-  return v;
-}
-// NaN-free inputs (the caller maps NaN to +inf)
-template <int G>
-__device__ __forceinline__ float group_min_f32(float v) {
-  float o = __uint_as_float(dpp_u32<0xB1>(__float_as_uint(v)));
-  v = o < v ? o : v;
-  if constexpr (G >= 4) { o = __uint_as_float(dpp_u32<0x4E>(__float_as_uint(v))); v = o < v ? o : v; }
-  if constexpr (G >= 8) { o = __uint_as_float(dpp_u32<0x141>(__float_as_uint(v))); v = o < v ? o : v; }
-  if constexpr (G >= 16) { o = __uint_as_float(dpp_u32<0x140>(__float_as_uint(v))); v = o < v ? o : v; }
+  if constexpr (G >= 4) { o = (int32_t)gdpp<0x4E>((uint32_t)v); v = o < v ? o : v; }
+  if constexpr (G >= 8) { o = (int32_t)gdpp<0x141>((uint32_t)v); v = o < v ? o : v; }
+  if constexpr (G >= 16) { o = (int32_t)gdpp<0x140>((uint32_t)v); v = o < v ? o : v; }
   return v;
 }
 template <int G>
 __device__ __forceinline__ uint32_t group_or(uint32_t v) {
-  v |= dpp_u32<0xB1>(v);
-  if constexpr (G >= 4) v |= dpp_u32<0x4E>(v);
-  if constexpr (G >= 8) v |= dpp_u32<0x141>(v);
-  if constexpr (G >= 16) v |= dpp_u32<0x140>(v);
+  v |= gdpp<0xB1>(v);
+  if constexpr (G >= 4) v |= gdpp<0x4E>(v);
+  if constexpr (G >= 8) v |= gdpp<0x141>(v);
+  if constexpr (G >= 16) v |= gdpp<0x140>(v);
   return v;
 }
 // This lane's group's bits of a wave ballot.
@@ -106,7 +127,13 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
   for (;;) {
     // ---- which event: earliest completion of the group (ties: lowest server) vs next arrival
     const int32_t key = (V.act && V.cnt > 0) ? V.head_tc : 0x7FFFFFFF;
-    const int32_t tmin = group_min_i32<G>(key);
+    const bool elig = V.act && V.cnt < Q;
+    const bool num = elig && V.score == V.score;
+    int32_t tmin = key;
+    int32_t mk = num ? f32_key(V.score) : 0x7f800000;  // SED / LSQ: min eligible score (+inf)
+    if constexpr (!alias && !two_choice) group_min2<G>(tmin, mk);
+    else tmin = group_min_i32<G>(key);
+    const float m = key_f32(mk);
     const uint32_t tb = group_bits<G>(__ballot(key == tmin && tmin != 0x7FFFFFFF), gbase);
     const int smin = tb ? __builtin_ctz(tb) : -1;
     const bool arrival_due = E.next_arr < dt;
@@ -117,7 +144,6 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
 
     // ---- arrival: choose a server (node.c:388-441); full servers are not eligible
     const int32_t ta = E.next_arr;
-    const bool elig = V.act && V.cnt < Q;
     const uint32_t em = group_bits<G>(__ballot(elig), gbase);
     int chosen = -1;
     if constexpr (alias) {
@@ -136,8 +162,6 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
     } else {
       const int h = (int)(((uint64_t)E.u2 * (uint64_t)S) >> 32);
       const int c0 = ((em >> h) & 1u) ? h : (em ? __builtin_ctz(em) : -1);
-      const bool num = elig && V.score == V.score;
-      const float m = group_min_f32<G>(num ? V.score : __uint_as_float(0x7f800000u));
       const uint32_t tie = group_bits<G>(__ballot(num && V.score == m), gbase);
       const uint32_t nan = group_bits<G>(__ballot(V.score != V.score), gbase);
       chosen = c0 < 0 ? -1 : ((((tie | nan) >> c0) & 1u) ? c0 : (tie ? __builtin_ctz(tie) : -1));

@@ -382,6 +382,9 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
   constexpr bool two_choice = (POLICY == 1 || POLICY == 3);
   constexpr bool alias = POLICY == kPolicyAlias;
   const uint32_t b0 = b * (uint32_t)S;
+  // this env's reservoirs and rings as per-lane (VGPR) pointers: no kernarg reload in the loop
+  uint3* const my_res = st.res + (size_t)b0 * K;
+  int2* const my_ring = st.ring + (size_t)b0 * (size_t)Q;
   int n_alias = 0;
 #pragma unroll
   for (int s = 0; s < MAXS; ++s)
@@ -493,15 +496,15 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
       slot = cres < (uint32_t)K ? (int)cres : (j < (uint64_t)K ? (int)j : -1);
     }
     if (comp && slot >= 0) {
-      const uint32_t r = (b0 + (uint32_t)smin) * (uint32_t)K + (uint32_t)slot;
-      st.res[r] = make_uint3((uint32_t)(tc - h_ta), (uint32_t)(tc - start_c),
-                             base_ms + (base_rem + (uint32_t)tc) / 1000u);
+      my_res[(uint32_t)smin * (uint32_t)K + (uint32_t)slot] =
+          make_uint3((uint32_t)(tc - h_ta), (uint32_t)(tc - start_c),
+                     base_ms + (base_rem + (uint32_t)tc) / 1000u);
     }
     // rare: the queue is longer than the window; bring entry WL-1 (after this pop) into LDS
     if (comp && c_cnt - 1 >= WL) {
       int pw = h_next + WL - 1;
       pw = pw >= Q ? pw - Q : pw;
-      *qslot<MAXS>(l, csi, c_lh) = st.ring[(b0 + (uint32_t)csi) * (uint32_t)Q + (uint32_t)pw];
+      *qslot<MAXS>(l, csi, c_lh) = my_ring[(uint32_t)csi * (uint32_t)Q + (uint32_t)pw];
       __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);  // drain in the rare branch, not at the back-edge
     }
     const int32_t nxt_tc = qslot<MAXS>(l, csi, lh_next)->x;  // next head (valid if cnt > 1)
@@ -521,7 +524,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
       } else {
         int pos = c_head + c_cnt;
         pos = pos >= Q ? pos - Q : pos;
-        st.ring[(b0 + (uint32_t)csi) * (uint32_t)Q + (uint32_t)pos] = e;
+        my_ring[(uint32_t)csi * (uint32_t)Q + (uint32_t)pos] = e;
         // keeps the compiler from sinking the two stores' common half into one flat (generic
         // pointer) store, which counts in lgkmcnt too: every LDS wait would then wait on it
         asm volatile("");
