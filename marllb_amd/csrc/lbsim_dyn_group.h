@@ -152,15 +152,15 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
         chosen = ((em >> a) & 1u) ? a : -1;
       }
     } else if constexpr (two_choice) {
-      const int h1 = (int)(((uint64_t)E.u2 * (uint64_t)S) >> 32);
-      const int h2 = (int)(((uint64_t)E.u3 * (uint64_t)S) >> 32);
+      const int h1 = (int)__umulhi(E.u2, (uint32_t)S);
+      const int h2 = (int)__umulhi(E.u3, (uint32_t)S);
       const uint32_t bits = __float_as_uint(V.score);
       const float s1 = __uint_as_float(group_or<G>(s == h1 ? bits : 0u));
       const float s2 = __uint_as_float(group_or<G>(s == h2 ? bits : 0u));
       const bool ok1 = (em >> h1) & 1u, ok2 = (em >> h2) & 1u;
       chosen = (ok1 && ok2) ? ((s2 < s1) ? h2 : h1) : (ok1 ? h1 : (ok2 ? h2 : -1));
     } else {
-      const int h = (int)(((uint64_t)E.u2 * (uint64_t)S) >> 32);
+      const int h = (int)__umulhi(E.u2, (uint32_t)S);
       const int c0 = ((em >> h) & 1u) ? h : (em ? __builtin_ctz(em) : -1);
       const uint32_t tie = group_bits<G>(__ballot(num && V.score == m), gbase);
       const uint32_t nan = group_bits<G>(__ballot(V.score != V.score), gbase);

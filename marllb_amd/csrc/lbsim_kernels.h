@@ -386,6 +386,8 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
   uint3* const my_res = st.res + (size_t)b0 * K;
   int2* const my_ring = st.ring + (size_t)b0 * (size_t)Q;
   int n_alias = 0;
+  // SED scores (cnt + 1) / den stay finite (cnt + 1 <= 65) for every finite |den| >= 1e-30
+  bool finite_scores = true;
 #pragma unroll
   for (int s = 0; s < MAXS; ++s)
     if (s < S) fld<MAXS>(l, F_SCALE, s) = (int32_t)__float_as_uint(p.svc_scale[s]);
@@ -397,6 +399,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
       if (s < S) {
         const double den = (double)w[s] + 1e-9;
         const double rcp = 1.0 / den;
+        finite_scores &= fabs(den) >= 1e-30 && fabs(den) <= 1e300;  // false for NaN
         fld<MAXS>(l, F_DEN_LO, s) = (int32_t)__double2loint(den);
         fld<MAXS>(l, F_DEN_HI, s) = (int32_t)__double2hiint(den);
         fld<MAXS>(l, F_RCP_LO, s) = (int32_t)__double2loint(rcp);
@@ -410,8 +413,8 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     int32_t tmin = 0x7FFFFFFF;
     int smin = -1;
 #pragma unroll
-    for (int s = 0; s < MAXS; ++s) {
-      const bool c = s < S && L.cnt[s] > 0 && L.head_tc[s] < tmin;
+    for (int s = 0; s < MAXS; ++s) {  // bitwise &: no short-circuit control flow
+      const bool c = (s < S) & (L.cnt[s] > 0) & (L.head_tc[s] < tmin);
       tmin = c ? L.head_tc[s] : tmin;
       smin = c ? s : smin;
     }
@@ -430,8 +433,8 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
         chosen = sel<MAXS>(L.cnt, a) < Q ? a : -1;
       }
     } else if constexpr (two_choice) {  // SED2 / LSQ2: two candidates, keep the second if strictly better
-      const int h1 = (int)(((uint64_t)L.u2 * (uint64_t)S) >> 32);
-      const int h2 = (int)(((uint64_t)L.u3 * (uint64_t)S) >> 32);
+      const int h1 = (int)__umulhi(L.u2, (uint32_t)S);  // (u * S) >> 32
+      const int h2 = (int)__umulhi(L.u3, (uint32_t)S);
       float s1 = 0.f, s2 = 0.f;
       bool ok1 = false, ok2 = false;
 #pragma unroll
@@ -443,19 +446,28 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
       }
       chosen = (ok1 && ok2) ? ((s2 < s1) ? h2 : h1) : (ok1 ? h1 : (ok2 ? h2 : -1));
     } else {  // SED / LSQ: start at the hashed server, replace on strictly lower score
-      const int h = (int)(((uint64_t)L.u2 * (uint64_t)S) >> 32);
-      float best = 0.f;
+      const int h = (int)__umulhi(L.u2, (uint32_t)S);  // (u * S) >> 32
+      float best = __uint_as_float(0x7f800000u);  // +inf: any finite score replaces it
 #pragma unroll
       for (int s = 0; s < MAXS; ++s) {
-        const bool m = s == h && L.cnt[s] < Q;
+        const bool m = (s == h) & (L.cnt[s] < Q);
         chosen = m ? s : chosen;
         best = m ? L.score[s] : best;
       }
+      if (finite_scores) {  // every score finite: "replace on strictly lower" from +inf is exact
 #pragma unroll
-      for (int s = 0; s < MAXS; ++s) {
-        const bool m = s < S && L.cnt[s] < Q && (chosen < 0 || L.score[s] < best);
-        chosen = m ? s : chosen;
-        best = m ? L.score[s] : best;
+        for (int s = 0; s < MAXS; ++s) {
+          const bool m = (s < S) & (L.cnt[s] < Q) & (L.score[s] < best);
+          chosen = m ? s : chosen;
+          best = m ? L.score[s] : best;
+        }
+      } else {  // NaN / inf scores: the first eligible server is taken whatever its score
+#pragma unroll
+        for (int s = 0; s < MAXS; ++s) {
+          const bool m = (s < S) & (L.cnt[s] < Q) & ((chosen < 0) | (L.score[s] < best));
+          chosen = m ? s : chosen;
+          best = m ? L.score[s] : best;
+        }
       }
     }
     const bool push = arr && chosen >= 0;

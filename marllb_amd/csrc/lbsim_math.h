@@ -1,7 +1,7 @@
 // lbsim_math.h — bit-reproducible scalar math for the gfx950 kernels.
 //
-// Every function here is written with plain IEEE-754 binary32/binary64 +,-,*,/ and integer ops
-// only, and the whole library is compiled with -ffp-contract=off, so a kernel lane produces the
+// Every function here is written with plain IEEE-754 binary32/binary64 +,-,*,/, explicit fma and
+// integer ops only, and the whole library is compiled with -ffp-contract=off, so a kernel lane produces the
 // same bits as oracle/lbsim_oracle.c (gcc, -ffp-contract=off) for the same inputs.  That is what
 // makes the server-assignment indices and every integer state word bit-exact against the oracle
 // (DESIGN.md §3.1).  No hardware transcendental (v_exp_f32/v_log_f32) is used on the state path.
@@ -46,41 +46,49 @@ __device__ __forceinline__ float u01_open0(uint32_t r) {
 __device__ __forceinline__ float as_f32(uint32_t u) { return __uint_as_float(u); }
 __device__ __forceinline__ uint32_t as_u32(float f) { return __float_as_uint(f); }
 
-// Natural log for x in [2^-24, 1]: m*2^e with m folded into [sqrt(1/2), sqrt(2)], then
-// ln m = 2 atanh(t), t = (m-1)/(m+1), odd series to t^9 (|t| <= 0.1716).
+// Natural log for x in [2^-24, 1], no division: x = m 2^e with m folded into [sqrt(1/2), sqrt(2)],
+// ln m = log1p(f), f = m - 1, by the Cephes single-precision logf polynomial (Moshier; max relative
+// error over every k 2^-24, k = 1..2^24: 8.2e-8) in fmaf Horner form -- an explicit fma is
+// correctly rounded on the GPU (v_fma_f32) and in C (fmaf), so both sides get the same bits.
 __device__ __forceinline__ float lb_logf(float x) {
   const uint32_t b = as_u32(x);
   int e = (int)(b >> 23) - 127;
   float m = as_f32((b & 0x007fffffu) | 0x3f800000u);
-  if (m > 1.41421354f) {
-    m = m * 0.5f;
-    e = e + 1;
-  }
-  const float t = (m - 1.0f) / (m + 1.0f);
-  const float t2 = t * t;
-  float p = 0.222222224f;
-  p = p * t2 + 0.285714298f;
-  p = p * t2 + 0.400000006f;
-  p = p * t2 + 0.666666687f;
-  p = p * t2 + 2.0f;
-  return t * p + (float)e * 0.693147182f;
+  if (m > 1.41421354f) { m = m * 0.5f; e = e + 1; }
+  const float f = m - 1.0f;  /* exact */
+  const float z = f * f;
+  float p = 7.0376836292e-2f;
+  p = fmaf(p, f, -1.1514610310e-1f);
+  p = fmaf(p, f, 1.1676998740e-1f);
+  p = fmaf(p, f, -1.2420140846e-1f);
+  p = fmaf(p, f, 1.4249322787e-1f);
+  p = fmaf(p, f, -1.6668057665e-1f);
+  p = fmaf(p, f, 2.0000714765e-1f);
+  p = fmaf(p, f, -2.4999993993e-1f);
+  p = fmaf(p, f, 3.3333331174e-1f);
+  float y = (p * f) * z;
+  y = fmaf(-0.5f, z, y);
+  const float fe = (float)e;  /* ln 2 = 0.693359375 - 2.12194440e-4 (Cephes split) */
+  float r = fmaf(fe, -2.12194440e-4f, y);
+  r = r + f;
+  return fmaf(fe, 0.693359375f, r);
 }
 
 // 2^x for x <= 0 (x < -60 -> 0): x = n + f, n = floor(x + 1/2), f in [-1/2, 1/2), degree-7
-// Taylor of e^(f ln2) (truncation error < 6e-9), times 2^n.
+// Taylor of e^(f ln2) (truncation error < 6e-9) in fmaf Horner form, times 2^n.
 __device__ __forceinline__ float lb_exp2f(float x) {
   if (x < -60.0f) return 0.0f;
   const float fl = floorf(x + 0.5f);  /* exact for |x| <= 60 */
   const int n = (int)fl;
   const float f = x - fl;             /* exact, in [-0.5, 0.5) */
   float p = 1.52527336e-5f;
-  p = p * f + 1.54035297e-4f;
-  p = p * f + 1.33335581e-3f;
-  p = p * f + 9.61812911e-3f;
-  p = p * f + 5.55041086e-2f;
-  p = p * f + 0.240226507f;
-  p = p * f + 0.693147182f;
-  p = p * f + 1.0f;
+  p = fmaf(p, f, 1.54035297e-4f);
+  p = fmaf(p, f, 1.33335581e-3f);
+  p = fmaf(p, f, 9.61812911e-3f);
+  p = fmaf(p, f, 5.55041086e-2f);
+  p = fmaf(p, f, 0.240226507f);
+  p = fmaf(p, f, 0.693147182f);
+  p = fmaf(p, f, 1.0f);
   return p * as_f32((uint32_t)(n + 127) << 23);
 }
 

@@ -65,20 +65,30 @@ static uint32_t f_bits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
 
 static float u01(uint32_t r) { return (float)((r >> 8) + 1u) * 5.9604644775390625e-8f; }
 
-/* ln x for x in [2^-24, 1] — DESIGN.md §3.2 (same operation sequence as the GPU). */
+/* ln x for x in [2^-24, 1] — DESIGN.md §3.2 (same operation sequence as the GPU: Cephes logf
+ * polynomial for log1p(m - 1), fmaf Horner, no division). */
 float oracle_logf(float x) {
   const uint32_t b = f_bits(x);
   int e = (int)(b >> 23) - 127;
   float m = bits_f((b & 0x007fffffu) | 0x3f800000u);
   if (m > 1.41421354f) { m = m * 0.5f; e = e + 1; }
-  const float t = (m - 1.0f) / (m + 1.0f);
-  const float t2 = t * t;
-  float p = 0.222222224f;
-  p = p * t2 + 0.285714298f;
-  p = p * t2 + 0.400000006f;
-  p = p * t2 + 0.666666687f;
-  p = p * t2 + 2.0f;
-  return t * p + (float)e * 0.693147182f;
+  const float f = m - 1.0f;  /* exact */
+  const float z = f * f;
+  float p = 7.0376836292e-2f;
+  p = fmaf(p, f, -1.1514610310e-1f);
+  p = fmaf(p, f, 1.1676998740e-1f);
+  p = fmaf(p, f, -1.2420140846e-1f);
+  p = fmaf(p, f, 1.4249322787e-1f);
+  p = fmaf(p, f, -1.6668057665e-1f);
+  p = fmaf(p, f, 2.0000714765e-1f);
+  p = fmaf(p, f, -2.4999993993e-1f);
+  p = fmaf(p, f, 3.3333331174e-1f);
+  float y = (p * f) * z;
+  y = fmaf(-0.5f, z, y);
+  const float fe = (float)e;  /* ln 2 = 0.693359375 - 2.12194440e-4 (Cephes split) */
+  float r = fmaf(fe, -2.12194440e-4f, y);
+  r = r + f;
+  return fmaf(fe, 0.693359375f, r);
 }
 
 /* 2^x for x <= 0 — DESIGN.md §3.4. */
@@ -88,13 +98,13 @@ float oracle_exp2f(float x) {
   const int n = (int)fl;
   const float f = x - fl;             /* exact, in [-0.5, 0.5) */
   float p = 1.52527336e-5f;
-  p = p * f + 1.54035297e-4f;
-  p = p * f + 1.33335581e-3f;
-  p = p * f + 9.61812911e-3f;
-  p = p * f + 5.55041086e-2f;
-  p = p * f + 0.240226507f;
-  p = p * f + 0.693147182f;
-  p = p * f + 1.0f;
+  p = fmaf(p, f, 1.54035297e-4f);
+  p = fmaf(p, f, 1.33335581e-3f);
+  p = fmaf(p, f, 9.61812911e-3f);
+  p = fmaf(p, f, 5.55041086e-2f);
+  p = fmaf(p, f, 0.240226507f);
+  p = fmaf(p, f, 0.693147182f);
+  p = fmaf(p, f, 1.0f);
   return p * bits_f((uint32_t)(n + 127) << 23);
 }
 

@@ -136,13 +136,16 @@ CONFIGS = [
     # synthetic trace that every env wraps around many times per episode
     dict(B=64, S=8, kw={"trace": "builtin"}),
     dict(B=50, S=4, kw={"trace": "short", "assign_policy": "sed2", "step_interval": 0.5}),
+    # NaN continuous actions pass np.clip (env.py:349-351): NaN SED scores take the exact scan
+    dict(B=60, S=5, kw={"action_type": "continuous", "_nan_actions": 0.15}),
 ]
 
 
 def resolve_kw(kw):
-    """CONFIGS entries name traces; build them here (module import stays cheap)."""
+    """CONFIGS entries name traces; build them here (module import stays cheap).  Keys starting
+    with '_' are test options, not config kwargs."""
     from marllb_amd import trace
-    kw = dict(kw)
+    kw = {k: v for k, v in kw.items() if not k.startswith("_")}
     if kw.get("trace") == "builtin":
         kw["trace"] = trace.builtin()
     elif kw.get("trace") == "short":
@@ -152,7 +155,9 @@ def resolve_kw(kw):
 
 def _actions(rng, B, S, cfgkw):
     if cfgkw.get("action_type") == "continuous":
-        return rng.uniform(-1.0, 11.0, (B, S)).astype(np.float32)
+        a = rng.uniform(-1.0, 11.0, (B, S)).astype(np.float32)
+        a[rng.random((B, S)) < cfgkw.get("_nan_actions", 0.0)] = np.nan
+        return a
     n = len(cfgkw.get("discrete_weights", [1, 1.5, 2]))
     return rng.integers(-n, n, (B, S)).astype(np.int64)
 
@@ -175,6 +180,7 @@ def test_simulator_bit_exact_vs_oracle(lib, oracle_mod, case, mapping):
     c = CONFIGS[case]
     B, S, kw = c["B"], c["S"], resolve_kw(c["kw"])
     kw.setdefault("seed", 1000 + case)
+    akw = dict(c["kw"])  # action options (incl. test-only '_' keys)
     env = VecLoadBalanceEnv(B, S, device="cuda:0", autoreset=False, dyn_mapping=mapping, **kw)
     ora = oracle_mod.OracleEnv(make_config(B, S, **kw), threads=4, trace=kw.get("trace"))
     Q, norm = env.cfg.queue_capacity, bool(env.cfg.normalize_obs)
@@ -183,7 +189,7 @@ def test_simulator_bit_exact_vs_oracle(lib, oracle_mod, case, mapping):
     np.testing.assert_array_equal(obs_g, obs_o)
     rng = np.random.default_rng(case)
     for k in range(12):
-        a = _actions(rng, B, S, kw)
+        a = _actions(rng, B, S, akw)
         og, rg, dg, info = env.step(torch.from_numpy(a), assign_counts=True)
         oo, ro, do, ao = ora.step(a)
         np.testing.assert_array_equal(info["assign_counts"].cpu().numpy(), ao, err_msg=f"assign step {k}")
@@ -197,7 +203,7 @@ def test_simulator_bit_exact_vs_oracle(lib, oracle_mod, case, mapping):
     oo = ora.reset(mask=mask, obs=og.copy())
     np.testing.assert_array_equal(og, oo)
     for k in range(4):
-        a = _actions(rng, B, S, kw)
+        a = _actions(rng, B, S, akw)
         og, rg, dg, _ = env.step(torch.from_numpy(a))
         oo, ro, do, _ = ora.step(a)
         np.testing.assert_array_equal(og.cpu().numpy(), oo)

@@ -30,7 +30,7 @@ def run_case(oracle_mod, case, steps=12):
     rng = np.random.default_rng(case)
     max_q = 0
     for _ in range(steps):
-        ora.step(_actions(rng, B, S, kw))
+        ora.step(_actions(rng, B, S, c["kw"]))  # the GPU test's action stream
         st = statelayout.parse(ora.state_bytes(), B, S, cfg.queue_capacity, bool(cfg.normalize_obs))
         max_q = max(max_q, int((st["hc"] >> 16).max()))
     return st, max_q, S
@@ -46,3 +46,4 @@ def test_parity_cases_cover_rare_paths(oracle_mod):
     assert two_pass, "no parity case produces a sample >= 2^25 - 1 us"
     assert overflow, "no parity case queues more flows than the LDS window"
     assert dropped, "no parity case drops arrivals"
+    assert any(c["kw"].get("_nan_actions") for c in CONFIGS), "no case with NaN SED scores"
