@@ -810,6 +810,43 @@ __device__ __forceinline__ T pairwise8(int n, int j, F term) {
   return t;
 }
 
+// Two pairwise sums over the same index walk (each in numpy's order on its own): `term(i, b)`
+// returns element i of the first and stores element i of the second in b.
+template <typename T, typename F>
+__device__ __forceinline__ T pairwise8x2(int n, int j, T& second, F term) {
+  if (n < 8) {
+    T r = (T)0, q = (T)0;
+    for (int i = 0; i < n; ++i) {
+      T bi;
+      r += term(i, bi);
+      q += bi;
+    }
+    second = q;
+    return r;
+  }
+  const int m8 = n - (n % 8);
+  T bacc;
+  T acc = term(j, bacc);
+  for (int i = 8 + j; i < m8; i += 8) {
+    T bi;
+    acc += term(i, bi);
+    bacc += bi;
+  }
+  const int lane = j;
+  T t = acc + xor_lane(acc, lane, 1), u = bacc + xor_lane(bacc, lane, 1);
+  t = t + xor_lane(t, lane, 2);
+  u = u + xor_lane(u, lane, 2);
+  t = t + xor_lane(t, lane, 4);
+  u = u + xor_lane(u, lane, 4);
+  for (int i = m8; i < n; ++i) {
+    T bi;
+    t += term(i, bi);
+    u += bi;
+  }
+  second = u;
+  return t;
+}
+
 // ================================================================ features of one env
 
 // LDS image of one env's reservoirs during observe (one wave per env, 64-thread blocks).
@@ -972,21 +1009,19 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
     const float sum = pairwise8<float>(n, j, [&](int i) { return sample_value<US>(a[i]); });
     if (j == 0 && r < R) sc.mean[r] = n > 0 ? sum / (float)n : 0.0f;
   }
-  for (int job0 = 0; job0 < 3 * S; job0 += 8) {  // float64 sum w (S jobs), sum v*w (R jobs)
-    const int q = job0 + g;
-    const bool wonly = q < S;
-    const int r = wonly ? 0 : q - S;
-    const int ws = wonly ? q : (r >> 1);
-    const int n = q < 3 * S ? sc.n[wonly ? 2 * q : r] : 0;
+  for (int job0 = 0; job0 < R; job0 += 8) {  // float64 sum v*w and sum w, one job per reservoir
+    const int r = job0 + g;
+    const int n = r < R ? sc.n[r] : 0;
     const uint32_t* a = sc.vals[r < R ? r : 0];
-    const float* w = sc.wts[ws < S ? ws : 0];
-    const double sum = pairwise8<double>(n, j, [&](int i) {
-      const double x = wonly ? 1.0 : (double)sample_value<US>(a[i]);
-      return x * (double)w[i];
+    const float* w = sc.wts[r < R ? r >> 1 : 0];
+    double sw;
+    const double svw = pairwise8x2<double>(n, j, sw, [&](int i, double& wi) {
+      wi = (double)w[i];
+      return (double)sample_value<US>(a[i]) * wi;
     });
-    if (j == 0 && q < 3 * S) {
-      if (wonly) sc.swt[q] = sum;
-      else sc.svw[r] = sum;
+    if (j == 0 && r < R) {
+      sc.svw[r] = svw;
+      if ((r & 1) == 0) sc.swt[r >> 1] = sw;  // the two reservoirs of a server share w
     }
   }
   __syncthreads();
@@ -1174,14 +1209,25 @@ __device__ __forceinline__ double pw_sum64(int n, F term) {
 // servers (any column > 0, env.py:410-413) at column `field`, metric in float64.  The active
 // servers' indices are packed into a 64-bit nibble list so no runtime-indexed local array (and
 // hence no scratch memory) is needed.
-__device__ double reward_of(const float* obs, int S, int metric, int field) {
+// Active servers of an (S, 11) row as a bit mask, one thread.
+__device__ __forceinline__ uint32_t active_mask_seq(const float* obs, int S) {
+  uint32_t m = 0;
+  for (int s = 0; s < S; ++s) {
+    bool active = false;
+    for (int f = 0; f < NF; ++f) active |= obs[s * NF + f] > 0.0f;
+    m |= active ? 1u << s : 0u;
+  }
+  return m;
+}
+
+// `act` = the active-server mask.  Inlined, so an LDS row is read with ds_read (no flat loads).
+__device__ __forceinline__ double reward_masked(const float* obs, uint32_t act, int S, int metric,
+                                                int field) {
   if (field < 0 || field >= NF) return 0.0;
   uint64_t ids = 0;
   int n = 0;
   for (int s = 0; s < S; ++s) {
-    bool active = false;
-    for (int f = 0; f < NF; ++f) active |= obs[s * NF + f] > 0.0f;
-    if (active) { ids |= (uint64_t)s << (4 * n); ++n; }
+    if ((act >> s) & 1u) { ids |= (uint64_t)s << (4 * n); ++n; }
   }
   if (n == 0) return 0.0;
   auto x = [&](int i) { return (double)obs[(int)((ids >> (4 * i)) & 15u) * NF + field]; };
@@ -1235,6 +1281,10 @@ __device__ double reward_of(const float* obs, int S, int metric, int field) {
   }
 }
 
+__device__ double reward_of(const float* obs, int S, int metric, int field) {
+  return reward_masked(obs, active_mask_seq(obs, S), S, metric, field);
+}
+
 // ================================================================ observe (one wave = one env)
 
 struct ObsOutputs {
@@ -1263,8 +1313,13 @@ __global__ void __launch_bounds__(64, kObsWaves<MAXS>)
   const int S = p.S;
   observe_env<MAXS, true>(st, p, b, sc, s_obs, lane);
 
+  // active servers (any column > 0): lane s scans its row, one ballot
+  bool act = false;
+  if (lane < S)
+    for (int f = 0; f < NF; ++f) act |= s_obs[lane * NF + f] > 0.0f;
+  const uint32_t act_mask = (uint32_t)__ballot(act);
   if (mode == kModeStep && lane == 0) {
-    const double r = reward_of(s_obs, S, p.reward_metric, p.reward_field);
+    const double r = reward_masked(s_obs, act_mask, S, p.reward_metric, p.reward_field);
     out.reward[b] = (float)r;
     const int32_t es = st.ep_step[b] + 1;
     const double er = st.ep_return[b] + r;
