@@ -13,7 +13,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "lbsim_api.hip")
-DEPS = [os.path.join(HERE, "csrc", f) for f in ("lbsim_api.hip", "lbsim_kernels.h", "lbsim_math.h")]
+DEPS = [os.path.join(HERE, "csrc", f) for f in sorted(os.listdir(os.path.join(HERE, "csrc")))]
 DEPS.append(os.path.join(ROOT, "include", "lbsim.h"))
 OUT = os.path.join(HERE, "liblbsim.so")
 ARCH = os.environ.get("LBSIM_OFFLOAD_ARCH", "gfx950")
