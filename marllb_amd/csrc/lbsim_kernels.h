@@ -113,15 +113,21 @@ __device__ __forceinline__ uint32_t trace_row(const SimParams& p, uint32_t gid, 
 // born and complete inside one step and never touch HBM.
 template <int MAXS>
 struct Win {
-  static constexpr int WL = MAXS <= 4 ? 8 : (MAXS <= 8 ? 4 : 2);  // LDS <= 24 / 32 / 48 KiB
+  static constexpr int WL = MAXS <= 4 ? 8 : (MAXS <= 8 ? 4 : 2);  // LDS <= 16 / 16 / 16 KiB
 };
 
-// Per-server fields touched only by the server an event changes live in LDS, lane-major
-// ([field][server][lane], conflict-free): one ds_read/ds_write per field per event instead of an
-// S-way register select chain.  cnt / head_tc / score stay in registers (scanned every event).
+// Per-server fields read or written only for the server an arrival picks live in LDS, lane-major
+// ([field][server][lane], conflict-free): one ds_read/ds_write per field instead of an S-way
+// register select chain.  Fields every server needs at every arrival (cnt, head_tc, the window /
+// ring head positions, the SED denominators) stay in registers.
 enum SrvField {
-  F_HEAD = 0, F_LH, F_TAIL, F_LAST, F_RCNT, F_ASSIGNED, F_DEN_LO, F_DEN_HI, F_RCP_LO, F_RCP_HI,
-  F_SCALE,  // service-time scale (us per unit work) of the server, f32 bits
+  F_TAIL = 0,  // t_complete of the last queued flow (valid if cnt > 0)
+  F_LAST,      // t_complete of the last completed flow (kLastNone if none)
+  F_RCNT,      // Algorithm R count of the server's reservoirs
+  F_ASSIGNED,  // arrivals assigned this launch (assign_count_out)
+  F_SCALE,     // service-time scale (us per unit work) of the server, f32 bits
+  F_TAB0,      // ALIAS table of this step, active position s: odd (f32 bits)
+  F_TAB1,      //   alias | server << 8
   F_NUM
 };
 
@@ -130,7 +136,8 @@ struct LaneState {
   static constexpr int WL = Win<MAXS>::WL;
   int32_t cnt[MAXS];      // flows in flight (n_flow_on)
   int32_t head_tc[MAXS];  // t_complete of the head flow (valid if cnt > 0)
-  float score[MAXS];      // SED / LSQ score
+  int32_t lh[MAXS];       // window slot of the head flow
+  int32_t head[MAXS];     // ring position of the head flow
   int32_t next_arr;
   float next_work;
   uint32_t u2, u3, arr_idx, episode, clock, dropped;
@@ -151,12 +158,6 @@ struct Lds {
 template <int MAXS>
 __device__ __forceinline__ int32_t& fld(const Lds& l, int field, int s) {
   return l.f[(field * MAXS + s) * 64 + l.lane];
-}
-
-template <int MAXS>
-__device__ __forceinline__ double den_of(const Lds& l, int s) {
-  const uint32_t lo = (uint32_t)fld<MAXS>(l, F_DEN_LO, s), hi = (uint32_t)fld<MAXS>(l, F_DEN_HI, s);
-  return __hiloint2double((int)hi, (int)lo);
 }
 
 // LDS window slot (server s, slot i) of this lane.
@@ -205,8 +206,8 @@ __device__ __forceinline__ T sel(const T (&a)[MAXS], int i) {
 // servers with weight > 0 in index order (register_as_weights, shm_proxy.py:642-648) are the
 // active list; gen_alias runs in float64 exactly as the reference's Python (sequential sum,
 // avg = sum / (n + 1e-6), p = w / (avg + 1e-6), small / big generators in index order, a big
-// reduced below 1 becomes the next small).  Stored per active position k in the lane's den
-// fields: F_DEN_LO = odd (f32 bits, the alias_t float), F_DEN_HI = alias | server << 8.
+// reduced below 1 becomes the next small).  Stored per active position k in the lane's table
+// fields: F_TAB0 = odd (f32 bits, the alias_t float), F_TAB1 = alias | server << 8.
 // `tab(f, k)` is the table word f (0: odd, 1: alias | server << 8) of active position k.
 // Returns the active count.
 template <int MAXS, typename Tab>
@@ -261,7 +262,7 @@ __device__ __forceinline__ int alias_pick(Tab tab, int n, uint32_t u) {
 template <int MAXS>
 struct FieldAliasTab {
   const Lds& l;
-  __device__ int32_t& operator()(int f, int k) const { return fld<MAXS>(l, F_DEN_LO + f, k); }
+  __device__ int32_t& operator()(int f, int k) const { return fld<MAXS>(l, F_TAB0 + f, k); }
 };
 
 // Arrival draw for one arrival index: gap to it, its work, its two hash words.
@@ -311,14 +312,14 @@ __device__ __forceinline__ void load_servers(const DevState& st, const SimParams
   for (int s = 0; s < MAXS; ++s) {
     L.cnt[s] = 0;
     L.head_tc[s] = 0;
-    L.score[s] = 0.f;
+    L.lh[s] = 0;
+    L.head[s] = 0;
     if (s < p.S) {
       const uint32_t sb = b * (uint32_t)p.S + (uint32_t)s;
       const uint32_t hc = st.hc[sb];
       const int head = (int)(hc & 0xFFFFu);
       L.cnt[s] = (int32_t)(hc >> 16);
-      fld<MAXS>(l, F_HEAD, s) = head;
-      fld<MAXS>(l, F_LH, s) = 0;
+      L.head[s] = head;
       fld<MAXS>(l, F_LAST, s) = st.last_tc[sb];
       fld<MAXS>(l, F_RCNT, s) = (int32_t)st.res_count[sb];
       fld<MAXS>(l, F_ASSIGNED, s) = 0;
@@ -347,9 +348,8 @@ __device__ __forceinline__ void clear_servers(const SimParams& p, LaneState<MAXS
   for (int s = 0; s < MAXS; ++s) {
     L.cnt[s] = 0;
     L.head_tc[s] = 0;
-    L.score[s] = 0.f;
-    fld<MAXS>(l, F_HEAD, s) = 0;
-    fld<MAXS>(l, F_LH, s) = 0;
+    L.lh[s] = 0;
+    L.head[s] = 0;
     fld<MAXS>(l, F_TAIL, s) = 0;
     fld<MAXS>(l, F_LAST, s) = kLastNone;
     fld<MAXS>(l, F_RCNT, s) = 0;
@@ -357,17 +357,36 @@ __device__ __forceinline__ void clear_servers(const SimParams& p, LaneState<MAXS
   }
 }
 
+// Algorithm R slot (reservoir.py:64-85) of the sample that makes count cres + 1: slot cres while
+// the reservoir fills, else j = randint(0, cres + 1) from the 64-bit half (cres & 1) of the Philox
+// block d of index cres >> 1, kept if j < K (-1: not stored).
+__device__ __forceinline__ int reservoir_slot(uint32_t cres, const u32x4& d) {
+  const uint32_t hi = (cres & 1u) ? d.w : d.y;
+  const uint32_t lo = (cres & 1u) ? d.z : d.x;
+  const uint64_t j = mulhi64_by_u33(hi, lo, (uint64_t)cres + 1u);
+  return cres < (uint32_t)K ? (int)cres : (j < (uint64_t)K ? (int)j : -1);
+}
+
+__device__ __forceinline__ uint32_t count_inc(uint32_t c) { return c != 0xFFFFFFFFu ? c + 1u : c; }
+
 // One simulated step of dt_us with server weights w[] (env.py:230-259 with real dynamics).
 //
-// Event loop, one event per iteration per lane: the earliest pending completion (if it is due no
-// later than the next arrival, or than the step end when no arrival is due) or else the next
-// arrival.  The body is straight-line and predicated: both event kinds are evaluated by every
-// lane and at most one server changes per event; its LDS fields are read once and written once.
-// This keeps the 64 lanes (64 envs) converged; a branchy body gets structurised by the compiler
-// into nested per-event-kind loops in which lanes wait for each other.  Per server the
-// completions are processed in t_complete order before any arrival at the same or a later time —
-// the order the oracle (server by server) produces — so every reservoir sees the same insert
-// sequence and the state is bit-identical.
+// Arrival-driven, as the oracle: a FIFO server fixes a flow's completion time when the flow is
+// queued (tc = max(ta, tail) + svc), so its completion sample {fct = tc - ta, duration = svc,
+// ts(tc)} is known at the push, and a server's reservoir sees its samples in FIFO order whatever
+// the interleaving with other servers.  So:
+//   1. flows carried in from earlier steps that complete in this one are inserted first, server
+//      by server in FIFO order (their predecessor's completion is F_LAST);
+//   2. the loop runs one iteration per arrival: first every server pops its flows completed at or
+//      before the arrival (one pop per server per iteration, in parallel over the unrolled
+//      servers; a lane with a second due pop spends one more iteration before its arrival), then
+//      the arrival is assigned on the counts (node.c:388-441) and pushed, and its sample inserted
+//      now if it completes in this step (Algorithm R draw of the server's count);
+//   3. after the last arrival, the pops up to dt; then the rebase.
+// The body is straight-line and predicated, so the 64 lanes (64 envs) stay converged; an iteration
+// costs one arrival's work (two Philox blocks: the next arrival's draw and the pushed flow's
+// Algorithm R draw), and a lane iterates ~arrivals times instead of arrivals + completions.  Every
+// reservoir gets the same insert sequence as the oracle's event order, so the state is bit-identical.
 template <int MAXS, int POLICY, bool TRACE>
 __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
                                          LaneState<MAXS>& L, uint32_t b, const float (&w)[MAXS],
@@ -381,67 +400,141 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
   const uint32_t base_rem = (uint32_t)(base_us - (uint64_t)base_ms * 1000u);
   constexpr bool two_choice = (POLICY == 1 || POLICY == 3);
   constexpr bool alias = POLICY == kPolicyAlias;
+  constexpr bool lsq = (POLICY == 2 || POLICY == 3);
   const uint32_t b0 = b * (uint32_t)S;
   // this env's reservoirs and rings as per-lane (VGPR) pointers: no kernarg reload in the loop
   uint3* const my_res = st.res + (size_t)b0 * K;
   int2* const my_ring = st.ring + (size_t)b0 * (size_t)Q;
   int n_alias = 0;
+  double den[MAXS], rcp[MAXS];
   // SED scores (cnt + 1) / den stay finite (cnt + 1 <= 65) for every finite |den| >= 1e-30
   bool finite_scores = true;
 #pragma unroll
-  for (int s = 0; s < MAXS; ++s)
+  for (int s = 0; s < MAXS; ++s) {
+    den[s] = 1.0;
+    rcp[s] = 1.0;
     if (s < S) fld<MAXS>(l, F_SCALE, s) = (int32_t)__float_as_uint(p.svc_scale[s]);
+  }
   if constexpr (alias) {
     n_alias = build_alias<MAXS>(w, S, FieldAliasTab<MAXS>{l});
-  } else {
+  } else if constexpr (!lsq) {
 #pragma unroll
     for (int s = 0; s < MAXS; ++s) {
       if (s < S) {
-        const double den = (double)w[s] + 1e-9;
-        const double rcp = 1.0 / den;
-        finite_scores &= fabs(den) >= 1e-30 && fabs(den) <= 1e300;  // false for NaN
-        fld<MAXS>(l, F_DEN_LO, s) = (int32_t)__double2loint(den);
-        fld<MAXS>(l, F_DEN_HI, s) = (int32_t)__double2hiint(den);
-        fld<MAXS>(l, F_RCP_LO, s) = (int32_t)__double2loint(rcp);
-        fld<MAXS>(l, F_RCP_HI, s) = (int32_t)__double2hiint(rcp);
-        L.score[s] = policy_score(POLICY, L.cnt[s], den);
+        den[s] = (double)w[s] + 1e-9;
+        rcp[s] = 1.0 / den[s];
+        finite_scores &= fabs(den[s]) >= 1e-30 && fabs(den[s]) <= 1e300;  // false for NaN
       }
     }
   }
-  for (;;) {
-    // ---- which event: earliest completion (ties: lowest server) vs next arrival
-    int32_t tmin = 0x7FFFFFFF;
-    int smin = -1;
-#pragma unroll
-    for (int s = 0; s < MAXS; ++s) {  // bitwise &: no short-circuit control flow
-      const bool c = (s < S) & (L.cnt[s] > 0) & (L.head_tc[s] < tmin);
-      tmin = c ? L.head_tc[s] : tmin;
-      smin = c ? s : smin;
-    }
-    const bool arrival_due = L.next_arr < dt;
-    const int32_t horizon = arrival_due ? L.next_arr : dt;
-    const bool comp = smin >= 0 && tmin <= horizon;
-    const bool arr = !comp && arrival_due;
-    if (!comp && !arr) break;
 
-    // ---- arrival: choose a server (node.c:388-441); full servers are not eligible
+  // ---- 1. carried-in flows completing in this step: samples in FIFO order per server
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) {
+    if (s < S && L.cnt[s] > 0 && L.head_tc[s] <= dt) {
+      int32_t prev = fld<MAXS>(l, F_LAST, s);
+      uint32_t rc = (uint32_t)fld<MAXS>(l, F_RCNT, s);
+      const int c = L.cnt[s];
+      int32_t etc = L.head_tc[s];
+      int32_t eta = qslot<MAXS>(l, s, L.lh[s])->y;
+      int i = 0;
+      for (;;) {
+        const u32x4 d = philox4x32_10(
+            u32x4{rc >> 1, L.gid, L.episode, (kStreamReservoir << 24) | (uint32_t)s}, p.key0, p.key1);
+        const int slot = reservoir_slot(rc, d);
+        if (slot >= 0)
+          my_res[(uint32_t)s * (uint32_t)K + (uint32_t)slot] =
+              make_uint3((uint32_t)(etc - eta), (uint32_t)(etc - (eta > prev ? eta : prev)),
+                         base_ms + (base_rem + (uint32_t)etc) / 1000u);
+        prev = etc;
+        rc = count_inc(rc);
+        if (++i >= c) break;
+        int2 e;
+        if (i < WL) {
+          int li = L.lh[s] + i;
+          li = li >= WL ? li - WL : li;
+          e = *qslot<MAXS>(l, s, li);
+        } else {  // rare: beyond the window
+          int pos = L.head[s] + i;
+          pos = pos >= Q ? pos - Q : pos;
+          e = my_ring[(uint32_t)s * (uint32_t)Q + (uint32_t)pos];
+        }
+        etc = e.x;
+        eta = e.y;
+        if (etc > dt) break;
+      }
+      fld<MAXS>(l, F_LAST, s) = prev;
+      fld<MAXS>(l, F_RCNT, s) = (int32_t)rc;
+    }
+  }
+
+  // ---- 2. one arrival per iteration (3. the final pops up to dt in the last iterations)
+  for (;;) {
+    const bool arrival_due = L.next_arr < dt;
+    const int32_t th = arrival_due ? L.next_arr : dt;  // a completion at the arrival time goes first
+    bool more = false;
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) {  // pop each server's head if it completed by th
+      const bool due = (s < S) & (L.cnt[s] > 0) & (L.head_tc[s] <= th);
+      const int nl = (L.lh[s] + 1 == WL) ? 0 : L.lh[s] + 1;
+      const int nh = (L.head[s] + 1 == Q) ? 0 : L.head[s] + 1;
+      if (due && L.cnt[s] - 1 >= WL) {  // rare: bring queue entry WL (ring) into the freed slot
+        int pw = nh + WL - 1;
+        pw = pw >= Q ? pw - Q : pw;
+        *qslot<MAXS>(l, s, L.lh[s]) = my_ring[(uint32_t)s * (uint32_t)Q + (uint32_t)pw];
+        __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);  // drain in the rare branch, not at the back-edge
+      }
+      const int32_t nt = qslot<MAXS>(l, s, nl)->x;  // next head (valid if cnt > 1)
+      L.cnt[s] -= due ? 1 : 0;
+      L.lh[s] = due ? nl : L.lh[s];
+      L.head[s] = due ? nh : L.head[s];
+      L.head_tc[s] = due ? nt : L.head_tc[s];
+      more |= due & (L.cnt[s] > 0) & (nt <= th);
+    }
+    if (!arrival_due && !more) break;
+    const bool arr = arrival_due & !more;
+
+    // ---- the arrival: choose a server (node.c:388-441); full servers are not eligible
     const int32_t ta = L.next_arr;
+    float score[MAXS];
+    if constexpr (!alias) {
+      bool bad = false;
+#pragma unroll
+      for (int s = 0; s < MAXS; ++s) {
+        if constexpr (lsq) {
+          score[s] = (float)L.cnt[s];
+        } else {  // (cnt + 1) / den correctly rounded by Markstein's corrected quotient
+          const double c = (double)(L.cnt[s] + 1);
+          const double q0 = c * rcp[s];
+          const double q = fma(fma(-q0, den[s], c), rcp[s], q0);
+          bad |= q != q;
+          score[s] = (float)q;
+        }
+      }
+      if (!lsq && bad) {  // den 0 / inf / NaN: the division
+#pragma unroll
+        for (int s = 0; s < MAXS; ++s) {
+          const float q = score[s];
+          if (q != q) score[s] = (float)((double)(L.cnt[s] + 1) / den[s]);
+        }
+      }
+    }
     int chosen = -1;
     if constexpr (alias) {  // full server: the flow is dropped (ALIAS has no eligibility test)
       if (n_alias > 0) {
         const int a = alias_pick(FieldAliasTab<MAXS>{l}, n_alias, L.u2);
         chosen = sel<MAXS>(L.cnt, a) < Q ? a : -1;
       }
-    } else if constexpr (two_choice) {  // SED2 / LSQ2: two candidates, keep the second if strictly better
+    } else if constexpr (two_choice) {  // SED2 / LSQ2: keep the second candidate if strictly better
       const int h1 = (int)__umulhi(L.u2, (uint32_t)S);  // (u * S) >> 32
       const int h2 = (int)__umulhi(L.u3, (uint32_t)S);
       float s1 = 0.f, s2 = 0.f;
       bool ok1 = false, ok2 = false;
 #pragma unroll
       for (int s = 0; s < MAXS; ++s) {
-        s1 = (s == h1) ? L.score[s] : s1;
+        s1 = (s == h1) ? score[s] : s1;
         ok1 = (s == h1) ? (L.cnt[s] < Q) : ok1;
-        s2 = (s == h2) ? L.score[s] : s2;
+        s2 = (s == h2) ? score[s] : s2;
         ok2 = (s == h2) ? (L.cnt[s] < Q) : ok2;
       }
       chosen = (ok1 && ok2) ? ((s2 < s1) ? h2 : h1) : (ok1 ? h1 : (ok2 ? h2 : -1));
@@ -452,117 +545,83 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
       for (int s = 0; s < MAXS; ++s) {
         const bool m = (s == h) & (L.cnt[s] < Q);
         chosen = m ? s : chosen;
-        best = m ? L.score[s] : best;
+        best = m ? score[s] : best;
       }
       if (finite_scores) {  // every score finite: "replace on strictly lower" from +inf is exact
 #pragma unroll
         for (int s = 0; s < MAXS; ++s) {
-          const bool m = (s < S) & (L.cnt[s] < Q) & (L.score[s] < best);
+          const bool m = (s < S) & (L.cnt[s] < Q) & (score[s] < best);
           chosen = m ? s : chosen;
-          best = m ? L.score[s] : best;
+          best = m ? score[s] : best;
         }
       } else {  // NaN / inf scores: the first eligible server is taken whatever its score
 #pragma unroll
         for (int s = 0; s < MAXS; ++s) {
-          const bool m = (s < S) & (L.cnt[s] < Q) & ((chosen < 0) | (L.score[s] < best));
+          const bool m = (s < S) & (L.cnt[s] < Q) & ((chosen < 0) | (score[s] < best));
           chosen = m ? s : chosen;
-          best = m ? L.score[s] : best;
+          best = m ? score[s] : best;
         }
       }
     }
     const bool push = arr && chosen >= 0;
     L.dropped += (arr && chosen < 0) ? 1u : 0u;
 
-    // ---- the one server this event changes, and its fields
-    const int cs = comp ? smin : (push ? chosen : -1);
-    const int csi = cs < 0 ? 0 : cs;
-    int32_t c_cnt = 0;
+    // ---- the chosen server: FIFO service starts when its last queued flow ends
+    const int cs = push ? chosen : 0;
+    int32_t c_cnt = 0, c_lh = 0, c_head = 0;
 #pragma unroll
-    for (int s = 0; s < MAXS; ++s) c_cnt = (s == cs) ? L.cnt[s] : c_cnt;
-    const int32_t c_head = fld<MAXS>(l, F_HEAD, csi);
-    const int32_t c_lh = fld<MAXS>(l, F_LH, csi);
-    const int32_t c_tail = fld<MAXS>(l, F_TAIL, csi);
-    const int32_t c_last = fld<MAXS>(l, F_LAST, csi);
-    const uint32_t cres = (uint32_t)fld<MAXS>(l, F_RCNT, csi);
-    const double c_den = den_of<MAXS>(l, csi);
-    const double c_rcp = __hiloint2double(fld<MAXS>(l, F_RCP_HI, csi), fld<MAXS>(l, F_RCP_LO, csi));
-    const float c_scale = __uint_as_float((uint32_t)fld<MAXS>(l, F_SCALE, csi));
-
-    // ---- the one Philox block of this event (Algorithm R draw, or the next arrival's draw)
-    const u32x4 ctr = comp
-        ? u32x4{cres >> 1, L.gid, L.episode, (kStreamReservoir << 24) | (uint32_t)smin}
-        : u32x4{L.arr_idx + 1u, L.gid, L.episode, kStreamArrival << 24};
-    const u32x4 d = philox4x32_10(ctr, p.key0, p.key1);
-
-    // ---- completion (lbhash.h:116-124, 131-135) + Algorithm R (reservoir.py:64-85)
-    const int32_t tc = tmin;
-    const int32_t h_ta = qslot<MAXS>(l, csi, c_lh)->y;  // arrival time of the head flow
-    const int32_t start_c = h_ta > c_last ? h_ta : c_last;
-    const int h_next = (c_head + 1 == Q) ? 0 : c_head + 1;
-    const int lh_next = (c_lh + 1 == WL) ? 0 : c_lh + 1;
-    int slot;
-    {
-      const uint32_t hi = (cres & 1u) ? d.w : d.y;
-      const uint32_t lo = (cres & 1u) ? d.z : d.x;
-      const uint64_t j = mulhi64_by_u33(hi, lo, (uint64_t)cres + 1u);
-      slot = cres < (uint32_t)K ? (int)cres : (j < (uint64_t)K ? (int)j : -1);
+    for (int s = 0; s < MAXS; ++s) {
+      const bool m = s == cs;
+      c_cnt = m ? L.cnt[s] : c_cnt;
+      c_lh = m ? L.lh[s] : c_lh;
+      c_head = m ? L.head[s] : c_head;
     }
-    if (comp && slot >= 0) {
-      my_res[(uint32_t)smin * (uint32_t)K + (uint32_t)slot] =
-          make_uint3((uint32_t)(tc - h_ta), (uint32_t)(tc - start_c),
-                     base_ms + (base_rem + (uint32_t)tc) / 1000u);
-    }
-    // rare: the queue is longer than the window; bring entry WL-1 (after this pop) into LDS
-    if (comp && c_cnt - 1 >= WL) {
-      int pw = h_next + WL - 1;
-      pw = pw >= Q ? pw - Q : pw;
-      *qslot<MAXS>(l, csi, c_lh) = my_ring[(uint32_t)csi * (uint32_t)Q + (uint32_t)pw];
-      __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);  // drain in the rare branch, not at the back-edge
-    }
-    const int32_t nxt_tc = qslot<MAXS>(l, csi, lh_next)->x;  // next head (valid if cnt > 1)
-
-    // ---- arrival: FIFO service starts when the server's last queued flow ends
-    const float a_scale = c_scale;  // csi is the chosen server whenever the flow is pushed
+    const int32_t c_tail = fld<MAXS>(l, F_TAIL, cs);
+    const uint32_t cres = (uint32_t)fld<MAXS>(l, F_RCNT, cs);
+    const float c_scale = __uint_as_float((uint32_t)fld<MAXS>(l, F_SCALE, cs));
     const int32_t start_a = c_cnt > 0 ? (c_tail > ta ? c_tail : ta) : ta;
-    int32_t svc = (int32_t)(L.next_work * a_scale);
+    int32_t svc = (int32_t)(L.next_work * c_scale);
     svc = svc < 1 ? 1 : svc;
     const int32_t tc_a = start_a + svc;
+    // completes in this step: its sample now (duration = tc - max(ta, predecessor's tc) = svc)
+    const bool ins = push && tc_a <= dt;
+
+    // ---- two Philox blocks: the pushed flow's Algorithm R draw, the next arrival's draw
+    const u32x4 dr = philox4x32_10(
+        u32x4{cres >> 1, L.gid, L.episode, (kStreamReservoir << 24) | (uint32_t)cs}, p.key0, p.key1);
+    const u32x4 d = philox4x32_10(u32x4{L.arr_idx + 1u, L.gid, L.episode, kStreamArrival << 24},
+                                  p.key0, p.key1);
+    const int slot = reservoir_slot(cres, dr);
+    if (ins && slot >= 0) {
+      my_res[(uint32_t)cs * (uint32_t)K + (uint32_t)slot] =
+          make_uint3((uint32_t)(tc_a - ta), (uint32_t)svc, base_ms + (base_rem + (uint32_t)tc_a) / 1000u);
+    }
     if (push) {  // queue index < WL: LDS window only; beyond it: the HBM ring (overflow)
       const int2 e = make_int2(tc_a, ta);
       if (c_cnt < WL) {
         int li = c_lh + c_cnt;
         li = li >= WL ? li - WL : li;
-        *qslot<MAXS>(l, csi, li) = e;
+        *qslot<MAXS>(l, cs, li) = e;
       } else {
         int pos = c_head + c_cnt;
         pos = pos >= Q ? pos - Q : pos;
-        my_ring[(uint32_t)csi * (uint32_t)Q + (uint32_t)pos] = e;
+        my_ring[(uint32_t)cs * (uint32_t)Q + (uint32_t)pos] = e;
         // keeps the compiler from sinking the two stores' common half into one flat (generic
         // pointer) store, which counts in lgkmcnt too: every LDS wait would then wait on it
         asm volatile("");
       }
+      fld<MAXS>(l, F_TAIL, cs) = tc_a;
+      atomicAdd(&fld<MAXS>(l, F_ASSIGNED, cs), 1);  // ds_add_u32: no read-back, no wait
     }
-
-    // ---- write back the changed server
-    const int32_t n_cs = comp ? c_cnt - 1 : c_cnt + 1;
-    const float sc_new = policy_score_r(POLICY, n_cs, c_den, c_rcp);
-    if (comp) {
-      fld<MAXS>(l, F_RCNT, csi) = (int32_t)(cres != 0xFFFFFFFFu ? cres + 1u : cres);
-      fld<MAXS>(l, F_LAST, csi) = tc;
-      fld<MAXS>(l, F_HEAD, csi) = h_next;
-      fld<MAXS>(l, F_LH, csi) = lh_next;
+    if (ins) {
+      fld<MAXS>(l, F_RCNT, cs) = (int32_t)count_inc(cres);
+      fld<MAXS>(l, F_LAST, cs) = tc_a;
     }
-    if (push) {
-      fld<MAXS>(l, F_TAIL, csi) = tc_a;
-      atomicAdd(&fld<MAXS>(l, F_ASSIGNED, csi), 1);  // ds_add_u32: no read-back, no wait
-    }
-    const int32_t new_head_tc = comp ? nxt_tc : tc_a;
 #pragma unroll
     for (int s = 0; s < MAXS; ++s) {
-      const bool m = s == cs;
-      L.cnt[s] = m ? n_cs : L.cnt[s];
-      L.score[s] = m ? sc_new : L.score[s];
-      L.head_tc[s] = (m && (comp || c_cnt == 0)) ? new_head_tc : L.head_tc[s];
+      const bool m = push & (s == cs);
+      L.head_tc[s] = (m && c_cnt == 0) ? tc_a : L.head_tc[s];
+      L.cnt[s] += m ? 1 : 0;
     }
 
     // ---- next arrival (draw d belongs to arrival index arr_idx + 1)
@@ -595,7 +654,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) {
     if (s < S) {
-      const int lh = fld<MAXS>(l, F_LH, s);
+      const int lh = L.lh[s];
       for (int i = 0; i < WL && i < L.cnt[s]; ++i) {
         int li = lh + i;
         li = li >= WL ? li - WL : li;
@@ -604,7 +663,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
         e->y -= dt;
       }
       const uint32_t sbase = b0 + (uint32_t)s;
-      int pos = fld<MAXS>(l, F_HEAD, s) + WL;
+      int pos = L.head[s] + WL;
       if (pos >= Q) pos -= Q;
       for (int i = WL; i < L.cnt[s]; ++i) {
         int2 e = st.ring[sbase * (uint32_t)Q + (uint32_t)pos];
@@ -633,7 +692,7 @@ __device__ __forceinline__ void store_servers(const DevState& st, const SimParam
   for (int s = 0; s < MAXS; ++s) {
     if (s < p.S) {
       const uint32_t sb = b * (uint32_t)p.S + (uint32_t)s;
-      const int head = fld<MAXS>(l, F_HEAD, s), lh = fld<MAXS>(l, F_LH, s);
+      const int head = L.head[s], lh = L.lh[s];
       for (int i = 0; i < WL && i < L.cnt[s]; ++i) {
         int pos = head + i;
         if (pos >= p.Q) pos -= p.Q;
@@ -1402,9 +1461,9 @@ __global__ void __launch_bounds__(64)
   const int na = build_alias<MAX_S>(w, S, FieldAliasTab<MAX_S>{l});
   for (int k = 0; k < S; ++k) {
     const bool v = k < na;
-    odd_out[r * S + k] = v ? __uint_as_float((uint32_t)fld<MAX_S>(l, F_DEN_LO, k)) : 1.0f;
-    alias_out[r * S + k] = v ? (fld<MAX_S>(l, F_DEN_HI, k) & 0xFF) : 0;
-    active_out[r * S + k] = v ? (fld<MAX_S>(l, F_DEN_HI, k) >> 8) : -1;
+    odd_out[r * S + k] = v ? __uint_as_float((uint32_t)fld<MAX_S>(l, F_TAB0, k)) : 1.0f;
+    alias_out[r * S + k] = v ? (fld<MAX_S>(l, F_TAB1, k) & 0xFF) : 0;
+    active_out[r * S + k] = v ? (fld<MAX_S>(l, F_TAB1, k) >> 8) : -1;
   }
 }
 
