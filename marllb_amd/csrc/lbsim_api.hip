@@ -216,7 +216,8 @@ struct ProfScope {
 template <int MAXS, int MODE, int POLICY>
 void launch_dyn(lbsim_t* h, const void* action, int dtype, int32_t* assign, const uint8_t* mask,
                 hipStream_t stream) {
-  const dim3 block(64), grid((unsigned)((h->B + 63) / 64));
+  constexpr unsigned epb = 64u * kDynWaves<MAXS>;  // envs per workgroup (one per CU, kDynWaves)
+  const dim3 block(epb), grid((unsigned)((h->B + epb - 1) / epb));
   if (h->prm.trace)
     hipLaunchKernelGGL((dynamics_kernel<MAXS, MODE, POLICY, true>), grid, block, 0, stream, h->st,
                        h->prm, action, dtype, assign, mask);

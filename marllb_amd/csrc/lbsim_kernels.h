@@ -723,18 +723,29 @@ __device__ __forceinline__ float action_weight(const SimParams& p, const void* a
   return a < p.min_w ? p.min_w : (a > p.max_w ? p.max_w : a);
 }
 
+// Waves per workgroup of dynamics_kernel.  Every wave runs a long, issue-bound event loop, so a
+// SIMD holding two waves finishes twice as late.  With one-wave workgroups the dispatcher stacked
+// some CUs (up to 6 fit by LDS) while others had room: at 65536 x 4 (1024 waves on 1024 SIMDs) the
+// kernel lasted 1.42x the mean wave lifetime (rocprofv3 SQ_WAVE_CYCLES vs duration), and capping
+// the CUs at 4 workgroups cut it 0.308 -> 0.266 ms.  Here one workgroup is 4 waves whose LDS
+// (> half a CU's 160 KiB) admits one workgroup per CU: its waves land on the CU's 4 SIMDs.
+// MAXS = 16 (44 KiB per wave) takes 2 waves per workgroup.
+template <int MAXS>
+constexpr int kDynWaves = MAXS <= 8 ? 4 : 2;
+
 // MODE is a template parameter so step and reset launches are separate kernels in profiles.
 // POLICY and TRACE (arrival source) are template parameters: each combination gets its own
 // straight-line event loop.
 template <int MAXS, int MODE, int POLICY, bool TRACE>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64 * kDynWaves<MAXS>)
     dynamics_kernel(DevState st, SimParams p, const void* action, int action_dtype,
                     int32_t* assign_out, const uint8_t* reset_mask) {
   constexpr int mode = MODE;
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  __shared__ int2 qwin[MAXS * Win<MAXS>::WL * 64];
-  __shared__ int32_t fields[F_NUM * MAXS * 64];
-  const Lds l{qwin, fields, (int)threadIdx.x};
+  const uint32_t b = blockIdx.x * (64u * kDynWaves<MAXS>) + threadIdx.x;
+  const int wv = (int)(threadIdx.x >> 6);
+  __shared__ int2 qwin[kDynWaves<MAXS>][MAXS * Win<MAXS>::WL * 64];
+  __shared__ int32_t fields[kDynWaves<MAXS>][F_NUM * MAXS * 64];
+  const Lds l{qwin[wv], fields[wv], (int)(threadIdx.x & 63u)};
   if (b >= (uint32_t)p.B) return;
   const int S = p.S;
   LaneState<MAXS> L;
