@@ -114,6 +114,7 @@ __device__ __forceinline__ uint32_t trace_row(const SimParams& p, uint32_t gid, 
 template <int MAXS>
 struct Win {
   static constexpr int WL = MAXS <= 4 ? 8 : (MAXS <= 8 ? 4 : 2);  // LDS <= 16 / 16 / 16 KiB
+  static_assert((WL & (WL - 1)) == 0, "window slots wrap by mask");
 };
 
 // Per-server fields read or written only for the server an arrival picks live in LDS, lane-major
@@ -122,7 +123,6 @@ struct Win {
 // ring head positions, the SED denominators) stay in registers.
 enum SrvField {
   F_TAIL = 0,  // t_complete of the last queued flow (valid if cnt > 0)
-  F_LAST,      // t_complete of the last completed flow (kLastNone if none)
   F_RCNT,      // Algorithm R count of the server's reservoirs
   F_ASSIGNED,  // arrivals assigned this launch (assign_count_out)
   F_SCALE,     // service-time scale (us per unit work) of the server, f32 bits
@@ -138,6 +138,7 @@ struct LaneState {
   int32_t head_tc[MAXS];  // t_complete of the head flow (valid if cnt > 0)
   int32_t lh[MAXS];       // window slot of the head flow
   int32_t head[MAXS];     // ring position of the head flow
+  int32_t last[MAXS];     // t_complete of the last completed flow (kLastNone if none)
   int32_t next_arr;
   float next_work;
   uint32_t u2, u3, arr_idx, episode, clock, dropped;
@@ -164,6 +165,13 @@ __device__ __forceinline__ int32_t& fld(const Lds& l, int field, int s) {
 template <int MAXS>
 __device__ __forceinline__ int2* qslot(const Lds& l, int s, int i) {
   return l.q + ((s * Win<MAXS>::WL + i) * 64 + l.lane);
+}
+
+// The lane's scratch slot after the window rows: the target of a push that does not happen, so
+// the push store needs no branch.
+template <int MAXS>
+__device__ __forceinline__ int2* qdummy(const Lds& l) {
+  return l.q + (MAXS * Win<MAXS>::WL * 64 + l.lane);
 }
 
 constexpr int kPolicyAlias = 4;
@@ -314,13 +322,14 @@ __device__ __forceinline__ void load_servers(const DevState& st, const SimParams
     L.head_tc[s] = 0;
     L.lh[s] = 0;
     L.head[s] = 0;
+    L.last[s] = kLastNone;
     if (s < p.S) {
       const uint32_t sb = b * (uint32_t)p.S + (uint32_t)s;
       const uint32_t hc = st.hc[sb];
       const int head = (int)(hc & 0xFFFFu);
       L.cnt[s] = (int32_t)(hc >> 16);
       L.head[s] = head;
-      fld<MAXS>(l, F_LAST, s) = st.last_tc[sb];
+      L.last[s] = st.last_tc[sb];
       fld<MAXS>(l, F_RCNT, s) = (int32_t)st.res_count[sb];
       fld<MAXS>(l, F_ASSIGNED, s) = 0;
       int32_t tail = 0;
@@ -351,7 +360,7 @@ __device__ __forceinline__ void clear_servers(const SimParams& p, LaneState<MAXS
     L.lh[s] = 0;
     L.head[s] = 0;
     fld<MAXS>(l, F_TAIL, s) = 0;
-    fld<MAXS>(l, F_LAST, s) = kLastNone;
+    L.last[s] = kLastNone;
     fld<MAXS>(l, F_RCNT, s) = 0;
     fld<MAXS>(l, F_ASSIGNED, s) = 0;
   }
@@ -376,7 +385,7 @@ __device__ __forceinline__ uint32_t count_inc(uint32_t c) { return c != 0xFFFFFF
 // ts(tc)} is known at the push, and a server's reservoir sees its samples in FIFO order whatever
 // the interleaving with other servers.  So:
 //   1. flows carried in from earlier steps that complete in this one are inserted first, server
-//      by server in FIFO order (their predecessor's completion is F_LAST);
+//      by server in FIFO order (their predecessor's completion is last[s]);
 //   2. the loop runs one iteration per arrival: first every server pops its flows completed at or
 //      before the arrival (one pop per server per iteration, in parallel over the unrolled
 //      servers; a lane with a second due pop spends one more iteration before its arrival), then
@@ -432,7 +441,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) {
     if (s < S && L.cnt[s] > 0 && L.head_tc[s] <= dt) {
-      int32_t prev = fld<MAXS>(l, F_LAST, s);
+      int32_t prev = L.last[s];
       uint32_t rc = (uint32_t)fld<MAXS>(l, F_RCNT, s);
       const int c = L.cnt[s];
       int32_t etc = L.head_tc[s];
@@ -463,7 +472,6 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
         eta = e.y;
         if (etc > dt) break;
       }
-      fld<MAXS>(l, F_LAST, s) = prev;
       fld<MAXS>(l, F_RCNT, s) = (int32_t)rc;
     }
   }
@@ -476,7 +484,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
 #pragma unroll
     for (int s = 0; s < MAXS; ++s) {  // pop each server's head if it completed by th
       const bool due = (s < S) & (L.cnt[s] > 0) & (L.head_tc[s] <= th);
-      const int nl = (L.lh[s] + 1 == WL) ? 0 : L.lh[s] + 1;
+      const int nl = (L.lh[s] + 1) & (WL - 1);
       const int nh = (L.head[s] + 1 == Q) ? 0 : L.head[s] + 1;
       if (due && L.cnt[s] - 1 >= WL) {  // rare: bring queue entry WL (ring) into the freed slot
         int pw = nh + WL - 1;
@@ -485,6 +493,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
         __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);  // drain in the rare branch, not at the back-edge
       }
       const int32_t nt = qslot<MAXS>(l, s, nl)->x;  // next head (valid if cnt > 1)
+      L.last[s] = due ? L.head_tc[s] : L.last[s];
       L.cnt[s] -= due ? 1 : 0;
       L.lh[s] = due ? nl : L.lh[s];
       L.head[s] = due ? nh : L.head[s];
@@ -596,27 +605,21 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
       my_res[(uint32_t)cs * (uint32_t)K + (uint32_t)slot] =
           make_uint3((uint32_t)(tc_a - ta), (uint32_t)svc, base_ms + (base_rem + (uint32_t)tc_a) / 1000u);
     }
-    if (push) {  // queue index < WL: LDS window only; beyond it: the HBM ring (overflow)
-      const int2 e = make_int2(tc_a, ta);
-      if (c_cnt < WL) {
-        int li = c_lh + c_cnt;
-        li = li >= WL ? li - WL : li;
-        *qslot<MAXS>(l, cs, li) = e;
-      } else {
-        int pos = c_head + c_cnt;
-        pos = pos >= Q ? pos - Q : pos;
-        my_ring[(uint32_t)cs * (uint32_t)Q + (uint32_t)pos] = e;
-        // keeps the compiler from sinking the two stores' common half into one flat (generic
-        // pointer) store, which counts in lgkmcnt too: every LDS wait would then wait on it
-        asm volatile("");
-      }
-      fld<MAXS>(l, F_TAIL, cs) = tc_a;
-      atomicAdd(&fld<MAXS>(l, F_ASSIGNED, cs), 1);  // ds_add_u32: no read-back, no wait
+    // queue index < WL: the LDS window (a push that does not happen writes the lane's scratch
+    // slot); beyond it: the HBM ring (overflow, rare)
+    *((push & (c_cnt < WL)) ? qslot<MAXS>(l, cs, (c_lh + c_cnt) & (WL - 1)) : qdummy<MAXS>(l)) =
+        make_int2(tc_a, ta);
+    if (push && c_cnt >= WL) {
+      int pos = c_head + c_cnt;
+      pos = pos >= Q ? pos - Q : pos;
+      my_ring[(uint32_t)cs * (uint32_t)Q + (uint32_t)pos] = make_int2(tc_a, ta);
+      // keeps the compiler from sinking the store into a flat (generic pointer) store shared with
+      // the window store, which counts in lgkmcnt too: every LDS wait would then wait on it
+      asm volatile("");
     }
-    if (ins) {
-      fld<MAXS>(l, F_RCNT, cs) = (int32_t)count_inc(cres);
-      fld<MAXS>(l, F_LAST, cs) = tc_a;
-    }
+    fld<MAXS>(l, F_TAIL, cs) = push ? tc_a : c_tail;
+    atomicAdd(&fld<MAXS>(l, F_ASSIGNED, cs), push ? 1 : 0);  // ds_add_u32: no read-back, no wait
+    fld<MAXS>(l, F_RCNT, cs) = (int32_t)(ins ? count_inc(cres) : cres);
 #pragma unroll
     for (int s = 0; s < MAXS; ++s) {
       const bool m = push & (s == cs);
@@ -674,8 +677,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
       }
       L.head_tc[s] -= dt;
       fld<MAXS>(l, F_TAIL, s) -= dt;
-      const int32_t last = fld<MAXS>(l, F_LAST, s);
-      fld<MAXS>(l, F_LAST, s) = (last < kLastNone + dt) ? kLastNone : last - dt;
+      L.last[s] = (L.last[s] < kLastNone + dt) ? kLastNone : L.last[s] - dt;
     }
   }
   L.clock += 1u;
@@ -701,7 +703,7 @@ __device__ __forceinline__ void store_servers(const DevState& st, const SimParam
         st.ring[sb * (uint32_t)p.Q + (uint32_t)pos] = *qslot<MAXS>(l, s, li);
       }
       st.hc[sb] = (uint32_t)head | ((uint32_t)L.cnt[s] << 16);
-      st.last_tc[sb] = fld<MAXS>(l, F_LAST, s);
+      st.last_tc[sb] = L.last[s];
       st.res_count[sb] = (uint32_t)fld<MAXS>(l, F_RCNT, s);
       if (assign_out != nullptr) assign_out[sb] = fld<MAXS>(l, F_ASSIGNED, s);
     }
@@ -743,7 +745,7 @@ __global__ void __launch_bounds__(64 * kDynWaves<MAXS>)
   constexpr int mode = MODE;
   const uint32_t b = blockIdx.x * (64u * kDynWaves<MAXS>) + threadIdx.x;
   const int wv = (int)(threadIdx.x >> 6);
-  __shared__ int2 qwin[kDynWaves<MAXS>][MAXS * Win<MAXS>::WL * 64];
+  __shared__ int2 qwin[kDynWaves<MAXS>][(MAXS * Win<MAXS>::WL + 1) * 64];  // + scratch slots
   __shared__ int32_t fields[kDynWaves<MAXS>][F_NUM * MAXS * 64];
   const Lds l{qwin[wv], fields[wv], (int)(threadIdx.x & 63u)};
   if (b >= (uint32_t)p.B) return;
