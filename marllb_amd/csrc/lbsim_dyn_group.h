@@ -8,17 +8,19 @@
 // layout as dynamics_kernel, so the two mappings are interchangeable between
 // launches and bit-identical to the oracle.
 //
-// Per event, the group agrees on the event with DPP reductions inside a 16-lane row (no LDS):
-//   earliest completion: min over head_tc (quad_perm / row_half_mirror / row_mirror), lowest
-//     server among ties from a ballot;
+// Arrival-driven like dynamics_kernel's sim_step: each iteration, every lane pops its own server's
+// head if it completed by the next arrival (a group with a second due pop spends one more
+// iteration), then the group assigns the arrival:
 //   SED / LSQ choice: the reference's scan "start at the hashed server h, replace on a strictly
 //     lower score" equals: h (or the first eligible server when h is full) if its score is the
-//     minimum or NaN, else the lowest eligible server holding the minimum — one min reduction and
-//     two ballots;
+//     minimum or NaN, else the lowest eligible server holding the minimum — one DPP min reduction
+//     inside the group's row and two ballots;
 //   SED2 / LSQ2: the two candidates' scores broadcast by OR-reducing a one-hot word.
-// Each lane runs the event's Philox block with its own counter: for a completion only the owning
-// lane's reservoir draw is used, for an arrival every lane draws the same block.  Per-server fields
-// are plain registers (one server per lane); the queue window lives in LDS [slot][lane].
+// One Philox block per lane per iteration: the chosen server's lane draws its Algorithm R block
+// (the pushed flow's sample is inserted at once if it completes in this step), every other lane
+// the next arrival's block, which the group reads from a lane that is not the chosen one.
+// Per-server fields are plain registers (one server per lane); the queue window lives in LDS
+// [slot][lane].
 #pragma once
 
 #include "lbsim_kernels.h"
@@ -113,37 +115,93 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
   const uint32_t base_rem = (uint32_t)(base_us - (uint64_t)base_ms * 1000u);
   constexpr bool two_choice = (POLICY == 1 || POLICY == 3);
   constexpr bool alias = POLICY == kPolicyAlias;
+  constexpr bool lsq = (POLICY == 2 || POLICY == 3);
   const uint32_t sb = b * (uint32_t)S + (uint32_t)s;  // valid when V.act
+  uint3* const my_res = st.res + (size_t)sb * K;
+  int2* const my_ring = st.ring + (size_t)sb * (size_t)Q;
   const GroupAliasTab tab{atab, gbase};
+  const int lane = gbase + s;
   int n_alias = 0;
   if constexpr (alias) {
     n_alias = build_alias<G>(wall, S, tab);
-  } else if (V.act) {
+  } else if (V.act && !lsq) {
     V.den = (double)w_own + 1e-9;
     V.rcp = 1.0 / V.den;
-    V.score = policy_score(POLICY, V.cnt, V.den);
   }
-  auto wslot = [&](int i) -> int2* { return win + i * 64 + (gbase + s); };
-  for (;;) {
-    // ---- which event: earliest completion of the group (ties: lowest server) vs next arrival
-    const int32_t key = (V.act && V.cnt > 0) ? V.head_tc : 0x7FFFFFFF;
-    const bool elig = V.act && V.cnt < Q;
-    const bool num = elig && V.score == V.score;
-    int32_t tmin = key;
-    int32_t mk = num ? f32_key(V.score) : 0x7f800000;  // SED / LSQ: min eligible score (+inf)
-    if constexpr (!alias && !two_choice) group_min2<G>(tmin, mk);
-    else tmin = group_min_i32<G>(key);
-    const float m = key_f32(mk);
-    const uint32_t tb = group_bits<G>(__ballot(key == tmin && tmin != 0x7FFFFFFF), gbase);
-    const int smin = tb ? __builtin_ctz(tb) : -1;
-    const bool arrival_due = E.next_arr < dt;
-    const int32_t horizon = arrival_due ? E.next_arr : dt;
-    const bool comp = smin >= 0 && tmin <= horizon;
-    const bool arr = !comp && arrival_due;
-    if (!comp && !arr) break;
+  auto wslot = [&](int i) -> int2* { return win + i * 64 + lane; };
 
-    // ---- arrival: choose a server (node.c:388-441); full servers are not eligible
+  // ---- 1. this lane's carried-in flows that complete in this step: samples in FIFO order
+  if (V.act && V.cnt > 0 && V.head_tc <= dt) {
+    int32_t prev = V.last;
+    uint32_t rc = V.rcnt;
+    int32_t etc = V.head_tc;
+    int32_t eta = wslot(V.lh)->y;
+    int i = 0;
+    for (;;) {
+      const u32x4 d = philox4x32_10(
+          u32x4{rc >> 1, E.gid, E.episode, (kStreamReservoir << 24) | (uint32_t)s}, p.key0, p.key1);
+      const int slot = reservoir_slot(rc, d);
+      if (slot >= 0)
+        my_res[(uint32_t)slot] =
+            make_uint3((uint32_t)(etc - eta), (uint32_t)(etc - (eta > prev ? eta : prev)),
+                       base_ms + (base_rem + (uint32_t)etc) / 1000u);
+      prev = etc;
+      rc = count_inc(rc);
+      if (++i >= V.cnt) break;
+      int2 e;
+      if (i < WL) {
+        e = *wslot((V.lh + i) & (WL - 1));
+      } else {  // rare: beyond the window
+        int pos = V.head + i;
+        pos = pos >= Q ? pos - Q : pos;
+        e = my_ring[(uint32_t)pos];
+      }
+      etc = e.x;
+      eta = e.y;
+      if (etc > dt) break;
+    }
+    V.rcnt = rc;
+  }
+
+  // ---- 2. one arrival per iteration (as dynamics_kernel's sim_step), the group in step
+  for (;;) {
+    const bool arrival_due = E.next_arr < dt;  // the same in every lane of the group
+    const int32_t th = arrival_due ? E.next_arr : dt;
+    const bool due = V.act && V.cnt > 0 && V.head_tc <= th;
+    if (due && V.cnt > WL) {  // rare: the slot the pop frees takes queue entry WL from the ring
+      int pw = V.head + WL;
+      pw = pw >= Q ? pw - Q : pw;
+      *wslot(V.lh) = my_ring[(uint32_t)pw];
+      __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+    }
+    const int nl = (V.lh + 1) & (WL - 1);
+    const int32_t nt = wslot(nl)->x;  // next head (valid if cnt > 1)
+    V.last = due ? V.head_tc : V.last;
+    V.cnt -= due ? 1 : 0;
+    V.head = due ? ((V.head + 1 == Q) ? 0 : V.head + 1) : V.head;
+    V.lh = due ? nl : V.lh;
+    V.head_tc = due ? nt : V.head_tc;
+    const bool more = group_bits<G>(__ballot(due && V.cnt > 0 && nt <= th), gbase) != 0u;
+    if (!arrival_due && !more) break;  // group-uniform
+    const bool arr = arrival_due && !more;
+
+    // ---- the arrival: choose a server (node.c:388-441); full servers are not eligible
     const int32_t ta = E.next_arr;
+    if constexpr (!alias) {
+      if constexpr (lsq) {
+        V.score = (float)V.cnt;
+      } else {  // (cnt + 1) / den correctly rounded (Markstein), division for den 0 / inf / NaN
+        const double c = (double)(V.cnt + 1);
+        const double q0 = c * V.rcp;
+        double q = fma(fma(-q0, V.den, c), V.rcp, q0);
+        if (q != q) {
+          asm volatile("");
+          q = c / V.den;
+        }
+        V.score = (float)q;
+      }
+    }
+    const bool elig = V.act && V.cnt < Q;
     const uint32_t em = group_bits<G>(__ballot(elig), gbase);
     int chosen = -1;
     if constexpr (alias) {
@@ -160,6 +218,8 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
       const bool ok1 = (em >> h1) & 1u, ok2 = (em >> h2) & 1u;
       chosen = (ok1 && ok2) ? ((s2 < s1) ? h2 : h1) : (ok1 ? h1 : (ok2 ? h2 : -1));
     } else {
+      const bool num = elig && V.score == V.score;
+      const float m = key_f32(group_min_i32<G>(num ? f32_key(V.score) : 0x7f800000));
       const int h = (int)__umulhi(E.u2, (uint32_t)S);
       const int c0 = ((em >> h) & 1u) ? h : (em ? __builtin_ctz(em) : -1);
       const uint32_t tie = group_bits<G>(__ballot(num && V.score == m), gbase);
@@ -168,77 +228,43 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
     }
     const bool push = arr && chosen >= 0;
     E.dropped += (arr && chosen < 0) ? 1u : 0u;
-    const int cs = comp ? smin : (push ? chosen : -1);
-    const bool mine = s == cs;
+    const bool mine = push && s == chosen;
 
-    // ---- the event's Philox block: this lane's reservoir draw, or the next arrival's draw
-    const u32x4 ctr = comp
-        ? u32x4{V.rcnt >> 1, E.gid, E.episode, (kStreamReservoir << 24) | (uint32_t)s}
-        : u32x4{E.arr_idx + 1u, E.gid, E.episode, kStreamArrival << 24};
-    const u32x4 d = philox4x32_10(ctr, p.key0, p.key1);
-
-    // ---- completion (lbhash.h:116-124, 131-135) + Algorithm R (reservoir.py:64-85)
-    const int32_t tc = tmin;
-    const int32_t h_ta = wslot(V.lh)->y;
-    const int32_t start_c = h_ta > V.last ? h_ta : V.last;
-    const int h_next = (V.head + 1 == Q) ? 0 : V.head + 1;
-    const int lh_next = (V.lh + 1 == WL) ? 0 : V.lh + 1;
-    int slot;
-    {
-      const uint32_t cres = V.rcnt;
-      const uint32_t hi = (cres & 1u) ? d.w : d.y;
-      const uint32_t lo = (cres & 1u) ? d.z : d.x;
-      const uint64_t j = mulhi64_by_u33(hi, lo, (uint64_t)cres + 1u);
-      slot = cres < (uint32_t)K ? (int)cres : (j < (uint64_t)K ? (int)j : -1);
-    }
-    if (comp && mine && slot >= 0) {
-      st.res[sb * (uint32_t)K + (uint32_t)slot] =
-          make_uint3((uint32_t)(tc - h_ta), (uint32_t)(tc - start_c),
-                     base_ms + (base_rem + (uint32_t)tc) / 1000u);
-    }
-    if (comp && mine && V.cnt - 1 >= WL) {  // rare: refill window entry WL-1 from the ring
-      int pw = h_next + WL - 1;
-      pw = pw >= Q ? pw - Q : pw;
-      *wslot(V.lh) = st.ring[sb * (uint32_t)Q + (uint32_t)pw];
-      __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
-    }
-    const int32_t nxt_tc = wslot(lh_next)->x;
-
-    // ---- arrival: FIFO service starts when the server's last queued flow ends
+    // ---- FIFO service on the chosen server (its lane)
     const int32_t start_a = V.cnt > 0 ? (V.tail > ta ? V.tail : ta) : ta;
     int32_t svc = (int32_t)(E.next_work * V.scale);
     svc = svc < 1 ? 1 : svc;
     const int32_t tc_a = start_a + svc;
-    if (push && mine) {
+    const bool ins = mine && tc_a <= dt;  // completes in this step: its sample now
+
+    // ---- one Philox block per lane: the chosen lane draws its reservoir block, the others the
+    //      next arrival's, which the group then reads from a lane that is not the chosen one
+    const u32x4 d = philox4x32_10(
+        mine ? u32x4{V.rcnt >> 1, E.gid, E.episode, (kStreamReservoir << 24) | (uint32_t)s}
+             : u32x4{E.arr_idx + 1u, E.gid, E.episode, kStreamArrival << 24},
+        p.key0, p.key1);
+    const int src = gbase + (chosen == 0 ? 1 : 0);  // never the chosen lane (G >= 2)
+    const u32x4 da = u32x4{(uint32_t)__shfl((int)d.x, src, 64), (uint32_t)__shfl((int)d.y, src, 64),
+                           (uint32_t)__shfl((int)d.z, src, 64), (uint32_t)__shfl((int)d.w, src, 64)};
+    const int slot = reservoir_slot(V.rcnt, d);
+    if (ins && slot >= 0)
+      my_res[(uint32_t)slot] = make_uint3((uint32_t)(tc_a - ta), (uint32_t)svc,
+                                          base_ms + (base_rem + (uint32_t)tc_a) / 1000u);
+    if (mine) {
       const int2 e = make_int2(tc_a, ta);
       if (V.cnt < WL) {
-        int li = V.lh + V.cnt;
-        li = li >= WL ? li - WL : li;
-        *wslot(li) = e;
+        *wslot((V.lh + V.cnt) & (WL - 1)) = e;
       } else {
         int pos = V.head + V.cnt;
         pos = pos >= Q ? pos - Q : pos;
-        st.ring[sb * (uint32_t)Q + (uint32_t)pos] = e;
+        my_ring[(uint32_t)pos] = e;
         asm volatile("");  // no flat store (see dynamics_kernel)
       }
-    }
-
-    // ---- write back the changed server (the owning lane)
-    if (mine) {
-      const int32_t n_cs = comp ? V.cnt - 1 : V.cnt + 1;
-      if (comp) {
-        V.rcnt = V.rcnt != 0xFFFFFFFFu ? V.rcnt + 1u : V.rcnt;
-        V.last = tc;
-        V.head = h_next;
-        V.lh = lh_next;
-        V.head_tc = nxt_tc;
-      } else {
-        V.tail = tc_a;
-        V.assigned += 1;
-        V.head_tc = V.cnt == 0 ? tc_a : V.head_tc;
-      }
-      V.cnt = n_cs;
-      V.score = policy_score_r(POLICY, n_cs, V.den, V.rcp);
+      V.tail = tc_a;
+      V.assigned += 1;
+      V.head_tc = V.cnt == 0 ? tc_a : V.head_tc;
+      V.cnt += 1;
+      V.rcnt = ins ? count_inc(V.rcnt) : V.rcnt;
     }
 
     // ---- next arrival (identical in every lane of the group)
@@ -248,15 +274,15 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
     if constexpr (TRACE) {
       na = ta + E.pf_gap;
       nw = E.pf_work;
-      nu2 = d.z;
-      nu3 = d.w;
+      nu2 = da.z;
+      nu3 = da.w;
       if (arr) {
         E.row = (E.row + 1u == p.trace_rows) ? 0u : E.row + 1u;
         E.pf_gap = (int32_t)st.trace_gap[E.row];
         E.pf_work = st.trace_work[E.row];
       }
     } else {
-      arrival_from_draw(p, d, ta, na, nw, nu2, nu3);
+      arrival_from_draw(p, da, ta, na, nw, nu2, nu3);
     }
     E.next_arr = arr ? na : E.next_arr;
     E.next_work = arr ? nw : E.next_work;
@@ -269,19 +295,17 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
   E.next_arr -= dt;
   if (V.act) {
     for (int i = 0; i < WL && i < V.cnt; ++i) {
-      int li = V.lh + i;
-      li = li >= WL ? li - WL : li;
-      int2* e = wslot(li);
+      int2* e = wslot((V.lh + i) & (WL - 1));
       e->x -= dt;
       e->y -= dt;
     }
     int pos = V.head + WL;
     if (pos >= Q) pos -= Q;
     for (int i = WL; i < V.cnt; ++i) {
-      int2 e = st.ring[sb * (uint32_t)Q + (uint32_t)pos];
+      int2 e = my_ring[(uint32_t)pos];
       e.x -= dt;
       e.y -= dt;
-      st.ring[sb * (uint32_t)Q + (uint32_t)pos] = e;
+      my_ring[(uint32_t)pos] = e;
       pos = (pos + 1 == Q) ? 0 : pos + 1;
     }
     V.head_tc -= dt;
