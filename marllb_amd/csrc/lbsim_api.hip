@@ -259,12 +259,14 @@ void launch_dyn_policy(lbsim_t* h, bool g, const void* action, int dtype, int32_
   }
 }
 
-// Mapping choice (LBSIM_DYN_AUTO): one lane per env while that gives at least half as many waves
-// as the device has SIMDs; below, one lane per server.
+// Mapping choice (LBSIM_DYN_AUTO): one lane per env when that fills every SIMD with at least one
+// wave and an env has at most 4 servers; otherwise one lane per server.  Measured
+// (profiles/r01s2e_group/mapping_sweep.txt): server-per-lane wins up to 32768 x 4 and at S = 16,
+// ties at 65536 x 8 and loses at 65536 x 4 (0.296 vs 0.256 ms).
 bool server_per_lane(const lbsim_t* h) {
   if (h->cfg.dyn_mapping == LBSIM_DYN_ENV_PER_LANE) return false;
   if (h->cfg.dyn_mapping == LBSIM_DYN_SERVER_PER_LANE) return true;
-  return (int64_t)(h->B + 63) / 64 < (int64_t)h->simds / 2;
+  return h->S > 4 || (int64_t)(h->B + 63) / 64 < (int64_t)h->simds;
 }
 
 template <int MODE>
