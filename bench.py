@@ -46,6 +46,27 @@ def algorithmic_bytes(S: int, flows_per_step: float):
     return {"observe_kernel": obs, "dynamics_kernel": dyn}
 
 
+MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32, dense
+
+
+def policy_flops(workload: str, S: int) -> float:
+    """Algorithmic FLOPs per env-step of the fused policy kernel (multiply-adds x 2, unpadded).
+
+    sac-gru: GRU (S*11 -> 128: three gates over input and hidden), fc1 128 -> 256, heads
+             256 -> 2S (networks.py:19-146).
+    qmix:    4 agents x [GRU (4k + 7S -> 64), fc1 64 -> 128, fc2 128 -> 128, fc3 128 -> 3]
+             + mixer (state 4S + 10: four 64/32-wide first layers, 64 -> 128, 64 -> 32, 64 -> 1).
+    """
+    if workload == "sac-gru":
+        i, h, f, a = S * 11, 128, 256, S
+        return 2.0 * (i * 3 * h + h * 3 * h + h * f + f * 2 * a)
+    k, ds = S // 4, 4 * S + 10
+    obs = 4 * k + 7 * S
+    agent = 2.0 * (obs * 192 + 64 * 192 + 64 * 128 + 128 * 128 + 128 * 3)
+    mixer = 2.0 * (ds * (3 * 64 + 32) + 64 * 128 + 64 * 32 + 64 * 1)
+    return 4 * agent + mixer
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -184,6 +205,9 @@ def main():
     if world > 1:
         dist.barrier()
     lib = _lib.load()
+    from marllb_amd import policies
+    if args.workload != "rollout":  # HIP events around each fused policy launch
+        policies.profile_events = []
     handle.check(lib.lbsim_profile_begin(handle.h, 4 * args.steps + 8))
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -195,6 +219,7 @@ def main():
     ms = (ctypes.c_double * 4)()
     cnt = (ctypes.c_int64 * 4)()
     handle.check(lib.lbsim_profile_end(handle.h, ms, cnt))
+    pol_events, policies.profile_events = policies.profile_events, None
     elapsed = lbdist.max_over_ranks(t1 - t0, dev if backend == "nccl" else None)
 
     if rank == 0:
@@ -252,6 +277,16 @@ def main():
             out["data"] = out["data"].replace("random discrete policy",
                                               "random-init network policy")
             out["policy_ms_per_step"] = out["ms_per_step"] - sum(avg.values())
+            out["config"]["fused_policy_tile"] = os.environ.get("LBSIM_FUSED_MT", "auto")
+            if pol_events:
+                pms = sum(a.elapsed_time(b) for a, b in pol_events) / len(pol_events)
+                fl = policy_flops(args.workload, S) * B
+                tf = fl / (pms * 1e-3) / 1e12
+                name = {"sac-gru": "sac_actor_kernel", "qmix": "qmix_policy_kernel"}[args.workload]
+                out["roofline"]["kernels"][name] = {
+                    "bound": "mfma", "avg_launch_ms": pms, "flops_per_launch": fl,
+                    "achieved_TFLOPs": tf, "peak_TFLOPs": MFMA_F32_PEAK_TFLOPS,
+                    "frac": tf / MFMA_F32_PEAK_TFLOPS}
         if world == 1 and not args.no_cpu_baseline and args.workload == "rollout":
             out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
         print(json.dumps(out), flush=True)

@@ -229,6 +229,75 @@ int lbsim_qmix_tail(const float* q, const float* w1, int64_t w1_ld, const float*
                     int64_t b1_ld, const float* w2, int64_t w2_ld, const float* b2, int64_t b2_ld,
                     int64_t B, int A, int E, float* q_tot, void* stream);
 
+/* ---- one-kernel policy inference (marllb_amd/csrc/lbsim_fused.h) ----
+ * The whole network of a tile of envs per workgroup on v_mfma_f32_16x16x4_f32, activations in LDS,
+ * one launch per step.  Weights are device pointers packed once by marllb_amd/policies.py
+ * `pack_linear`: a Linear weight W [N, K] zero-padded to [16 ceil(N/16), 16 ceil(K/16)] and stored
+ * in MFMA-fragment order P[nt][kb][lane 0..63][4] = W[16 nt + (lane & 15)][16 kb + 4 (lane >> 4)
+ * + s]; biases zero-padded to the padded N.  Layer widths other than the reference defaults return
+ * LBSIM_ENOTSUP (callers then use the GEMM + epilogue entry points above). */
+typedef struct lbsim_sac_actor { /* problem-04 PolicyNetwork (networks.py:19-146)             */
+  int32_t state_dim;             /* S * 11, <= 512                                            */
+  int32_t gru_dim;               /* 128 (networks.py default)                                 */
+  int32_t hidden_dim;            /* 256                                                       */
+  int32_t action_dim;            /* A <= 16                                                   */
+  const float* w_ih;             /* gru.weight_ih_l0 [3 gru, state_dim] packed (gates r, z, n) */
+  const float* w_hh;             /* gru.weight_hh_l0 [3 gru, gru] packed                      */
+  const float* b_ih;             /* [3 gru]                                                   */
+  const float* b_hh;             /* [3 gru]                                                   */
+  const float* w1;               /* fc1 [hidden, gru] packed                                  */
+  const float* b1;               /* [hidden]                                                  */
+  const float* wh;               /* [fc_mean; fc_logstd] [2 A, hidden] packed                 */
+  const float* bh;               /* [2 A], zero-padded to a multiple of 16                    */
+  float log_std_min, log_std_max; /* clamp (networks.py:93)                                   */
+  float action_scale, action_bias;
+} lbsim_sac_actor_t;
+size_t lbsim_sac_actor_size(void);
+
+/* PolicyNetwork.sample (networks.py:113-146) of B envs in one launch: state [B, state_dim];
+ * hidden [B, gru] updated IN PLACE, rows whose reset_mask byte is set starting from zeros
+ * (init_hidden at an episode start; reset_mask may be NULL); action_out [B, A] = tanh(x) * scale +
+ * bias, x = mean (deterministic) or mean + exp(clamped log_std) eps with eps ~ N(0,1) drawn from
+ * Philox exactly as lbsim_sac_head; log_std_out [B, A] optional. */
+int lbsim_sac_actor_step(const lbsim_sac_actor_t* net, const float* state, float* hidden,
+                         const uint8_t* reset_mask, int64_t B, int deterministic, uint64_t seed,
+                         uint32_t step, float* action_out, float* log_std_out, void* stream);
+
+typedef struct lbsim_qmix_policy { /* problem-05 QMIXAgent agents + QMixingNetwork            */
+  int32_t num_agents;            /* A <= 16                                                   */
+  int32_t obs_dim;               /* per-agent observation (128 at 4 x 4), <= 512              */
+  int32_t gru_dim;               /* 64 (agent_network.py default)                             */
+  int32_t hidden_dim;            /* 128                                                       */
+  int32_t n_actions;             /* <= 16                                                     */
+  int32_t state_dim;             /* global state (74 at 4 x 4), <= 512                        */
+  int32_t mixing_embed_dim;      /* E = 32 (mixing_network.py default)                        */
+  int32_t hypernet_embed_dim;    /* 64                                                        */
+  int32_t servers_per_agent;     /* k: server_actions_out repeats each agent's action k times */
+  float epsilon;                 /* exploration rate (qmix_agent.py:153)                      */
+  /* agent networks, A copies stacked agent-major (packed / padded as above) */
+  const float *w_ih, *w_hh, *b_ih, *b_hh; /* GRU [3 gru, obs_dim], [3 gru, gru]; [3 gru]      */
+  const float *w1, *b1, *w2, *b2;         /* fc1 [hidden, gru], fc2 [hidden, hidden]           */
+  const float *w3, *b3;                   /* fc3 [n_actions padded to 16, hidden]; [16]        */
+  /* mixer: m0 = the first layers stacked [hyper_w1[0]; hyper_w2[0]; hyper_b2[0]; hyper_b1[0]]
+   * [3 he + E, state_dim]; then hyper_w1[2] [A E, he], hyper_w2[2] [E, he], hyper_b2[2] [1, he]
+   * (rows padded to 16) with their biases */
+  const float *m0, *mb0, *mw1, *mbw1, *mw2, *mbw2, *mb2, *mbb2;
+} lbsim_qmix_policy_t;
+size_t lbsim_qmix_policy_size(void);
+
+/* QMIXAgent.select_actions (qmix_agent.py:138-178) for every agent + QMixingNetwork.forward
+ * (mixing_network.py:78-117) of B envs in one launch: obs [B, A, obs_dim]; hidden [B, A, gru]
+ * updated in place (reset_mask as above); state [B, state_dim]; per agent the greedy action
+ * (first maximum, as torch.argmax) or, with probability epsilon, a uniform one, drawn from Philox
+ * (key = seed, counter = (env, step, agent, 4 << 24)); actions_out [B, A] int64,
+ * server_actions_out [B, A k] int32 or NULL, q_out [B, A, n_actions] or NULL, q_chosen_out
+ * [B, A] or NULL, q_tot_out [B] = the mixer on the chosen Q-values. */
+int lbsim_qmix_policy_step(const lbsim_qmix_policy_t* net, const float* obs, float* hidden,
+                           const uint8_t* reset_mask, const float* state, int64_t B,
+                           uint64_t seed, uint32_t step, int64_t* actions_out,
+                           int32_t* server_actions_out, float* q_out, float* q_chosen_out,
+                           float* q_tot_out, void* stream);
+
 /* Arrival trace for arrival_source == TRACE (the TRACE counterpart of the Poisson draw in
  * env.py's simulation; rows of replay_fork_io.py:95-121's `time<TAB>query` CSV): gap_us[rows]
  * (us since the previous row; row 0: the wrap-around gap) and work[rows] (service demand in mean-1

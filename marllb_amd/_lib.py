@@ -71,6 +71,31 @@ class StepOutputs(ctypes.Structure):
     ]
 
 
+_SAC_WEIGHTS = ("w_ih", "w_hh", "b_ih", "b_hh", "w1", "b1", "wh", "bh")
+_QMIX_WEIGHTS = ("w_ih", "w_hh", "b_ih", "b_hh", "w1", "b1", "w2", "b2", "w3", "b3",
+                 "m0", "mb0", "mw1", "mbw1", "mw2", "mbw2", "mb2", "mbb2")
+
+
+class SacActor(ctypes.Structure):
+    """Mirror of lbsim_sac_actor_t (include/lbsim.h); weight fields are device pointers."""
+
+    _fields_ = ([("state_dim", ctypes.c_int32), ("gru_dim", ctypes.c_int32),
+                 ("hidden_dim", ctypes.c_int32), ("action_dim", ctypes.c_int32)]
+                + [(n, ctypes.c_void_p) for n in _SAC_WEIGHTS]
+                + [("log_std_min", ctypes.c_float), ("log_std_max", ctypes.c_float),
+                   ("action_scale", ctypes.c_float), ("action_bias", ctypes.c_float)])
+
+
+class QmixPolicy(ctypes.Structure):
+    """Mirror of lbsim_qmix_policy_t (include/lbsim.h); weight fields are device pointers."""
+
+    _fields_ = ([(n, ctypes.c_int32) for n in ("num_agents", "obs_dim", "gru_dim", "hidden_dim",
+                                               "n_actions", "state_dim", "mixing_embed_dim",
+                                               "hypernet_embed_dim", "servers_per_agent")]
+                + [("epsilon", ctypes.c_float)]
+                + [(n, ctypes.c_void_p) for n in _QMIX_WEIGHTS])
+
+
 class LbsimError(RuntimeError):
     """A liblbsim call returned a negative status."""
 
@@ -105,6 +130,14 @@ _SIGNATURES = {
     "lbsim_qmix_tail": (ctypes.c_int, [_P, _P, ctypes.c_int64, _P, ctypes.c_int64, _P,
                                        ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64,
                                        ctypes.c_int, ctypes.c_int, _P, _P]),
+    "lbsim_sac_actor_size": (ctypes.c_size_t, []),
+    "lbsim_qmix_policy_size": (ctypes.c_size_t, []),
+    "lbsim_sac_actor_step": (ctypes.c_int, [ctypes.POINTER(SacActor), _P, _P, _P, ctypes.c_int64,
+                                            ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, _P,
+                                            _P, _P]),
+    "lbsim_qmix_policy_step": (ctypes.c_int, [ctypes.POINTER(QmixPolicy), _P, _P, _P, _P,
+                                              ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint32,
+                                              _P, _P, _P, _P, _P, _P]),
     "lbsim_agent_obs": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, _P, _P]),
     "lbsim_set_trace": (ctypes.c_int, [_P, _P, _P, ctypes.c_int64, _P]),

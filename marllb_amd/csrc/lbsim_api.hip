@@ -5,9 +5,11 @@
 // happens inside lbsim_reset / lbsim_step, so a caller may capture them into a hipGraph.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -15,6 +17,7 @@
 #include "../../include/lbsim.h"
 #include "lbsim_kernels.h"
 #include "lbsim_dyn_group.h"
+#include "lbsim_fused.h"
 #include "lbsim_nets.h"
 
 using namespace lbk;
@@ -305,6 +308,36 @@ int launch_observe(lbsim_t* h, const ObsOutputs& o, const uint8_t* mask, int mod
   return launch_check(h, "observe_kernel");
 }
 
+// ---- one-kernel policy inference (lbsim_fused.h)
+
+// LDS row stride of the fused kernels: >= need floats and = 4 (mod 64), so the 16 rows one
+// ds_read_b128 touches fall in distinct banks.
+int fused_ld(int need) { return ((need - 4 + 63) / 64) * 64 + 4; }
+int round16(int x) { return (x + 15) / 16 * 16; }
+constexpr size_t kFusedLdsMax = 160 * 1024;
+
+// Envs per workgroup = 16 MT.  MT = 1 measured best for both kernels (profiles/r01s3a: SAC-GRU
+// 65536 x 8 0.231 / 0.267 / 0.352 ms at MT = 1 / 2 / 4 -- the MT = 4 tile needs 290 VGPRs, one
+// wave per SIMD; QMIX 8192 x 16 0.121 / 0.157 / 0.251 ms).  LBSIM_FUSED_MT = 1 | 2 | 4 forces it.
+int fused_mt(int64_t) {
+  static const int forced = [] {
+    const char* s = std::getenv("LBSIM_FUSED_MT");
+    return s ? std::atoi(s) : 0;
+  }();
+  return (forced == 2 || forced == 4) ? forced : 1;
+}
+
+template <typename Args>
+int launch_fused(void (*kern)(Args), int64_t B, int mt, size_t lds, hipStream_t s, Args a) {
+  const void* f = reinterpret_cast<const void*>(kern);
+  if (lds > 65536 &&
+      hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return LBSIM_EDEVICE;
+  void* args[] = {&a};
+  const dim3 grid((unsigned)((B + 16 * mt - 1) / (16 * mt))), block(256);
+  return hipLaunchKernel(f, grid, block, args, lds, s) == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
+}
+
 }  // namespace
 
 extern "C" {
@@ -575,6 +608,134 @@ int lbsim_qmix_tail(const float* q, const float* w1, int64_t w1_ld, const float*
                      (hipStream_t)stream, q, w1, w1_ld, b1, b1_ld, w2, w2_ld, b2, b2_ld, B, A, E,
                      q_tot);
   return hipGetLastError() == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
+}
+
+size_t lbsim_sac_actor_size(void) { return sizeof(lbsim_sac_actor_t); }
+size_t lbsim_qmix_policy_size(void) { return sizeof(lbsim_qmix_policy_t); }
+
+int lbsim_sac_actor_step(const lbsim_sac_actor_t* n, const float* state, float* hidden,
+                         const uint8_t* reset_mask, int64_t B, int deterministic, uint64_t seed,
+                         uint32_t step, float* action_out, float* log_std_out, void* stream) {
+  if (n == nullptr || B < 0 || n->state_dim < 1 || n->state_dim > 512 || n->action_dim < 1 ||
+      n->action_dim > 16)
+    return LBSIM_EINVAL;
+  if (n->gru_dim != 128 || n->hidden_dim != 256) return LBSIM_ENOTSUP;
+  if (B == 0) return LBSIM_OK;
+  if (!state || !hidden || !action_out || !n->w_ih || !n->w_hh || !n->b_ih || !n->b_hh ||
+      !n->w1 || !n->b1 || !n->wh || !n->bh)
+    return LBSIM_EINVAL;
+  SacActorArgs a{};
+  a.state = state;
+  a.hidden = hidden;
+  a.reset = reset_mask;
+  a.w_ih = n->w_ih;
+  a.w_hh = n->w_hh;
+  a.b_ih = n->b_ih;
+  a.b_hh = n->b_hh;
+  a.w1 = n->w1;
+  a.b1 = n->b1;
+  a.wh = n->wh;
+  a.bh = n->bh;
+  a.action = action_out;
+  a.log_std = log_std_out;
+  a.B = B;
+  a.I = n->state_dim;
+  a.kxp = round16(n->state_dim);
+  a.ld = fused_ld(std::max(a.kxp + 128, 256));
+  a.A = n->action_dim;
+  a.lo = n->log_std_min;
+  a.hi = n->log_std_max;
+  a.scale = n->action_scale;
+  a.bias = n->action_bias;
+  a.deterministic = deterministic;
+  a.key0 = (uint32_t)(seed & 0xFFFFFFFFull);
+  a.key1 = (uint32_t)(seed >> 32);
+  a.step = step;
+  int mt = fused_mt(B);
+  // the [R][ld] tile + split-K scratch of the heads ([4][2][R][16])
+  auto lds_of = [&](int m) { return (size_t)16 * m * (a.ld + 128) * 4; };
+  while (mt > 1 && lds_of(mt) > kFusedLdsMax) mt >>= 1;
+  const size_t lds = lds_of(mt);
+  const hipStream_t s = (hipStream_t)stream;
+  if (mt == 4) return launch_fused(&sac_actor_kernel<4, 128, 256>, B, 4, lds, s, a);
+  if (mt == 2) return launch_fused(&sac_actor_kernel<2, 128, 256>, B, 2, lds, s, a);
+  return launch_fused(&sac_actor_kernel<1, 128, 256>, B, 1, lds, s, a);
+}
+
+int lbsim_qmix_policy_step(const lbsim_qmix_policy_t* n, const float* obs, float* hidden,
+                           const uint8_t* reset_mask, const float* state, int64_t B,
+                           uint64_t seed, uint32_t step, int64_t* actions_out,
+                           int32_t* server_actions_out, float* q_out, float* q_chosen_out,
+                           float* q_tot_out, void* stream) {
+  if (n == nullptr || B < 0) return LBSIM_EINVAL;
+  const int A = n->num_agents, E = n->mixing_embed_dim, he = n->hypernet_embed_dim;
+  if (A < 1 || A > 16 || n->obs_dim < 1 || n->obs_dim > 512 || n->state_dim < 1 ||
+      n->state_dim > 512 || n->n_actions < 1 || n->n_actions > 16 || n->servers_per_agent < 1 ||
+      !(n->epsilon >= 0.0f && n->epsilon <= 1.0f))
+    return LBSIM_EINVAL;
+  // layer widths the kernel is built for; the mixer's second-layer outputs [0, A E + E + 16)
+  // must not reach hyper_b1's columns [3 he, 3 he + E) of the same LDS rows
+  if (n->gru_dim != 64 || n->hidden_dim != 128 || E < 16 || E % 16 != 0 || he < 16 ||
+      he % 16 != 0 || 3 * he + E > 256 || A * E / 16 + E / 16 + 1 > 16 || A * E + E + 16 > 3 * he)
+    return LBSIM_ENOTSUP;
+  if (B == 0) return LBSIM_OK;
+  if (!obs || !hidden || !state || !actions_out || !q_tot_out || !n->w_ih || !n->w_hh ||
+      !n->b_ih || !n->b_hh || !n->w1 || !n->b1 || !n->w2 || !n->b2 || !n->w3 || !n->b3 ||
+      !n->m0 || !n->mb0 || !n->mw1 || !n->mbw1 || !n->mw2 || !n->mbw2 || !n->mb2 || !n->mbb2)
+    return LBSIM_EINVAL;
+  QmixArgs a{};
+  a.obs = obs;
+  a.hidden = hidden;
+  a.reset = reset_mask;
+  a.state = state;
+  a.w_ih = n->w_ih;
+  a.w_hh = n->w_hh;
+  a.b_ih = n->b_ih;
+  a.b_hh = n->b_hh;
+  a.w1 = n->w1;
+  a.b1 = n->b1;
+  a.w2 = n->w2;
+  a.b2 = n->b2;
+  a.w3 = n->w3;
+  a.b3 = n->b3;
+  a.m0 = n->m0;
+  a.mb0 = n->mb0;
+  a.mw1 = n->mw1;
+  a.mbw1 = n->mbw1;
+  a.mw2 = n->mw2;
+  a.mbw2 = n->mbw2;
+  a.mb2 = n->mb2;
+  a.mbb2 = n->mbb2;
+  a.actions = actions_out;
+  a.server_actions = server_actions_out;
+  a.q_out = q_out;
+  a.q_chosen = q_chosen_out;
+  a.q_tot = q_tot_out;
+  a.B = B;
+  a.A = A;
+  a.I = n->obs_dim;
+  a.kxp = round16(n->obs_dim);
+  a.Ds = n->state_dim;
+  a.ksp = round16(n->state_dim);
+  a.ld = fused_ld(std::max({a.kxp + 64, 128, a.ksp, 3 * he + E}));
+  a.n_act = n->n_actions;
+  a.k = n->servers_per_agent;
+  a.he = he;
+  a.E = E;
+  a.epsilon = n->epsilon;
+  a.key0 = (uint32_t)(seed & 0xFFFFFFFFull);
+  a.key1 = (uint32_t)(seed >> 32);
+  a.step = step;
+  auto lds_of = [&](int mt) {
+    const size_t R = 16 * (size_t)mt;
+    return (R * a.ld + (size_t)A * R * 16 + R * A + 64 * R) * 4;  // + split-K scratch
+  };
+  int mt = fused_mt(B);
+  while (mt > 1 && lds_of(mt) > kFusedLdsMax) mt >>= 1;
+  const hipStream_t s = (hipStream_t)stream;
+  if (mt == 4) return launch_fused(&qmix_policy_kernel<4, 64, 128>, B, 4, lds_of(4), s, a);
+  if (mt == 2) return launch_fused(&qmix_policy_kernel<2, 64, 128>, B, 2, lds_of(2), s, a);
+  return launch_fused(&qmix_policy_kernel<1, 64, 128>, B, 1, lds_of(1), s, a);
 }
 
 int lbsim_alias_tables(const float* weights, int64_t n, int S, float* odd_out, int32_t* alias_out,

@@ -1,0 +1,512 @@
+// lbsim_fused.h — one-kernel policy inference for the policy-in-the-loop rollouts (SURVEY §8f
+// ranks 1-2, BASELINE configs[3] and configs[4]) on the f32-input MFMA of gfx950.
+//
+//   sac_actor_kernel   problem-04 PolicyNetwork.sample (networks.py:82-146): GRU(state -> H),
+//                      fc1 -> F + ReLU, [fc_mean | fc_logstd] -> 2A, clamp, Philox noise, tanh.
+//   qmix_policy_kernel problem-05 QMIXAgent.select_actions (qmix_agent.py:138-178) for all A agents
+//                      (AgentQNetwork agent_network.py:63-87: GRU(obs -> H), fc1/fc2 -> F + ReLU,
+//                      fc3 -> n_actions), epsilon-greedy, the chosen Q-values, then QMixingNetwork
+//                      (mixing_network.py:78-117) on the global state -> Q_tot.
+//
+// One workgroup (4 waves) owns a tile of R = 16 MT envs for the whole network: activations never
+// leave LDS ([R][ld] f32, ld = 4 mod 64 so the MFMA operand reads are bank-conflict free), weights
+// stream from L2 in MFMA-fragment order, every GEMM is v_mfma_f32_16x16x4_f32 (exact f32 FMA
+// chain, the same numerics class as the fp32 hipBLASLt path it replaces: tested to 1e-5 against
+// the torch modules).  Per layer each wave accumulates its output tiles in registers, the
+// workgroup barriers, then writes the activated tile back over its input (so one LDS buffer serves
+// every layer).
+//
+// Packed weight layout (marllb_amd/policies.py `pack_linear`): a torch Linear weight W [N, K] is
+// zero-padded to [16 NT, 16 KB] and stored as P[nt][kb][lane][s] = W[16 nt + (lane & 15)]
+// [16 kb + 4 (lane >> 4) + s]: for k-step s of block kb, lane l feeds A[row l&15][k = l>>4] and
+// B[k = l>>4][col l&15] of the 16x16x4 MFMA with the same permuted k, so one 16-B load per lane
+// per block gives the B operands of four MFMAs and one ds_read_b128 per M-tile the A operands.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "lbsim_math.h"
+
+namespace lbk {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4 splat4(float v) { return f4{v, v, v, v}; }
+
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// acc[m] += X[rows 16m .. 16m+15, cols col0 .. col0 + 16 nkb) . W^T for one 16-column output tile
+// whose packed k-blocks start at wp.  Software-pipelined: B fragments two blocks ahead (L2
+// latency), A fragments one block ahead (LDS latency); the clamped tail re-reads the last block.
+template <int MT>
+__device__ __forceinline__ void mma_tile(f4 (&acc)[MT], const float* lds, int ld, int col0,
+                                         const f4* __restrict__ wp, int nkb, int lane) {
+  const float* arow = lds + (lane & 15) * ld + col0 + 4 * (lane >> 4);
+  f4 b0 = wp[lane];
+  f4 b1 = wp[(nkb > 1 ? 64 : 0) + lane];
+  f4 a[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) a[m] = *(const f4*)(arow + m * 16 * ld);
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int n2 = kb + 2 < nkb ? kb + 2 : nkb - 1;
+    const int n1 = kb + 1 < nkb ? kb + 1 : nkb - 1;
+    const f4 b2 = wp[n2 * 64 + lane];
+    f4 an[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) an[m] = *(const f4*)(arow + m * 16 * ld + n1 * 16);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][s], b0[s], acc[m], 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) a[m] = an[m];
+    b0 = b1;
+    b1 = b2;
+  }
+}
+
+// NB output tiles over the same input columns in one pipelined loop: the A fragments are read
+// once per block for all of them, and NB x MT independent accumulator chains keep the MFMA pipe
+// busy even at MT = 1 (a single chain waits out the 40-cycle dependent latency every MFMA).
+template <int MT, int NB>
+__device__ __forceinline__ void mma_multi(f4 (&acc)[NB][MT], const float* lds, int ld, int col0,
+                                          const f4* const (&wp)[NB], int nkb, int lane) {
+  const float* arow = lds + (lane & 15) * ld + col0 + 4 * (lane >> 4);
+  f4 b0[NB], b1[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    b0[j] = wp[j][lane];
+    b1[j] = wp[j][(nkb > 1 ? 64 : 0) + lane];
+  }
+  f4 a[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) a[m] = *(const f4*)(arow + m * 16 * ld);
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int n2 = kb + 2 < nkb ? kb + 2 : nkb - 1;
+    const int n1 = kb + 1 < nkb ? kb + 1 : nkb - 1;
+    f4 b2[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) b2[j] = wp[j][n2 * 64 + lane];
+    f4 an[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) an[m] = *(const f4*)(arow + m * 16 * ld + n1 * 16);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          acc[j][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][s], b0[j][s], acc[j][m], 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) a[m] = an[m];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      b0[j] = b1[j];
+      b1[j] = b2[j];
+    }
+  }
+}
+
+// Dense layer, accumulate phase: wave w owns output tiles nt = w, w + 4, ... < ntiles, all in
+// one mma_multi pass (a wave with fewer tiles recomputes the last one; dense_store skips it).
+template <int MT, int NTW>
+__device__ __forceinline__ void dense_acc(f4 (&acc)[NTW][MT], const float* lds, int ld, int col0,
+                                          const float* __restrict__ w, int nkb, int ntiles,
+                                          const float* __restrict__ bias, int wave, int lane) {
+  const f4* wp[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    const int nt = wave + 4 * j < ntiles ? wave + 4 * j : ntiles - 1;
+    wp[j] = (const f4*)w + (size_t)nt * nkb * 64;
+    const float bv = bias[nt * 16 + (lane & 15)];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[j][m] = splat4(bv);
+  }
+  mma_multi<MT, NTW>(acc, lds, ld, col0, wp, nkb, lane);
+}
+
+// A narrow output (<= 2 tiles: the SAC heads, the Q-values) with K split over the 4 waves: wave w
+// runs the k-blocks [w nkb / 4, (w + 1) nkb / 4) of every M-tile, the partial tiles meet in LDS
+// scratch ([4][nt][R][16]) and the workgroup sums them: dst[r * dld + c] = bias[c] + sum, c <
+// ncols.  Contains a barrier; the caller barriers again before reading dst.
+template <int MT>
+__device__ __forceinline__ void splitk_out(const float* lds, int ld, const float* __restrict__ w,
+                                           const float* __restrict__ bias, int nkb, int nt,
+                                           float* scratch, float* dst, int dld, int ncols,
+                                           int wave, int lane) {
+  constexpr int R = 16 * MT;
+  const int k0 = wave * nkb / 4, k1 = (wave + 1) * nkb / 4;
+  for (int t = 0; t < nt; ++t) {
+    f4 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = splat4(0.0f);
+    if (k1 > k0)
+      mma_tile<MT>(acc, lds, ld, k0 * 16, (const f4*)w + ((size_t)t * nkb + k0) * 64, k1 - k0,
+                   lane);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        scratch[((wave * nt + t) * R + m * 16 + 4 * (lane >> 4) + i) * 16 + (lane & 15)] =
+            acc[m][i];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < R * ncols; e += blockDim.x) {
+    const int r = e / ncols, c = e - r * ncols, t = c >> 4, cc = c & 15;
+    float v = bias[c];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v += scratch[((q * nt + t) * R + r) * 16 + cc];
+    dst[r * dld + c] = v;
+  }
+}
+
+// Dense layer, store phase (after a barrier): out[row][col0 + 16 nt + c] = act(acc, 16 nt + c).
+template <int MT, int NTW, class Act>
+__device__ __forceinline__ void dense_store(const f4 (&acc)[NTW][MT], float* lds, int ld, int col0,
+                                            int ntiles, int wave, int lane, Act act) {
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    const int nt = wave + 4 * j;
+    if (nt < ntiles) {
+      const int c = nt * 16 + (lane & 15);
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          lds[(m * 16 + 4 * (lane >> 4) + i) * ld + col0 + c] = act(acc[j][m][i], c);
+    }
+  }
+}
+
+// torch.nn.GRU cell over the tile (gate order r, z, n):
+//   r = sig(x W_ir + b_ir + h W_hr + b_hr), z likewise, n = tanh(x W_in + b_in + r (h W_hn + b_hn)),
+//   h' = (1 - z) n + z h,
+// with x in LDS cols [0, kxp) and h in [kxp, kxp + H).  Returns h' of the wave's unit tiles in
+// hn (wave w: unit tiles u = w, w + 4, ...); the caller barriers before overwriting h.
+template <int MT, int H>
+__device__ __forceinline__ void gru_tile(f4 (&hn)[(H / 16 + 3) / 4][MT], const float* lds, int ld,
+                                         int kxp, const float* __restrict__ w_ih,
+                                         const float* __restrict__ w_hh,
+                                         const float* __restrict__ b_ih,
+                                         const float* __restrict__ b_hh, int wave, int lane) {
+  constexpr int UT = H / 16, UTW = (UT + 3) / 4, KBH = H / 16;
+  const int kbx = kxp / 16;
+  const f4* wi = (const f4*)w_ih;
+  const f4* wh = (const f4*)w_hh;
+#pragma unroll
+  for (int j = 0; j < UTW; ++j) {
+    const int u = wave + 4 * j;
+    if (u >= UT) continue;
+    const int col = u * 16 + (lane & 15);
+    // g = {x W_in + b_in, r, z, h W_hn + b_hn}: the input part feeds g[0..2], the hidden part
+    // g[1..3], each in one mma_multi pass sharing its A fragments
+    f4 g[4][MT];
+    const float bg[4] = {b_ih[2 * H + col], b_ih[col] + b_hh[col], b_ih[H + col] + b_hh[H + col],
+                         b_hh[2 * H + col]};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) g[q][m] = splat4(bg[q]);
+    const f4* const wx[3] = {wi + (size_t)(2 * UT + u) * kbx * 64, wi + (size_t)u * kbx * 64,
+                             wi + (size_t)(UT + u) * kbx * 64};
+    const f4* const wy[3] = {wh + (size_t)u * KBH * 64, wh + (size_t)(UT + u) * KBH * 64,
+                             wh + (size_t)(2 * UT + u) * KBH * 64};
+    mma_multi<MT, 3>(*reinterpret_cast<f4(*)[3][MT]>(&g[0]), lds, ld, 0, wx, kbx, lane);
+    mma_multi<MT, 3>(*reinterpret_cast<f4(*)[3][MT]>(&g[1]), lds, ld, kxp, wy, KBH, lane);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float hp = lds[(m * 16 + 4 * (lane >> 4) + i) * ld + kxp + col];
+        const float r = sigmoid_f(g[1][m][i]);
+        const float z = sigmoid_f(g[2][m][i]);
+        const float n = tanhf(g[0][m][i] + r * g[3][m][i]);
+        hn[j][m][i] = (1.0f - z) * n + z * hp;
+      }
+  }
+}
+
+// Store h' into LDS cols [kxp, kxp + H) and to hidden[b, H] (row stride h_ld floats).
+template <int MT, int H>
+__device__ __forceinline__ void gru_store(const f4 (&hn)[(H / 16 + 3) / 4][MT], float* lds, int ld,
+                                          int kxp, float* hidden, int64_t h_ld, int64_t row0,
+                                          int64_t B, int wave, int lane) {
+  constexpr int UT = H / 16, UTW = (UT + 3) / 4;
+#pragma unroll
+  for (int j = 0; j < UTW; ++j) {
+    const int u = wave + 4 * j;
+    if (u >= UT) continue;
+    const int col = u * 16 + (lane & 15);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = m * 16 + 4 * (lane >> 4) + i;
+        lds[r * ld + kxp + col] = hn[j][m][i];
+        if (row0 + r < B) hidden[(row0 + r) * h_ld + col] = hn[j][m][i];
+      }
+  }
+}
+
+// Stage rows [row0, row0 + R) of a [B, n] matrix (row stride src_ld) into LDS cols [col0, col0 +
+// npad), zero past n, past B and (if reset_mask) for rows whose mask byte is set.
+__device__ __forceinline__ void stage_rows(float* lds, int ld, int col0, const float* src,
+                                           int64_t src_ld, int n, int npad, int R, int64_t row0,
+                                           int64_t B, const uint8_t* reset_mask) {
+  for (int e = threadIdx.x; e < R * npad; e += blockDim.x) {
+    const int r = e / npad, c = e - r * npad;
+    const int64_t b = row0 + r;
+    float v = 0.0f;
+    if (c < n && b < B && !(reset_mask && reset_mask[b])) v = src[b * src_ld + c];
+    lds[r * ld + col0 + c] = v;
+  }
+}
+
+struct ReluAct {
+  __device__ float operator()(float v, int) const { return v > 0.0f ? v : 0.0f; }
+};
+
+// ------------------------------------------------------------------------------ SAC-GRU actor
+struct SacActorArgs {
+  const float* state;     // [B, I]
+  float* hidden;          // [B, H], updated in place
+  const uint8_t* reset;   // [B] or null: rows whose hidden state starts from zero
+  const float *w_ih, *w_hh, *b_ih, *b_hh, *w1, *b1, *wh, *bh;
+  float* action;          // [B, A]
+  float* log_std;         // [B, A] or null
+  int64_t B;
+  int I, kxp, ld, A;
+  float lo, hi, scale, bias;
+  int deterministic;
+  uint32_t key0, key1, step;
+};
+
+template <int MT, int H, int F>
+__global__ void __launch_bounds__(256) sac_actor_kernel(SacActorArgs p) {
+  extern __shared__ float lds[];
+  constexpr int R = 16 * MT;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row0 = (int64_t)blockIdx.x * R;
+  const int ld = p.ld, kxp = p.kxp;
+  stage_rows(lds, ld, 0, p.state, p.I, p.I, kxp, R, row0, p.B, nullptr);
+  stage_rows(lds, ld, kxp, p.hidden, H, H, H, R, row0, p.B, p.reset);
+  __syncthreads();
+  {
+    f4 hn[(H / 16 + 3) / 4][MT];
+    gru_tile<MT, H>(hn, lds, ld, kxp, p.w_ih, p.w_hh, p.b_ih, p.b_hh, wave, lane);
+    __syncthreads();
+    gru_store<MT, H>(hn, lds, ld, kxp, p.hidden, H, row0, p.B, wave, lane);
+  }
+  __syncthreads();
+  {
+    constexpr int NT = F / 16, NTW = (NT + 3) / 4;
+    f4 acc[NTW][MT];
+    dense_acc<MT, NTW>(acc, lds, ld, kxp, p.w1, H / 16, NT, p.b1, wave, lane);
+    __syncthreads();
+    dense_store<MT, NTW>(acc, lds, ld, 0, NT, wave, lane, ReluAct{});
+  }
+  __syncthreads();
+  // heads [mean | log_std] (2A <= 32 columns), K split over the waves; y over the first 2A
+  // columns of the tile
+  splitk_out<MT>(lds, ld, p.wh, p.bh, F / 16, (2 * p.A + 15) / 16, lds + R * ld, lds, ld,
+                 2 * p.A, wave, lane);
+  __syncthreads();
+  const int A = p.A;
+  for (int e = threadIdx.x; e < R * A; e += blockDim.x) {
+    const int r = e / A, a = e - r * A;
+    const int64_t b = row0 + r;
+    if (b >= p.B) continue;
+    const float mean = lds[r * ld + a];
+    float ls = lds[r * ld + A + a];
+    ls = ls < p.lo ? p.lo : (ls > p.hi ? p.hi : ls);
+    float x = mean;
+    if (!p.deterministic) {  // the noise of sac_head_kernel (lbsim_nets.h), same counter
+      const u32x4 d = philox4x32_10(u32x4{(uint32_t)b, p.step, (uint32_t)a, 3u << 24}, p.key0,
+                                    p.key1);
+      const float u1 = u01_open0(d.x), u2 = (float)(d.y >> 8) * 5.9604644775390625e-8f;
+      const float eps = sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+      x = mean + expf(ls) * eps;
+    }
+    p.action[b * A + a] = tanhf(x) * p.scale + p.bias;
+    if (p.log_std) p.log_std[b * A + a] = ls;
+  }
+}
+
+// ------------------------------------------------------------------------------ QMIX policy
+struct QmixArgs {
+  const float* obs;       // [B, A, I]
+  float* hidden;          // [B, A, H], updated in place
+  const uint8_t* reset;   // [B] or null
+  const float* state;     // [B, Ds]
+  // agent networks, A stacked copies each: packed weights and padded biases
+  const float *w_ih, *w_hh, *b_ih, *b_hh, *w1, *b1, *w2, *b2, *w3, *b3;
+  // mixer: first layers [hyper_w1[0] | hyper_w2[0] | hyper_b2[0] | hyper_b1] (3 he + E rows),
+  // second layers hyper_w1[2] (A E x he), hyper_w2[2] (E x he), hyper_b2[2] (1 x he, padded)
+  const float *m0, *mb0, *mw1, *mbw1, *mw2, *mbw2, *mb2, *mbb2;
+  int64_t* actions;         // [B, A]
+  int32_t* server_actions;  // [B, A k] or null: each agent's action repeated for its k servers
+  float* q_out;             // [B, A, n_actions] or null
+  float* q_chosen;          // [B, A] or null
+  float* q_tot;             // [B]
+  int64_t B;
+  int A, I, kxp, Ds, ksp, ld, n_act, k, he, E;
+  float epsilon;
+  uint32_t key0, key1, step;
+};
+
+struct QmixMixAct {
+  int relu_cols;  // columns [0, relu_cols) are ReLU'd (the three hypernetwork hidden layers)
+  __device__ float operator()(float v, int c) const {
+    return c < relu_cols ? (v > 0.0f ? v : 0.0f) : v;
+  }
+};
+
+template <int MT, int H, int F>
+__global__ void __launch_bounds__(256) qmix_policy_kernel(QmixArgs p) {
+  extern __shared__ float lds[];
+  constexpr int R = 16 * MT;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row0 = (int64_t)blockIdx.x * R;
+  const int ld = p.ld, kxp = p.kxp, A = p.A, NQ = p.n_act;
+  float* qv = lds + R * ld;         // [A][R][16]
+  float* chosen = qv + A * R * 16;  // [R][A]
+  float* scratch = chosen + R * A;  // [4][R][16] split-K partials
+  const size_t s_ih = (size_t)3 * H * kxp, s_hh = (size_t)3 * H * H;
+  constexpr int NT = F / 16, NTW = (NT + 3) / 4;
+  for (int a = 0; a < A; ++a) {
+    stage_rows(lds, ld, 0, p.obs + (size_t)a * p.I, (int64_t)A * p.I, p.I, kxp, R, row0, p.B,
+               nullptr);
+    stage_rows(lds, ld, kxp, p.hidden + (size_t)a * H, (int64_t)A * H, H, H, R, row0, p.B,
+               p.reset);
+    __syncthreads();
+    {
+      f4 hn[(H / 16 + 3) / 4][MT];
+      gru_tile<MT, H>(hn, lds, ld, kxp, p.w_ih + a * s_ih, p.w_hh + a * s_hh,
+                      p.b_ih + a * 3 * H, p.b_hh + a * 3 * H, wave, lane);
+      __syncthreads();
+      gru_store<MT, H>(hn, lds, ld, kxp, p.hidden + (size_t)a * H, (int64_t)A * H, row0, p.B,
+                       wave, lane);
+    }
+    __syncthreads();
+    {
+      f4 acc[NTW][MT];
+      dense_acc<MT, NTW>(acc, lds, ld, kxp, p.w1 + (size_t)a * F * H, H / 16, NT, p.b1 + a * F,
+                         wave, lane);
+      __syncthreads();
+      dense_store<MT, NTW>(acc, lds, ld, 0, NT, wave, lane, ReluAct{});
+    }
+    __syncthreads();
+    {
+      f4 acc[NTW][MT];
+      dense_acc<MT, NTW>(acc, lds, ld, 0, p.w2 + (size_t)a * F * F, F / 16, NT, p.b2 + a * F,
+                         wave, lane);
+      __syncthreads();
+      dense_store<MT, NTW>(acc, lds, ld, 0, NT, wave, lane, ReluAct{});
+    }
+    __syncthreads();
+    // fc3 -> Q-values (n_actions <= 16: one output tile), K split over the waves
+    splitk_out<MT>(lds, ld, p.w3 + (size_t)a * 16 * F, p.b3 + a * 16, F / 16, 1, scratch,
+                   qv + a * R * 16, 16, 16, wave, lane);
+    __syncthreads();
+  }
+  // epsilon-greedy (qmix_agent.py:153-164): argmax (first maximum, as torch.argmax), explore with
+  // probability epsilon to a uniform action; Philox counter (row, step, agent, 4 << 24)
+  for (int e = threadIdx.x; e < R * A; e += blockDim.x) {
+    const int r = e / A, a = e - r * A;
+    const int64_t b = row0 + r;
+    const float* q = qv + (a * R + r) * 16;
+    int g = 0;
+    for (int j = 1; j < NQ; ++j)
+      if (q[j] > q[g]) g = j;
+    const u32x4 d = philox4x32_10(u32x4{(uint32_t)b, p.step, (uint32_t)a, 4u << 24}, p.key0,
+                                  p.key1);
+    const float u = (float)(d.x >> 8) * 5.9604644775390625e-8f;  // [0, 1)
+    const int act = u < p.epsilon ? (int)(((uint64_t)d.y * (uint32_t)NQ) >> 32) : g;
+    chosen[r * A + a] = q[act];
+    if (b < p.B) {
+      p.actions[b * A + a] = act;
+      if (p.server_actions)
+        for (int j = 0; j < p.k; ++j) p.server_actions[(b * A + a) * p.k + j] = act;
+      if (p.q_out)
+        for (int j = 0; j < NQ; ++j) p.q_out[(b * A + a) * NQ + j] = q[j];
+      if (p.q_chosen) p.q_chosen[b * A + a] = q[act];
+    }
+  }
+  // mixer (mixing_network.py:78-117) on the global state
+  stage_rows(lds, ld, 0, p.state, p.Ds, p.Ds, p.ksp, R, row0, p.B, nullptr);
+  __syncthreads();
+  const int he = p.he, E = p.E;
+  {
+    const int nt0 = (3 * he + E) / 16;  // <= 16
+    f4 acc[4][MT];
+    dense_acc<MT, 4>(acc, lds, ld, 0, p.m0, p.ksp / 16, nt0, p.mb0, wave, lane);
+    __syncthreads();
+    dense_store<MT, 4>(acc, lds, ld, 0, nt0, wave, lane, QmixMixAct{3 * he});
+  }
+  __syncthreads();
+  {
+    // second layers: w1 tiles (A E / 16) from cols [0, he), w2 tiles (E / 16) from [he, 2 he),
+    // b2 (one tile) from [2 he, 3 he); outputs to cols [0, A E), [A E, A E + E), A E + E
+    const int n1 = A * E / 16, n2 = E / 16, ntot = n1 + n2 + 1, kb = he / 16;
+    f4 acc[4][MT];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = wave + 4 * j;
+      if (t >= ntot) continue;
+      const float* w;
+      const float* bias;
+      int col0, tt;
+      if (t < n1) {
+        w = p.mw1, bias = p.mbw1, col0 = 0, tt = t;
+      } else if (t < n1 + n2) {
+        w = p.mw2, bias = p.mbw2, col0 = he, tt = t - n1;
+      } else {
+        w = p.mb2, bias = p.mbb2, col0 = 2 * he, tt = 0;
+      }
+      const float bv = bias[tt * 16 + (lane & 15)];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[j][m] = splat4(bv);
+      mma_tile<MT>(acc[j], lds, ld, col0, (const f4*)w + (size_t)tt * kb * 64, kb, lane);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = wave + 4 * j;
+      if (t >= ntot) continue;
+      const bool is_abs = t < n1 + n2;  // |W1|, |W2| (mixing_network.py:96,105)
+      const int c = t * 16 + (lane & 15);
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float v = acc[j][m][i];
+          lds[(m * 16 + 4 * (lane >> 4) + i) * ld + c] = is_abs ? fabsf(v) : v;
+        }
+    }
+  }
+  __syncthreads();
+  // tail: hidden_e = elu(b1_e + sum_a q_a |w1[a E + e]|), Q_tot = sum_e hidden_e |w2_e| + b2;
+  // 4 threads per row, E / 4 embedding units each, combined by shuffles (R * 4 is a multiple of
+  // 64, so every wave is either fully inside the loop or fully outside it)
+  const int b1c = 3 * he, w2c = A * E, b2c = A * E + E;
+  for (int e0 = threadIdx.x; e0 < R * 4; e0 += blockDim.x) {
+    const int r = e0 >> 2, part = e0 & 3;
+    const float* row = lds + r * ld;
+    float acc = 0.0f;
+    for (int u = part * (E / 4); u < (part + 1) * (E / 4); ++u) {
+      float h = 0.0f;
+      for (int a = 0; a < A; ++a) h += chosen[r * A + a] * row[a * E + u];
+      h += row[b1c + u];
+      h = h > 0.0f ? h : expm1f(h);
+      acc += h * row[w2c + u];
+    }
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    if (part == 0 && row0 + r < p.B) p.q_tot[row0 + r] = acc + row[b2c];
+  }
+}
+
+}  // namespace lbk

@@ -12,10 +12,13 @@ reference checkpoint's state_dict loads unchanged (`load_state_dict(torch.load(.
               global state give |W1| (A x 32), b1, |W2| (32), b2; Q_tot = elu(q W1 + b1) W2 + b2.
 
 These modules run on the GPU as torch fp32 (GEMMs through hipBLASLt); they are also the fp32
-reference for the fused inference kernel.  Rollout harnesses (marllb_amd/rollout.py) keep the GRU
+reference for the fused inference forms below (one MFMA kernel per step at the reference widths).  Rollout harnesses (marllb_amd/rollout.py) keep the GRU
 hidden state resident on the device and feed actions to lbsim_step without a host round trip.
 """
 from __future__ import annotations
+
+import ctypes
+from typing import Optional
 
 import torch
 import torch.nn as nn
@@ -137,22 +140,20 @@ def load_prefixed(module: nn.Module, arrays, prefix: str) -> nn.Module:
 
 
 # ---------------------------------------------------------------------------- fused inference
-# A step of a GRU + MLP network as hipBLASLt GEMMs (torch.addmm / baddbmm, ReLU as the GEMM
-# epilogue) with every elementwise stage in our HIP kernels (csrc/lbsim_nets.h): 5 launches per
-# step instead of MIOpen's generic RNN path.  Inference only (no autograd); the torch modules above
-# are the fp32 reference these are tested against.
+# Two forms.  One kernel per step (lbsim_sac_actor_step / lbsim_qmix_policy_step, csrc/lbsim_fused.h:
+# the whole network of a tile of envs on the f32 MFMA, activations in LDS) at the reference's
+# layer widths; otherwise hipBLASLt GEMMs (torch.addmm / baddbmm, ReLU as the GEMM epilogue) with
+# every elementwise stage in our HIP kernels (csrc/lbsim_nets.h).  Inference only (no autograd);
+# the torch modules above are the fp32 reference both are tested against.
 
 def _lib_and_stream(device):
-    import ctypes
-
     from . import _lib
     lib = _lib.load()
     return lib, ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
-def _ptr(t: torch.Tensor):
-    import ctypes
-    return ctypes.c_void_p(t.data_ptr())
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
 def _linear_relu(x, w, b):
@@ -163,10 +164,48 @@ def _linear_relu(x, w, b):
     return torch.relu_(torch.addmm(b, x, w.t()))
 
 
-class FusedGRUPolicy:
-    """GRUPolicy.forward + sample for inference on the GPU (networks.py:82-146)."""
+def pack_linear(w: torch.Tensor, n_pad: Optional[int] = None) -> torch.Tensor:
+    """A Linear weight [N, K] in the MFMA-fragment order of csrc/lbsim_fused.h: zero-padded to
+    [16 NT, 16 KB] (N to n_pad if given), P[nt][kb][l][s] = W[16 nt + (l & 15)][16 kb + 4 (l >> 4)
+    + s], flat float32."""
+    n, k = w.shape
+    npd = n_pad if n_pad is not None else -(-n // 16) * 16
+    kpd = -(-k // 16) * 16
+    p = torch.zeros(npd, kpd, dtype=torch.float32, device=w.device)
+    p[:n, :k] = w.detach()
+    return p.view(npd // 16, 16, kpd // 16, 4, 4).permute(0, 2, 3, 1, 4).contiguous().view(-1)
 
-    def __init__(self, policy: GRUPolicy, seed: int = 0):
+
+def _pad_vec(v: torch.Tensor, n: int) -> torch.Tensor:
+    out = torch.zeros(n, dtype=torch.float32, device=v.device)
+    out[:v.numel()] = v.detach().reshape(-1)
+    return out
+
+
+# bench.py sets this to a list to collect (start, end) CUDA events around each fused launch
+profile_events: Optional[list] = None
+
+
+def _timed(launch):
+    if profile_events is None:
+        return launch()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    rc = launch()
+    e1.record()
+    profile_events.append((e0, e1))
+    return rc
+
+
+class FusedGRUPolicy:
+    """GRUPolicy.forward + sample for inference on the GPU (networks.py:82-146).
+
+    kernel=True (default) and the reference widths (gru 128, hidden 256, action_dim <= 16): one
+    launch per step, lbsim_sac_actor_step; otherwise the GEMM form (hipBLASLt + lbsim_gru_gates +
+    lbsim_sac_head).  Both draw the exploration noise from the same Philox counters.
+    """
+
+    def __init__(self, policy: GRUPolicy, seed: int = 0, kernel: bool = True):
         g = policy.gru
         self.p = policy
         self.w_ih, self.b_ih = g.weight_ih_l0.detach(), g.bias_ih_l0.detach()
@@ -176,26 +215,130 @@ class FusedGRUPolicy:
         self.bh = torch.cat([policy.fc_mean.bias, policy.fc_logstd.bias]).detach().contiguous()
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         self.step_no = 0
+        self.kernel = None
+        if (kernel and self.w_ih.is_cuda and policy.gru_dim == 128 and policy.hidden_dim == 256
+                and policy.action_dim <= 16 and policy.state_dim <= 512):
+            self.kernel = self._pack()
+
+    def _pack(self):
+        from . import _lib
+        p = self.p
+        self._packed = [pack_linear(self.w_ih), pack_linear(self.w_hh), self.b_ih.contiguous(),
+                        self.b_hh.contiguous(), pack_linear(self.w1), self.b1.contiguous(),
+                        pack_linear(self.wh), _pad_vec(self.bh, -(-2 * p.action_dim // 16) * 16)]
+        return _lib.SacActor(p.state_dim, p.gru_dim, p.hidden_dim, p.action_dim,
+                             *[t.data_ptr() for t in self._packed], float(p.log_std_min),
+                             float(p.log_std_max), float(p.action_scale), float(p.action_bias))
 
     @torch.no_grad()
-    def __call__(self, state: torch.Tensor, hidden: torch.Tensor, deterministic: bool = False):
-        """state (B, I), hidden (B, H) -> action (B, A), hidden_new (B, H), log_std (B, A)."""
+    def __call__(self, state: torch.Tensor, hidden: torch.Tensor, deterministic: bool = False,
+                 reset_mask: Optional[torch.Tensor] = None, inplace: bool = False):
+        """state (B, I), hidden (B, H) -> action (B, A), hidden_new (B, H), log_std (B, A).
+
+        reset_mask (B,) bool: envs whose hidden state starts from zeros (a new episode).
+        inplace: hidden_new is `hidden` itself, updated in place."""
         from . import _lib
-        B, A, H = state.shape[0], self.p.action_dim, self.p.gru_dim
+        B, A = state.shape[0], self.p.action_dim
         lib, stream = _lib_and_stream(state.device)
-        gi = torch.addmm(self.b_ih, state, self.w_ih.t())
-        gh = torch.addmm(self.b_hh, hidden, self.w_hh.t())
-        h1 = torch.empty_like(hidden)
-        _lib.check(lib.lbsim_gru_gates(_ptr(gi), _ptr(gh), _ptr(hidden), _ptr(h1), B, H, stream))
-        y = torch.addmm(self.bh, _linear_relu(h1, self.w1, self.b1), self.wh.t())
         action = torch.empty((B, A), dtype=torch.float32, device=state.device)
         log_std = torch.empty_like(action)
+        mask = None if reset_mask is None else reset_mask.contiguous()
+        if self.kernel is not None:
+            h = hidden if inplace else hidden.clone()
+            x = state.contiguous()
+            _lib.check(_timed(lambda: lib.lbsim_sac_actor_step(
+                ctypes.byref(self.kernel), _ptr(x), _ptr(h), _ptr(mask), B, int(deterministic),
+                self.seed, self.step_no & 0xFFFFFFFF, _ptr(action), _ptr(log_std), stream)))
+            self.step_no += 1
+            return action, h, log_std
+        h0 = hidden if mask is None else hidden * (~mask.bool()).unsqueeze(1).to(hidden.dtype)
+        gi = torch.addmm(self.b_ih, state, self.w_ih.t())
+        gh = torch.addmm(self.b_hh, h0, self.w_hh.t())
+        h1 = torch.empty_like(hidden)
+        _lib.check(lib.lbsim_gru_gates(_ptr(gi), _ptr(gh), _ptr(h0), _ptr(h1), B, h1.shape[1],
+                                       stream))
+        y = torch.addmm(self.bh, _linear_relu(h1, self.w1, self.b1), self.wh.t())
         _lib.check(lib.lbsim_sac_head(
             _ptr(y), B, A, float(self.p.log_std_min), float(self.p.log_std_max),
             float(self.p.action_scale), float(self.p.action_bias), int(deterministic), self.seed,
             self.step_no & 0xFFFFFFFF, _ptr(action), _ptr(log_std), stream))
         self.step_no += 1
+        if inplace:
+            hidden.copy_(h1)
+            h1 = hidden
         return action, h1, log_std
+
+
+class FusedQMIXPolicy:
+    """problem-05 QMIXAgent.select_actions for every agent (qmix_agent.py:138-178) and
+    QMixingNetwork.forward (mixing_network.py:78-117) in ONE launch per step
+    (lbsim_qmix_policy_step): per tile of envs each agent's GRU + three linear layers,
+    epsilon-greedy with Philox noise (counter (env, step, agent)), the chosen Q-values and the
+    mixer on the global state.  Reference widths: gru 64, hidden 128, embed 32, hypernet 64."""
+
+    @staticmethod
+    def supported(agents, mixer: QMixer, n_actions: int) -> bool:
+        a0 = agents[0]
+        A, E, he = len(agents), mixer.mixing_embed_dim, mixer.hypernet_embed_dim
+        return (all(a.gru_dim == 64 and a.hidden_dim == 128 and a.obs_dim == a0.obs_dim
+                    for a in agents)
+                and 1 <= n_actions <= 16 and A <= 16 and a0.obs_dim <= 512
+                and mixer.state_dim <= 512 and E % 16 == 0 and he % 16 == 0
+                and 3 * he + E <= 256 and A * E // 16 + E // 16 + 1 <= 16
+                and A * E + E + 16 <= 3 * he and next(mixer.parameters()).is_cuda)
+
+    def __init__(self, agents, mixer: QMixer, n_actions: int = 3, epsilon: float = 0.05,
+                 seed: int = 0, servers_per_agent: int = 1):
+        from . import _lib
+        if not self.supported(agents, mixer, n_actions):
+            raise ValueError("FusedQMIXPolicy: layer widths not built into lbsim_qmix_policy_step")
+        self.A, self.n_actions, self.k = len(agents), n_actions, servers_per_agent
+        self.H = agents[0].gru_dim
+        cat = lambda f: torch.cat([f(a).reshape(-1) for a in agents]).contiguous()  # noqa: E731
+        m = mixer
+        first = [m.hyper_w1[0], m.hyper_w2[0], m.hyper_b2[0], m.hyper_b1[0]]
+        self._packed = [
+            cat(lambda a: pack_linear(a.gru.weight_ih_l0)),
+            cat(lambda a: pack_linear(a.gru.weight_hh_l0)),
+            cat(lambda a: a.gru.bias_ih_l0.detach()), cat(lambda a: a.gru.bias_hh_l0.detach()),
+            cat(lambda a: pack_linear(a.fc1.weight)), cat(lambda a: a.fc1.bias.detach()),
+            cat(lambda a: pack_linear(a.fc2.weight)), cat(lambda a: a.fc2.bias.detach()),
+            cat(lambda a: pack_linear(a.fc3.weight, 16)), cat(lambda a: _pad_vec(a.fc3.bias, 16)),
+            pack_linear(torch.cat([l.weight for l in first])),
+            torch.cat([l.bias for l in first]).detach().contiguous(),
+            pack_linear(m.hyper_w1[2].weight), m.hyper_w1[2].bias.detach().contiguous(),
+            pack_linear(m.hyper_w2[2].weight), m.hyper_w2[2].bias.detach().contiguous(),
+            pack_linear(m.hyper_b2[2].weight, 16), _pad_vec(m.hyper_b2[2].bias, 16)]
+        self.net = _lib.QmixPolicy(self.A, agents[0].obs_dim, self.H, agents[0].hidden_dim,
+                                   n_actions, m.state_dim, m.mixing_embed_dim,
+                                   m.hypernet_embed_dim, servers_per_agent, float(epsilon),
+                                   *[t.data_ptr() for t in self._packed])
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.step_no = 0
+
+    @torch.no_grad()
+    def __call__(self, obs: torch.Tensor, hidden: torch.Tensor, state: torch.Tensor,
+                 reset_mask: Optional[torch.Tensor] = None, q_values: bool = False):
+        """obs (B, A, I), hidden (B, A, H) f32 contiguous, updated in place, state (B, Ds) ->
+        actions (B, A) int64, server_actions (B, A k) int32, q_tot (B, 1), q (B, A, n) or None."""
+        from . import _lib
+        B, dev = obs.shape[0], obs.device
+        if not (hidden.is_contiguous() and hidden.shape == (B, self.A, self.H)):
+            raise ValueError("hidden must be a contiguous (B, A, gru) tensor")
+        lib, stream = _lib_and_stream(dev)
+        acts = torch.empty((B, self.A), dtype=torch.int64, device=dev)
+        sacts = torch.empty((B, self.A * self.k), dtype=torch.int32, device=dev)
+        q_tot = torch.empty((B, 1), dtype=torch.float32, device=dev)
+        q = torch.empty((B, self.A, self.n_actions), dtype=torch.float32, device=dev) \
+            if q_values else None
+        o, s = obs.contiguous(), state.contiguous()
+        mask = None if reset_mask is None else reset_mask.contiguous()
+        _lib.check(_timed(lambda: lib.lbsim_qmix_policy_step(
+            ctypes.byref(self.net), _ptr(o), _ptr(hidden), _ptr(mask), _ptr(s), B, self.seed,
+            self.step_no & 0xFFFFFFFF, _ptr(acts), _ptr(sacts), _ptr(q), None, _ptr(q_tot),
+            stream)))
+        self.step_no += 1
+        return acts, sacts, q_tot, q
 
 
 class FusedAgentQNets:

@@ -3,7 +3,8 @@ simulator with no host round trip (BASELINE configs[3] and configs[4]; SURVEY §
 
 SACGRURollout  problem-04 Trainer's acting loop (trainer.py:96-126): flattened (S*11) state ->
                PolicyNetwork.sample (GRU hidden state resident, (1, B, 128)) -> continuous weights
-               -> env.step; hidden state of finished envs zeroed (init_hidden at episode start).
+               -> env.step; hidden state of finished envs zeroed (init_hidden at episode start,
+               folded into the next policy launch).
 QMIXRollout    problem-05 QMIXAgent.select_actions (qmix_agent.py:138-178) over the multi-agent
                facade: per-agent GRU Q-networks, epsilon-greedy argmax, one int per agent, then
                the mixing network on the chosen Q-values and the global state (qmix_agent.py:110).
@@ -16,7 +17,8 @@ import torch
 
 from .env import VecLoadBalanceEnv
 from .multi_agent import VecMultiAgentLoadBalanceEnv
-from .policies import AgentQNet, FusedAgentQNets, FusedGRUPolicy, FusedQMixer, GRUPolicy, QMixer
+from .policies import (AgentQNet, FusedAgentQNets, FusedGRUPolicy, FusedQMIXPolicy, FusedQMixer,
+                       GRUPolicy, QMixer)
 
 
 class SACGRURollout:
@@ -25,31 +27,41 @@ class SACGRURollout:
         self.env = env
         S = env.num_servers
         self.policy = (policy or GRUPolicy(S * 11, S, 256, 128)).to(env.device).eval()
-        # fused: hipBLASLt GEMMs + lbsim_gru_gates / lbsim_sac_head (noise from Philox);
-        # unfused: the torch module (noise from torch's generator)
+        # fused: one lbsim_sac_actor_step launch per step at the reference widths (else hipBLASLt
+        # GEMMs + lbsim_gru_gates / lbsim_sac_head), noise from Philox; unfused: the torch module
+        # (noise from torch's generator)
         self.fused = FusedGRUPolicy(self.policy, seed=seed) if fused else None
         self.deterministic = deterministic
         self.gen = torch.Generator(device=env.device)
         self.gen.manual_seed(seed)
-        self.hidden = torch.zeros(1, env.num_envs, self.policy.gru_dim, device=env.device)
+        self._h = torch.zeros(1, env.num_envs, self.policy.gru_dim, device=env.device)
+        self._reset = None  # done of the last step: those envs start the next one from h = 0
         self.obs = env.reset()
+
+    @property
+    def hidden(self):
+        """The GRU state the next step starts from, (1, B, gru): init_hidden (zeros) for envs whose
+        episode just ended (trainer.py:96-98)."""
+        if self._reset is None:
+            return self._h
+        return self._h * (~self._reset).view(1, -1, 1).to(self._h.dtype)
 
     @torch.no_grad()
     def step(self):
         B = self.env.num_envs
         state = self.obs.reshape(B, -1)
-        if self.fused is not None:
-            action, h, _ = self.fused(state, self.hidden[0], self.deterministic)
-            h1 = h.unsqueeze(0)
+        if self.fused is not None:  # hidden updated in place, finished envs zeroed in the launch
+            action, _, _ = self.fused(state, self._h[0], self.deterministic,
+                                      reset_mask=self._reset, inplace=True)
         else:
-            mean, log_std, h1 = self.policy(state, self.hidden)
+            mean, log_std, self._h = self.policy(state, self.hidden)
             if self.deterministic:
                 action = self.policy.squash(mean)
             else:
                 eps = torch.randn(mean.shape, device=mean.device, generator=self.gen)
                 action = self.policy.squash(mean + log_std.exp() * eps)
         obs, rew, done, info = self.env.step(action)
-        self.hidden = h1 * (~done).view(1, B, 1).to(h1.dtype)
+        self._reset = done
         self.obs = obs
         return rew, done, info
 
@@ -67,16 +79,34 @@ class QMIXRollout:
         self.n_actions = n_actions
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(seed)
-        self.hidden = [torch.zeros(1, env.num_envs, a.gru_dim, device=dev) for a in self.agents]
-        self.fused = (FusedAgentQNets(self.agents), FusedQMixer(self.mixer)) if fused else None
-        if fused:
-            self.hidden = torch.zeros(A, env.num_envs, self.agents[0].gru_dim, device=dev)
+        H = self.agents[0].gru_dim
+        # fused: one lbsim_qmix_policy_step launch per step at the reference widths (agents,
+        # epsilon-greedy with Philox noise, mixer; hidden (B, A, gru)), else hipBLASLt GEMMs + HIP
+        # epilogues (hidden (A, B, gru)); unfused: the torch modules (a (1, B, gru) list)
+        self.kernel = self.fused = None
+        self._reset = None
+        if fused and FusedQMIXPolicy.supported(self.agents, self.mixer, n_actions):
+            self.kernel = FusedQMIXPolicy(self.agents, self.mixer, n_actions, epsilon, seed,
+                                          env.k)
+            self.hidden = torch.zeros(env.num_envs, A, H, device=dev)
+        elif fused:
+            self.fused = (FusedAgentQNets(self.agents), FusedQMixer(self.mixer))
+            self.hidden = torch.zeros(A, env.num_envs, H, device=dev)
+        else:
+            self.hidden = [torch.zeros(1, env.num_envs, H, device=dev) for _ in self.agents]
         self.obs = env.reset()
 
     @torch.no_grad()
     def step(self):
         B, A = self.env.num_envs, self.env.num_agents
         state = self.env.get_state()
+        if self.kernel is not None:  # envs that finished last step restart from h = 0
+            _, server_actions, q_tot, _ = self.kernel(self.obs, self.hidden, state,
+                                                      reset_mask=self._reset)
+            obs, rewards, done, info = self.env.step(server_actions)
+            self._reset = done
+            self.obs = obs
+            return q_tot, rewards, done, info
         if self.fused is not None:
             nets, mixer = self.fused
             q, self.hidden = nets(self.obs.transpose(0, 1).contiguous(), self.hidden)  # (A, B, n)
