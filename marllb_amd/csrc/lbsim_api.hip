@@ -733,6 +733,16 @@ int lbsim_qmix_policy_step(const lbsim_qmix_policy_t* n, const float* obs, float
   int mt = fused_mt(B);
   while (mt > 1 && lds_of(mt) > kFusedLdsMax) mt >>= 1;
   const hipStream_t s = (hipStream_t)stream;
+  static const bool tile_form = [] {
+    const char* e = std::getenv("LBSIM_QMIX_KERNEL");
+    return e != nullptr && std::strcmp(e, "tile") == 0;
+  }();
+  if (mt == 1 && !tile_form) {  // one wave per agent, 16 envs per workgroup (default)
+    a.lda = fused_ld(std::max(a.kxp + 64, 128));
+    const size_t lds = ((size_t)4 * 16 * a.lda + (size_t)A * 16 * 16 + 16 * (size_t)A) * 4;
+    if (a.ld > 4 * a.lda || lds > kFusedLdsMax) return LBSIM_ENOTSUP;
+    return launch_fused(&qmix_agent_wave_kernel<64, 128>, B, 1, lds, s, a);
+  }
   if (mt == 4) return launch_fused(&qmix_policy_kernel<4, 64, 128>, B, 4, lds_of(4), s, a);
   if (mt == 2) return launch_fused(&qmix_policy_kernel<2, 64, 128>, B, 2, lds_of(2), s, a);
   return launch_fused(&qmix_policy_kernel<1, 64, 128>, B, 1, lds_of(1), s, a);

@@ -353,6 +353,7 @@ struct QmixArgs {
   float* q_tot;             // [B]
   int64_t B;
   int A, I, kxp, Ds, ksp, ld, n_act, k, he, E;
+  int lda;  // qmix_agent_wave_kernel: row stride of a wave's own [16][lda] agent region
   float epsilon;
   uint32_t key0, key1, step;
 };
@@ -363,6 +364,86 @@ struct QmixMixAct {
     return c < relu_cols ? (v > 0.0f ? v : 0.0f) : v;
   }
 };
+
+// QMixingNetwork.forward (mixing_network.py:78-117) of the tile, all 4 waves, after the agents:
+// chosen[R][A] holds the chosen Q-values; the LDS tile [R][p.ld] is free.
+template <int MT>
+__device__ __forceinline__ void qmix_mixer(const QmixArgs& p, float* lds, const float* chosen,
+                                           int64_t row0, int wave, int lane) {
+  constexpr int R = 16 * MT;
+  const int ld = p.ld, A = p.A;
+  stage_rows(lds, ld, 0, p.state, p.Ds, p.Ds, p.ksp, R, row0, p.B, nullptr);
+  __syncthreads();
+  const int he = p.he, E = p.E;
+  {
+    const int nt0 = (3 * he + E) / 16;  // <= 16
+    f4 acc[4][MT];
+    dense_acc<MT, 4>(acc, lds, ld, 0, p.m0, p.ksp / 16, nt0, p.mb0, wave, lane);
+    __syncthreads();
+    dense_store<MT, 4>(acc, lds, ld, 0, nt0, wave, lane, QmixMixAct{3 * he});
+  }
+  __syncthreads();
+  {
+    // second layers: w1 tiles (A E / 16) from cols [0, he), w2 tiles (E / 16) from [he, 2 he),
+    // b2 (one tile) from [2 he, 3 he); outputs to cols [0, A E), [A E, A E + E), A E + E
+    const int n1 = A * E / 16, n2 = E / 16, ntot = n1 + n2 + 1, kb = he / 16;
+    f4 acc[4][MT];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = wave + 4 * j;
+      if (t >= ntot) continue;
+      const float* w;
+      const float* bias;
+      int col0, tt;
+      if (t < n1) {
+        w = p.mw1, bias = p.mbw1, col0 = 0, tt = t;
+      } else if (t < n1 + n2) {
+        w = p.mw2, bias = p.mbw2, col0 = he, tt = t - n1;
+      } else {
+        w = p.mb2, bias = p.mbb2, col0 = 2 * he, tt = 0;
+      }
+      const float bv = bias[tt * 16 + (lane & 15)];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[j][m] = splat4(bv);
+      mma_tile<MT>(acc[j], lds, ld, col0, (const f4*)w + (size_t)tt * kb * 64, kb, lane);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = wave + 4 * j;
+      if (t >= ntot) continue;
+      const bool is_abs = t < n1 + n2;  // |W1|, |W2| (mixing_network.py:96,105)
+      const int c = t * 16 + (lane & 15);
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float v = acc[j][m][i];
+          lds[(m * 16 + 4 * (lane >> 4) + i) * ld + c] = is_abs ? fabsf(v) : v;
+        }
+    }
+  }
+  __syncthreads();
+  // tail: hidden_e = elu(b1_e + sum_a q_a |w1[a E + e]|), Q_tot = sum_e hidden_e |w2_e| + b2;
+  // 4 threads per row, E / 4 embedding units each, combined by shuffles (R * 4 is a multiple of
+  // 64, so every wave is either fully inside the loop or fully outside it)
+  const int b1c = 3 * he, w2c = A * E, b2c = A * E + E;
+  for (int e0 = threadIdx.x; e0 < R * 4; e0 += blockDim.x) {
+    const int r = e0 >> 2, part = e0 & 3;
+    const float* row = lds + r * ld;
+    float acc = 0.0f;
+    for (int u = part * (E / 4); u < (part + 1) * (E / 4); ++u) {
+      float h = 0.0f;
+      for (int a = 0; a < A; ++a) h += chosen[r * A + a] * row[a * E + u];
+      h += row[b1c + u];
+      h = h > 0.0f ? h : expm1f(h);
+      acc += h * row[w2c + u];
+    }
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    if (part == 0 && row0 + r < p.B) p.q_tot[row0 + r] = acc + row[b2c];
+  }
+}
 
 template <int MT, int H, int F>
 __global__ void __launch_bounds__(256) qmix_policy_kernel(QmixArgs p) {
@@ -435,78 +516,142 @@ __global__ void __launch_bounds__(256) qmix_policy_kernel(QmixArgs p) {
       if (p.q_chosen) p.q_chosen[b * A + a] = q[act];
     }
   }
-  // mixer (mixing_network.py:78-117) on the global state
-  stage_rows(lds, ld, 0, p.state, p.Ds, p.Ds, p.ksp, R, row0, p.B, nullptr);
-  __syncthreads();
-  const int he = p.he, E = p.E;
-  {
-    const int nt0 = (3 * he + E) / 16;  // <= 16
-    f4 acc[4][MT];
-    dense_acc<MT, 4>(acc, lds, ld, 0, p.m0, p.ksp / 16, nt0, p.mb0, wave, lane);
-    __syncthreads();
-    dense_store<MT, 4>(acc, lds, ld, 0, nt0, wave, lane, QmixMixAct{3 * he});
-  }
-  __syncthreads();
-  {
-    // second layers: w1 tiles (A E / 16) from cols [0, he), w2 tiles (E / 16) from [he, 2 he),
-    // b2 (one tile) from [2 he, 3 he); outputs to cols [0, A E), [A E, A E + E), A E + E
-    const int n1 = A * E / 16, n2 = E / 16, ntot = n1 + n2 + 1, kb = he / 16;
-    f4 acc[4][MT];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int t = wave + 4 * j;
-      if (t >= ntot) continue;
-      const float* w;
-      const float* bias;
-      int col0, tt;
-      if (t < n1) {
-        w = p.mw1, bias = p.mbw1, col0 = 0, tt = t;
-      } else if (t < n1 + n2) {
-        w = p.mw2, bias = p.mbw2, col0 = he, tt = t - n1;
-      } else {
-        w = p.mb2, bias = p.mbb2, col0 = 2 * he, tt = 0;
-      }
-      const float bv = bias[tt * 16 + (lane & 15)];
-#pragma unroll
-      for (int m = 0; m < MT; ++m) acc[j][m] = splat4(bv);
-      mma_tile<MT>(acc[j], lds, ld, col0, (const f4*)w + (size_t)tt * kb * 64, kb, lane);
+  qmix_mixer<MT>(p, lds, chosen, row0, wave, lane);
+}
+
+// Wave-local LDS ordering: a wave's own writes are visible to its later reads (no workgroup barrier).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The same step with one WAVE per agent (agents w, w + 4, ...) over a 16-env tile: each wave runs
+// its agent's whole network in its own LDS region [16][lda] with no workgroup barrier between
+// layers, every layer's tiles in mma_multi passes (the GRU's three gates per unit tile, fc1 / fc2
+// four tiles at a time); the workgroup meets once, for the mixer.
+template <int H, int F>
+__global__ void __launch_bounds__(256) qmix_agent_wave_kernel(QmixArgs p) {
+  extern __shared__ float lds[];
+  constexpr int R = 16, UT = H / 16, NT = F / 16;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row0 = (int64_t)blockIdx.x * R;
+  const int lda = p.lda, kxp = p.kxp, A = p.A, NQ = p.n_act;
+  float* mine = lds + wave * R * lda;
+  float* qv = lds + 4 * R * lda;    // [A][R][16]
+  float* chosen = qv + A * R * 16;  // [R][A]
+  const int kbx = kxp / 16;
+  for (int a = wave; a < A; a += 4) {
+    for (int e = lane; e < R * kxp; e += 64) {  // obs rows of agent a, zero padded
+      const int r = e / kxp, c = e - r * kxp;
+      const int64_t b = row0 + r;
+      mine[r * lda + c] = (c < p.I && b < p.B) ? p.obs[(b * A + a) * p.I + c] : 0.0f;
     }
-    __syncthreads();
+    for (int e = lane; e < R * H; e += 64) {  // hidden rows (zeros for reset envs)
+      const int r = e / H, c = e - r * H;
+      const int64_t b = row0 + r;
+      const bool live = b < p.B && !(p.reset && p.reset[b]);
+      mine[r * lda + kxp + c] = live ? p.hidden[(b * A + a) * H + c] : 0.0f;
+    }
+    wave_sync();
+    const f4* wi = (const f4*)(p.w_ih + (size_t)a * 3 * H * kxp);
+    const f4* wh = (const f4*)(p.w_hh + (size_t)a * 3 * H * H);
+    const float* bi = p.b_ih + a * 3 * H;
+    const float* bh = p.b_hh + a * 3 * H;
+    f4 hn[UT][1];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int t = wave + 4 * j;
-      if (t >= ntot) continue;
-      const bool is_abs = t < n1 + n2;  // |W1|, |W2| (mixing_network.py:96,105)
-      const int c = t * 16 + (lane & 15);
+    for (int u = 0; u < UT; ++u) {
+      const int col = u * 16 + (lane & 15);
+      f4 g[4][1];
+      g[0][0] = splat4(bi[2 * H + col]);
+      g[1][0] = splat4(bi[col] + bh[col]);
+      g[2][0] = splat4(bi[H + col] + bh[H + col]);
+      g[3][0] = splat4(bh[2 * H + col]);
+      const f4* const wx[3] = {wi + (size_t)(2 * UT + u) * kbx * 64, wi + (size_t)u * kbx * 64,
+                               wi + (size_t)(UT + u) * kbx * 64};
+      const f4* const wy[3] = {wh + (size_t)u * UT * 64, wh + (size_t)(UT + u) * UT * 64,
+                               wh + (size_t)(2 * UT + u) * UT * 64};
+      mma_multi<1, 3>(*reinterpret_cast<f4(*)[3][1]>(&g[0]), mine, lda, 0, wx, kbx, lane);
+      mma_multi<1, 3>(*reinterpret_cast<f4(*)[3][1]>(&g[1]), mine, lda, kxp, wy, UT, lane);
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
+      for (int i = 0; i < 4; ++i) {
+        const float hp = mine[(4 * (lane >> 4) + i) * lda + kxp + col];
+        const float r = sigmoid_f(g[1][0][i]);
+        const float z = sigmoid_f(g[2][0][i]);
+        const float n = tanhf(g[0][0][i] + r * g[3][0][i]);
+        hn[u][0][i] = (1.0f - z) * n + z * hp;
+      }
+    }
+    wave_sync();
+#pragma unroll
+    for (int u = 0; u < UT; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 4 * (lane >> 4) + i, col = u * 16 + (lane & 15);
+        mine[r * lda + kxp + col] = hn[u][0][i];
+        if (row0 + r < p.B) p.hidden[((row0 + r) * A + a) * H + col] = hn[u][0][i];
+      }
+    wave_sync();
+    // fc1 (H -> F) then fc2 (F -> F), ReLU, four output tiles per mma_multi pass
+#pragma unroll
+    for (int layer = 0; layer < 2; ++layer) {
+      const int col0 = layer == 0 ? kxp : 0, nkb = layer == 0 ? H / 16 : F / 16;
+      const float* w = layer == 0 ? p.w1 + (size_t)a * F * H : p.w2 + (size_t)a * F * F;
+      const float* bias = (layer == 0 ? p.b1 : p.b2) + a * F;
+      f4 acc[NT][1];
+#pragma unroll
+      for (int t0 = 0; t0 < NT; t0 += 4) {
+        const f4* wp[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          wp[j] = (const f4*)w + (size_t)(t0 + j) * nkb * 64;
+          acc[t0 + j][0] = splat4(bias[(t0 + j) * 16 + (lane & 15)]);
+        }
+        mma_multi<1, 4>(*reinterpret_cast<f4(*)[4][1]>(&acc[t0]), mine, lda, col0, wp, nkb, lane);
+      }
+      wave_sync();
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float v = acc[j][m][i];
-          lds[(m * 16 + 4 * (lane >> 4) + i) * ld + c] = is_abs ? fabsf(v) : v;
+          const float v = acc[t][0][i];
+          mine[(4 * (lane >> 4) + i) * lda + t * 16 + (lane & 15)] = v > 0.0f ? v : 0.0f;
         }
+      wave_sync();
     }
+    // fc3 -> Q-values (<= 16 actions: one tile)
+    {
+      f4 q[1] = {splat4(p.b3[a * 16 + (lane & 15)])};
+      mma_tile<1>(q, mine, lda, 0, (const f4*)(p.w3 + (size_t)a * 16 * F), NT, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) qv[(a * R + 4 * (lane >> 4) + i) * 16 + (lane & 15)] = q[0][i];
+    }
+    wave_sync();
+    if (lane < R) {  // epsilon-greedy for (env lane, agent a), as qmix_policy_kernel
+      const int r = lane;
+      const int64_t b = row0 + r;
+      const float* q = qv + (a * R + r) * 16;
+      int g = 0;
+      for (int j = 1; j < NQ; ++j)
+        if (q[j] > q[g]) g = j;
+      const u32x4 d = philox4x32_10(u32x4{(uint32_t)b, p.step, (uint32_t)a, 4u << 24}, p.key0,
+                                    p.key1);
+      const float u = (float)(d.x >> 8) * 5.9604644775390625e-8f;
+      const int act = u < p.epsilon ? (int)(((uint64_t)d.y * (uint32_t)NQ) >> 32) : g;
+      chosen[r * A + a] = q[act];
+      if (b < p.B) {
+        p.actions[b * A + a] = act;
+        if (p.server_actions)
+          for (int j = 0; j < p.k; ++j) p.server_actions[(b * A + a) * p.k + j] = act;
+        if (p.q_out)
+          for (int j = 0; j < NQ; ++j) p.q_out[(b * A + a) * NQ + j] = q[j];
+        if (p.q_chosen) p.q_chosen[b * A + a] = q[act];
+      }
+    }
+    wave_sync();
   }
   __syncthreads();
-  // tail: hidden_e = elu(b1_e + sum_a q_a |w1[a E + e]|), Q_tot = sum_e hidden_e |w2_e| + b2;
-  // 4 threads per row, E / 4 embedding units each, combined by shuffles (R * 4 is a multiple of
-  // 64, so every wave is either fully inside the loop or fully outside it)
-  const int b1c = 3 * he, w2c = A * E, b2c = A * E + E;
-  for (int e0 = threadIdx.x; e0 < R * 4; e0 += blockDim.x) {
-    const int r = e0 >> 2, part = e0 & 3;
-    const float* row = lds + r * ld;
-    float acc = 0.0f;
-    for (int u = part * (E / 4); u < (part + 1) * (E / 4); ++u) {
-      float h = 0.0f;
-      for (int a = 0; a < A; ++a) h += chosen[r * A + a] * row[a * E + u];
-      h += row[b1c + u];
-      h = h > 0.0f ? h : expm1f(h);
-      acc += h * row[w2c + u];
-    }
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
-    if (part == 0 && row0 + r < p.B) p.q_tot[row0 + r] = acc + row[b2c];
-  }
+  qmix_mixer<1>(p, lds, chosen, row0, wave, lane);
 }
 
 }  // namespace lbk
