@@ -92,7 +92,8 @@ def test_sac_actor_kernel_matches_module(g):
     np.testing.assert_allclose(ls.cpu().numpy(), g["policy_log_std"], **TOL)
     assert h1.data_ptr() != h.data_ptr()
     np.testing.assert_array_equal(h.cpu().numpy(), g["policy_h"][0])  # input untouched
-    # a ragged batch (1000 = 15 tiles of 64 + 40) with reset rows, hidden updated in place
+    # a ragged batch (1000: not a multiple of the 16, 32 or 64-env tile) with reset rows, hidden
+    # updated in place
     gen = torch.Generator(device=dev).manual_seed(1)
     B = 1000
     xb = torch.randn(B, 88, device=dev, generator=gen) * 3
@@ -125,7 +126,7 @@ def test_qmix_policy_kernel_matches_modules(g):
                 p.mul_(1.0 + 0.1 * k)
     mix = load_prefixed(QMixer(4, 74, 32, 64), g, "mixer").to(dev)
     gen = torch.Generator(device=dev).manual_seed(3)
-    B = 300  # ragged: 18 tiles of 16 + 12
+    B = 300  # ragged: not a multiple of the tile
     obs = torch.randn(B, 4, 128, device=dev, generator=gen)
     hid = torch.randn(B, 4, 64, device=dev, generator=gen) * 0.5
     state = torch.randn(B, 74, device=dev, generator=gen)
@@ -158,3 +159,21 @@ def test_qmix_policy_kernel_matches_modules(g):
     a2, _, _, _ = pol2(obs, hid.clone(), state)
     a3, _, _, _ = pol2(obs, hid.clone(), state)
     assert torch.equal(a1, a2) and not torch.equal(a2, a3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [{"LBSIM_QMIX_KERNEL": "tile"},
+                                 {"LBSIM_FUSED_MT": "2", "LBSIM_QMIX_KERNEL": "tile"},
+                                 {"LBSIM_FUSED_MT": "4", "LBSIM_QMIX_KERNEL": "tile"}])
+def test_other_tile_forms_match_modules(env):
+    """The layer-split QMIX kernel and the 32 / 64-env tiles (selected once per process by the
+    environment, so checked in a child process) pass the same parity tests."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p",
+                        "no:cacheprovider", os.path.join(root, "tests", "test_fused_policy.py"),
+                        "-k", "matches_module"],
+                       cwd=root, env={**os.environ, **env}, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
