@@ -175,8 +175,8 @@ class VecMultiAgentLoadBalanceEnv:
         torch = _torch()
         obs, rew, done, info = self.vec.step(self.expand_actions(actions))
         self._ep_len = info["episode_length"].to(torch.int32)
-        if self.vec.autoreset:
-            self._ep_len = torch.where(done, torch.zeros_like(self._ep_len), self._ep_len)
+        if self.vec.autoreset:  # out of place: info["episode_length"] keeps the finished length
+            self._ep_len = self._ep_len.masked_fill(done, 0)
         loads = obs[:, :, 0]
         info = dict(info)
         info["server_loads"] = loads
@@ -191,10 +191,12 @@ class VecMultiAgentLoadBalanceEnv:
 
     def get_state(self):
         torch = _torch()
-        st = torch.zeros((self.num_envs, self.state_dim), dtype=torch.float32, device=self.device)
-        st[:, -2] = self._ep_len.float() / float(self.max_steps)
-        st[:, -1] = float(self.num_agents)
-        return st
+        if getattr(self, "_state", None) is None:  # zeros, then the constant agent-count column
+            self._state = torch.zeros((self.num_envs, self.state_dim), dtype=torch.float32,
+                                      device=self.device)
+            self._state[:, -1] = float(self.num_agents)
+        torch.div(self._ep_len, float(self.max_steps), out=self._state[:, -2])
+        return self._state.clone()  # callers may keep it (replay buffers): value semantics
 
     def close(self):
         self.vec.close()
