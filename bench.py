@@ -3,7 +3,8 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--servers S]
 
-One rank per GPU (torchrun for N > 1).  Weak scaling: every GPU steps its own shard of B envs
+One rank per GPU: under torch.distributed.run, or, for --gpus N > 1 without it, N rank processes
+this script starts itself (same environment contract).  Weak scaling: every GPU steps its own shard of B envs
 (global ids [rank*B, (rank+1)*B) key the RNG, so shards never communicate); the only collectives
 are the timing barrier and the max/sum reductions of the result.  A "step" is one VecEnv.step of
 every env: random-policy actions drawn on the GPU, dynamics kernel, observe kernel (features,
@@ -91,18 +92,43 @@ def parse():
     return ap.parse_args()
 
 
+def _cpu_info():
+    """CPU model, affinity core count and the cgroup CPU quota (cpu.max) of this process."""
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    return model or "host CPU", cores, quota
+
+
 def cpu_baseline(args, seconds: float):
-    """Oracle (C restatement, identical dynamics/features) on host cores, bounded sample."""
+    """Oracle (C restatement, identical dynamics/features) on ALL of this process's cores
+    (sched_getaffinity, one OpenMP thread each), bounded sample of the same workload: >= 64 envs
+    per thread, about `seconds` of stepping.  Beside it, the reference's own CPU step
+    (env.py simulation mode: MT19937 observations, dict round trip, reward; no flow dynamics),
+    restated in marllb_amd.plumbing and timed here on one core, and the figure the survey
+    recorded for the reference itself on a different host."""
     import numpy as np
 
     import oracle
-    from marllb_amd.env import make_config
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except AttributeError:
-        avail = os.cpu_count() or 1
-    threads = max(1, min(16, avail))
-    nb = 2048
+    from marllb_amd.env import LoadBalanceEnv, make_config
+    model, threads, quota = _cpu_info()
+    nb = max(2048, 64 * threads)
     cfg = make_config(nb, args.servers, seed=args.seed, env_id_offset=0)
     ora = oracle.OracleEnv(cfg, threads=threads)
     ora.reset()
@@ -116,22 +142,69 @@ def cpu_baseline(args, seconds: float):
         el = time.perf_counter() - t0
         if el >= seconds and n >= 3:
             break
-    cpu_model = ""
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu_model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
+    ora.close()
+    # the reference's CPU plumbing step (configs[0], 1 x S, step_interval 0), one core
+    pe = LoadBalanceEnv(num_servers=args.servers, step_interval=0.0, seed=0,
+                        reference_plumbing=True)
+    pe.reset()
+    pa = [rng.integers(0, 3, args.servers) for _ in range(64)]
+    m, t1 = 0, time.perf_counter()
+    while time.perf_counter() - t1 < 2.0:
+        pe.step(pa[m % 64])
+        m += 1
+    pel = time.perf_counter() - t1
     return {"value": nb * n / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "cgroup_cpu_quota": quota,
             "sample": f"{nb} of the {args.batch} envs (global ids 0-{nb - 1}), S={args.servers}, "
                       f"{n} random-policy steps, {el:.1f} s, oracle/lbsim_oracle.c "
-                      f"(OpenMP {threads} threads) on {cpu_model or 'host CPU'}"}
+                      f"(OpenMP, {threads} threads = every core in sched_getaffinity) on {model}",
+            "reference_plumbing": {
+                "value": m / pel, "unit": "env-steps/s/core", "cores": 1, "kind": "port",
+                "what": "the reference's own LoadBalanceEnv.step in simulation mode (random "
+                        "observations, no flow dynamics, step_interval=0), restated byte-exact "
+                        "in marllb_amd/plumbing.py, timed here",
+                "survey_recorded": {"value": 8164.0, "unit": "env-steps/s/core",
+                                    "host": "different host: survey container, Intel Xeon "
+                                            "8 vCPU, reference Python run in place "
+                                            "(SURVEY.md §6, BASELINE.md §2)"}}}
+
+
+def spawn_ranks(args) -> int:
+    """`bench.py --gpus N` without torchrun: start N rank processes of this script (one per GPU,
+    the torchrun environment contract: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), before this
+    parent touches the GPU; only rank 0 prints the JSON line.  Returns the worst exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = {**os.environ, "RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(args.gpus),
+               "LOCAL_WORLD_SIZE": str(args.gpus), "GROUP_RANK": "0",
+               "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)}
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in live:  # one rank failed: the others would wait in a collective
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(spawn_ranks(args))
     import torch
     import torch.distributed as dist
 
@@ -147,8 +220,7 @@ def main():
     world, rank = shard.world, shard.rank
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("for --gpus N > 1 launch with torch.distributed.run --nproc-per-node N")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # one process per GPU; LBSIM_DIST_BACKEND=gloo rehearses several ranks on fewer GPUs
     backend = os.environ.get("LBSIM_DIST_BACKEND", "nccl")
     local = local % max(1, torch.cuda.device_count())
@@ -244,7 +316,8 @@ def main():
             if t.get("batch") == B and t.get("servers") == S and dom in t.get("bytes_per_launch", {}):
                 traffic = t["bytes_per_launch"][dom]
         out = {
-            "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
+            "metric": METRIC, "value": value, "unit": "env-steps/s",
+            "n_gpus": dist.get_world_size() if world > 1 else 1,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32/int32 (f64 reward)",

@@ -10,7 +10,9 @@ LoadBalanceEnv      the reference's single-environment API, call for call
 Both run every step through the gfx950 kernels (marllb_amd/csrc).  What differs from the
 reference by design: observations come from a real flow simulator (arrivals ->
 server assignment -> FIFO service -> reservoir features) instead of np.random draws, and there is
-no wall-clock sleep (step_interval is SIMULATED seconds).
+no wall-clock sleep (step_interval is SIMULATED seconds).  The reference's own random-observation
+simulation mode is available on the host as LoadBalanceEnv(reference_plumbing=True)
+(BASELINE configs[0], marllb_amd/plumbing.py).
 """
 from __future__ import annotations
 
@@ -212,13 +214,18 @@ class VecLoadBalanceEnv:
     reset(mask=None) -> obs (B, S, 11) f32 cuda tensor
     step(actions)    -> obs, reward (B,) f32, done (B,) bool, info dict of tensors
     Actions: (B, S) int32/int64 indices (discrete) or float32 weights (continuous), any device.
+    Discrete indices follow Python list indexing for -n <= a < n (env.py:346); out-of-range
+    indices are CLAMPED on the device (a >= n -> n-1, a < -n -> 0) where the reference raises
+    IndexError -- a device-side raise would need a host sync per step.  strict_actions=True checks
+    the range on the host before every launch (one sync per step; for debugging callers).
     With autoreset=True, envs whose episode ended are reset inside step(); their returned obs is
     the first obs of the new episode and info['terminal_obs'] (if keep_terminal_obs) holds the
     last one, as gym/SB3 vector envs do.
     """
 
     def __init__(self, num_envs: int, num_servers: int = 4, *, device=None,
-                 autoreset: bool = True, keep_terminal_obs: bool = False, **kwargs):
+                 autoreset: bool = True, keep_terminal_obs: bool = False,
+                 strict_actions: bool = False, **kwargs):
         torch = _torch()
         self.device_index = _device_index(device)
         self.device = torch.device("cuda", self.device_index)
@@ -229,6 +236,7 @@ class VecLoadBalanceEnv:
         self.action_type = "discrete" if self.cfg.action_type == _lib.ACTION_DISCRETE else "continuous"
         self.autoreset = autoreset
         self.keep_terminal_obs = keep_terminal_obs
+        self.strict_actions = strict_actions
         self.handle = Handle(self.cfg, self.device_index)
         if self.trace is not None:
             self.handle.set_trace(self.trace)
@@ -257,8 +265,27 @@ class VecLoadBalanceEnv:
             if a.dtype != torch.float32:
                 a = a.to(torch.float32)
             dt = _lib.DTYPE_F32
+        if a.numel() != self.num_envs * self.num_servers:
+            raise ValueError(f"actions: expected {self.num_envs} x {self.num_servers} values, "
+                             f"got shape {tuple(a.shape)}")
         a = a.to(self.device).reshape(self.num_envs, self.num_servers).contiguous()
+        if self.strict_actions and self.action_type == "discrete":
+            n = int(self.cfg.num_discrete)
+            if bool(((a >= n) | (a < -n)).any()):  # env.py:346 list indexing
+                raise IndexError("list index out of range")
         return a, dt
+
+    def _mask(self, mask):
+        """A reset mask as a contiguous u8 device tensor of exactly num_envs entries (the kernels
+        read mask[b] for every b < B)."""
+        torch = _torch()
+        m = torch.as_tensor(mask)
+        if m.dtype not in (torch.bool, torch.uint8):
+            raise ValueError(f"reset mask must be bool or uint8, got {m.dtype}")
+        if m.numel() != self.num_envs:
+            raise ValueError(f"reset mask must have num_envs={self.num_envs} entries, "
+                             f"got {m.numel()}")
+        return m.reshape(-1).to(self.device).to(torch.uint8).contiguous()
 
     # -- API
     def reset(self, mask=None):
@@ -278,7 +305,7 @@ class VecLoadBalanceEnv:
             return obs
         if not self._reset_done:
             raise RuntimeError("call reset() without a mask first")
-        m = torch.as_tensor(mask).to(self.device).to(torch.uint8).contiguous()
+        m = self._mask(mask)
         obs = self._last_obs.clone()
         self.handle.check(self.handle.lib.lbsim_reset(self.handle.h, m.data_ptr(),
                                                       obs.data_ptr(), self._stream()))
@@ -344,7 +371,17 @@ class VecLoadBalanceEnv:
 
 
 class LoadBalanceEnv:
-    """Drop-in for the reference LoadBalanceEnv (env.py:41-470), one env, numpy I/O."""
+    """Drop-in for the reference LoadBalanceEnv (env.py:41-470), one env, numpy I/O.
+
+    Modes (all behind the reference's constructor, env.py:71-87):
+      default                 the GPU flow simulator (one env of a VecLoadBalanceEnv); one
+                              device->host copy per step (obs, raw obs, reward in one buffer)
+      use_shm=True            problem-02 frames from shared memory (env.py:197-254), falling back
+                              to the simulator when attach / read fails, as the reference does
+      reference_plumbing=True BASELINE configs[0]: the reference's own CPU simulation mode
+                              (MT19937 random observations, marllb_amd/plumbing.py), host only,
+                              byte-identical to env.py for the same seed; opt-in, never a fallback
+    """
 
     DEFAULT_DISCRETE_WEIGHTS = DEFAULT_DISCRETE_WEIGHTS
 
@@ -354,7 +391,8 @@ class LoadBalanceEnv:
                  reward_field: str = "flow_duration_avg_decay", step_interval: float = 0.25,
                  max_steps: int = 10000, use_shm: bool = False, shm_name: Optional[str] = None,
                  use_ground_truth: bool = False, normalize_obs: bool = False,
-                 seed: Optional[int] = None, *, device=None, **sim_kwargs):
+                 seed: Optional[int] = None, *, device=None, reference_plumbing: bool = False,
+                 **sim_kwargs):
         self.num_servers = num_servers
         self.action_type = action_type
         self.discrete_weights = discrete_weights or self.DEFAULT_DISCRETE_WEIGHTS
@@ -383,7 +421,23 @@ class LoadBalanceEnv:
                 print(f"Warning: Failed to attach shared memory: {e}")
                 print("Falling back to simulation mode")
                 self.use_shm = False
-        self._norm = None  # host running statistics for SHM observations (env.py:450-470)
+        self.current_step = 0
+        self.last_observation = None
+        self.episode_rewards: List[float] = []
+        self.episode_return = 0.0
+        self._last_raw = None  # un-normalised obs of the last reset/step (problem-05 loads)
+        self._plumb = None
+        self._vec = None
+        if reference_plumbing:
+            from .plumbing import ReferencePlumbing
+            self._plumb = ReferencePlumbing(num_servers, seed, normalize_obs, reward_metric,
+                                            reward_field)
+            return
+        # With a live SHM region, frames and the simulator fallback share ONE running
+        # normalisation (host float64, env.py:450-470), as the reference's single obs_mean/obs_std
+        # do; otherwise the device kernel normalises.
+        self._host_norm = self.shm is not None and normalize_obs
+        self._norm = None
         self._vec = VecLoadBalanceEnv(
             1, num_servers, device=device, autoreset=False, action_type=action_type,
             discrete_weights=self.discrete_weights, max_weight=max_weight, min_weight=min_weight,
@@ -391,11 +445,9 @@ class LoadBalanceEnv:
             # step_interval is the reference's wall-clock sleep (env.py:257; 0 = none, used by
             # its tests); the simulator needs simulated time per step, 0.25 s when it is 0
             step_interval=step_interval if step_interval > 0 else 0.25,
-            max_steps=max_steps, normalize_obs=normalize_obs, seed=seed, **sim_kwargs)
-        self.current_step = 0
-        self.last_observation = None
-        self.episode_rewards: List[float] = []
-        self.episode_return = 0.0
+            max_steps=max_steps, normalize_obs=normalize_obs and not self._host_norm, seed=seed,
+            **sim_kwargs)
+        self._io = None
 
     # ---- spaces (env.py:156-184)
     def _setup_spaces(self):
@@ -403,19 +455,78 @@ class LoadBalanceEnv:
             self.num_servers, self.action_type, self.discrete_weights, self.min_weight,
             self.max_weight, self.use_ground_truth)
 
+    # ---- single-env I/O: one device buffer [obs | raw | reward], one copy to pinned host memory
+    def _io_buffers(self):
+        if self._io is None:
+            torch = _torch()
+            n = self.num_servers * NF
+            dev = torch.empty(2 * n + 2, dtype=torch.float32, device=self._vec.device)
+            host = torch.empty(2 * n + 2, dtype=torch.float32, pin_memory=True)
+            act_dt = torch.int64 if self.action_type == "discrete" else torch.float32
+            act_h = torch.empty(self.num_servers, dtype=act_dt, pin_memory=True)
+            act_d = torch.empty(self.num_servers, dtype=act_dt, device=self._vec.device)
+            done = torch.empty(1, dtype=torch.uint8, device=self._vec.device)
+            self._io = (dev, host, act_h, act_d, done, n)
+        return self._io
+
+    def _sim_reset(self) -> np.ndarray:
+        """Reset the simulator; returns the (possibly normalised) first observation."""
+        obs = self._vec.reset()[0].cpu().numpy()
+        self._last_raw = obs
+        if self._host_norm:
+            obs = self._normalize_host(obs)
+        return obs
+
+    def _sim_step(self, idx_or_w: np.ndarray):
+        """One simulator step -> (obs, raw obs, reward) with a single device->host transfer."""
+        torch = _torch()
+        v = self._vec
+        if not v._reset_done:  # e.g. SHM mode whose reset came from a frame
+            v.reset()
+        dev, host, act_h, act_d, done, n = self._io_buffers()
+        act_h.numpy()[:] = idx_or_w
+        act_d.copy_(act_h, non_blocking=True)
+        out = _lib.StepOutputs()
+        base = dev.data_ptr()
+        out.obs, out.raw_obs, out.reward = base, base + 4 * n, base + 8 * n
+        out.done = done.data_ptr()
+        dt = _lib.DTYPE_I64 if self.action_type == "discrete" else _lib.DTYPE_F32
+        stream = v._stream()
+        v.handle.check(v.handle.lib.lbsim_step_ex(v.handle.h, act_d.data_ptr(), dt,
+                                                  ctypes.byref(out), stream))
+        v._step_bound += 1
+        host.copy_(dev, non_blocking=True)
+        torch.cuda.current_stream(v.device).synchronize()
+        h = host.numpy()
+        S = self.num_servers
+        obs = h[:n].reshape(S, NF).copy()
+        raw = h[n:2 * n].reshape(S, NF).copy()
+        if self._host_norm:
+            obs = self._normalize_host(raw)
+        return obs, raw, float(h[2 * n])
+
     # ---- gym API
     def reset(self) -> np.ndarray:
         self.current_step = 0
         self.episode_rewards = []
         self.episode_return = 0.0
+        if self._plumb is not None:  # env.py:206-213
+            obs = self._plumb.simulate()
+            self._last_raw = obs
+            return self._plumb.normalize(obs) if self.normalize_obs else obs
         if self.use_shm and self.shm is not None:  # env.py:197-205
-            obs_dict = self.shm.read_observation()
+            # the simulator is reset too, so a later step without a new frame can fall back to it
+            self._vec.reset()
+            try:
+                obs_dict = self.shm.read_observation()
+            except Exception as e:
+                obs_dict = None
+                print(f"Warning: Failed to read from SHM: {e}")
             if obs_dict is not None:
                 self.last_observation = obs_dict
                 return self._shm_obs(obs_dict)
             print("Warning: Failed to read from SHM: no observation published")
-        obs = self._vec.reset()[0].cpu().numpy()
-        return obs
+        return self._sim_reset()
 
     # ---- SHM path (env.py:235-254): frames in problem-02's wire format (marllb_amd/shm.py)
     def _shm_obs(self, obs_dict: dict) -> np.ndarray:
@@ -427,7 +538,7 @@ class LoadBalanceEnv:
             if sid < self.num_servers:
                 obs[sid, 0] = st.get("n_flow_on", 0)
                 obs[sid, 1:] = st.get("reservoir_features", [0.0] * 10)[:10]
-        self._shm_raw = obs
+        self._last_raw = obs
         if self.normalize_obs:
             obs = self._normalize_host(obs)
         return obs
@@ -458,39 +569,48 @@ class LoadBalanceEnv:
         return float(out.item())
 
     def _shm_step(self, weights: np.ndarray):
-        seq = (self.last_observation or {}).get("sequence_id", self.current_step)
-        self.shm.write_action(sequence_id=seq, weights=[float(x) for x in weights])
+        """env.py:235-254: write the weights, wait, read the next frame.  Write and read errors
+        are reported and tolerated as the reference does; None = no new frame (the caller falls
+        back to the simulator)."""
+        try:
+            seq = (self.last_observation or {}).get("sequence_id", self.current_step)
+            self.shm.write_action(sequence_id=seq, weights=[float(x) for x in weights])
+        except Exception as e:
+            print(f"Warning: Failed to write action to SHM: {e}")
         time.sleep(self.step_interval)  # the live LB runs in wall-clock time
-        obs_dict = self.shm.read_observation()
+        try:
+            obs_dict = self.shm.read_observation()
+        except Exception as e:
+            print(f"Warning: Failed to read from SHM: {e}")
+            return None
         if obs_dict is None:
             print("Warning: Failed to read from SHM: no new observation")
             return None
         self.last_observation = obs_dict
         obs = self._shm_obs(obs_dict)
-        return obs, self._shm_raw, self._shm_reward(self._shm_raw), obs_dict
+        return obs, self._last_raw, self._shm_reward(self._last_raw), obs_dict
 
     def step(self, action) -> Tuple[np.ndarray, float, bool, Dict[str, Any]]:
-        torch = _torch()
         self.current_step += 1
-        weights = self._action_to_weights(action)
-        a = np.asarray(action)
-        if self.action_type == "discrete":
-            idx = np.array([int(x) for x in a.reshape(-1)], dtype=np.int64)
-            n = len(self.discrete_weights)
-            if np.any(idx >= n) or np.any(idx < -n):  # python list indexing (env.py:346)
-                raise IndexError("list index out of range")
-            act = torch.from_numpy(idx.reshape(1, -1))
+        weights = self._action_to_weights(action)  # IndexError on a bad index, as env.py:346
+        if self._plumb is not None:  # env.py:255-286, simulation mode
+            raw = self._plumb.simulate()
+            obs_dict = self._array_to_dict(raw)
+            reward = self._plumb.reward(obs_dict)
+            next_obs = self._plumb.normalize(raw) if self.normalize_obs else raw
         else:
-            act = torch.from_numpy(np.asarray(a, dtype=np.float32).reshape(1, -1))
-        shm_res = self._shm_step(weights) if (self.use_shm and self.shm is not None) else None
-        if shm_res is not None:
-            next_obs, raw, reward, _ = shm_res
-        else:
-            obs_t, rew_t, _, info_t = self._vec.step(act, raw_obs=True)
-            next_obs = obs_t[0].cpu().numpy()
-            raw = info_t["raw_obs"][0].cpu().numpy()
-            reward = float(rew_t[0].item())
-        obs_dict = self._array_to_dict(raw)
+            a = np.asarray(action)
+            if self.action_type == "discrete":
+                act = np.array([int(x) for x in a.reshape(-1)], dtype=np.int64)
+            else:
+                act = np.asarray(a, dtype=np.float32).reshape(-1)
+            shm_res = self._shm_step(weights) if (self.use_shm and self.shm is not None) else None
+            if shm_res is not None:
+                next_obs, raw, reward, _ = shm_res
+            else:
+                next_obs, raw, reward = self._sim_step(act)
+            obs_dict = self._array_to_dict(raw)
+        self._last_raw = raw
         # the reference sets last_observation only in SHM mode (env.py:201,249); problem-05's
         # get_state() relies on it staying None in simulation (multi_agent_env.py:249-254)
         self._last_obs_dict = obs_dict
@@ -531,10 +651,14 @@ class LoadBalanceEnv:
         if self.shm is not None:
             self.shm.close()
             self.shm = None
-        self._vec.close()
+        if self._vec is not None:
+            self._vec.close()
 
-    def seed(self, seed: Optional[int] = None):
-        self._vec.seed(seed)
+    def seed(self, seed: Optional[int] = None):  # env.py:327-330
+        if self._plumb is not None:
+            self._plumb.seed(seed)
+        else:
+            self._vec.seed(seed)
         return [seed]
 
     # ---- reference helpers (host plumbing, env.py:334-423)

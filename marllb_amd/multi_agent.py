@@ -59,12 +59,13 @@ class MultiAgentLoadBalanceEnv:
 
     def reset(self) -> List[np.ndarray]:
         g = self.env.reset()
-        self._server_loads = [float(x) for x in g[:, 0]]
+        self._server_loads = [float(x) for x in self.env._last_raw[:, 0]]
         return [self._get_agent_observation(g, i) for i in range(self.num_agents)]
 
     def step(self, actions):
         g, reward, done, info = self.env.step(self._combine_actions(actions))
-        self._server_loads = [float(x) for x in g[:, 0]]
+        # raw n_flow_on (not the normalised column) of this step
+        self._server_loads = [float(x) for x in self.env._last_raw[:, 0]]
         info = dict(info)
         info["server_loads"] = list(self._server_loads)  # FIX 2
         obs = [self._get_agent_observation(g, i) for i in range(self.num_agents)]
@@ -173,11 +174,17 @@ class VecMultiAgentLoadBalanceEnv:
 
     def step(self, actions):
         torch = _torch()
-        obs, rew, done, info = self.vec.step(self.expand_actions(actions))
+        v = self.vec
+        # server loads are this step's raw n_flow_on: the un-normalised column, and for envs the
+        # masked auto-reset restarts, the terminal step's value (not the next episode's first
+        # obs, which step() writes over `obs`).  raw_obs is requested only when they can differ.
+        need_raw = bool(v.cfg.normalize_obs) or (
+            v.autoreset and v._step_bound + 1 >= v.cfg.max_steps)
+        obs, rew, done, info = v.step(self.expand_actions(actions), raw_obs=need_raw)
         self._ep_len = info["episode_length"].to(torch.int32)
-        if self.vec.autoreset:  # out of place: info["episode_length"] keeps the finished length
+        if v.autoreset:  # out of place: info["episode_length"] keeps the finished length
             self._ep_len = self._ep_len.masked_fill(done, 0)
-        loads = obs[:, :, 0]
+        loads = (info["raw_obs"] if need_raw else obs)[:, :, 0]
         info = dict(info)
         info["server_loads"] = loads
         if self.global_reward:

@@ -186,6 +186,33 @@ def _pad_vec(v: torch.Tensor, n: int) -> torch.Tensor:
 profile_events: Optional[list] = None
 
 
+class _ParamWatch:
+    """Notices when the torch modules behind a fused form change their weights: every in-place
+    update (optimizer.step, load_state_dict, copy_) bumps a parameter's version counter, and a
+    re-registered parameter changes identity.  The fused forms keep packed COPIES of the weights,
+    so they check this before each launch and repack in place (same device pointers) when needed.
+    Assigning `param.data = ...` bypasses the counter: call sync_weights() after that."""
+
+    def __init__(self, modules):
+        self.params = [p for m in modules for p in m.parameters()]
+        self.sig = self._sig()
+
+    def _sig(self):
+        return [(id(p), p._version) for p in self.params]
+
+    def changed(self) -> bool:
+        s = self._sig()
+        if s == self.sig:
+            return False
+        self.sig = s
+        return True
+
+
+def _copy_into(dst, src):
+    for d, x in zip(dst, src):
+        d.copy_(x)
+
+
 def _timed(launch):
     if profile_events is None:
         return launch()
@@ -208,27 +235,45 @@ class FusedGRUPolicy:
     def __init__(self, policy: GRUPolicy, seed: int = 0, kernel: bool = True):
         g = policy.gru
         self.p = policy
+        # views of the module's parameters (the GEMM form follows in-place updates by itself)
         self.w_ih, self.b_ih = g.weight_ih_l0.detach(), g.bias_ih_l0.detach()
         self.w_hh, self.b_hh = g.weight_hh_l0.detach(), g.bias_hh_l0.detach()
         self.w1, self.b1 = policy.fc1.weight.detach(), policy.fc1.bias.detach()
-        self.wh = torch.cat([policy.fc_mean.weight, policy.fc_logstd.weight]).detach().contiguous()
-        self.bh = torch.cat([policy.fc_mean.bias, policy.fc_logstd.bias]).detach().contiguous()
+        self.wh, self.bh = self._heads()
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         self.step_no = 0
         self.kernel = None
         if (kernel and self.w_ih.is_cuda and policy.gru_dim == 128 and policy.hidden_dim == 256
                 and policy.action_dim <= 16 and policy.state_dim <= 512):
             self.kernel = self._pack()
+        self._watch = _ParamWatch([policy])
+
+    def _heads(self):
+        p = self.p
+        return (torch.cat([p.fc_mean.weight, p.fc_logstd.weight]).detach().contiguous(),
+                torch.cat([p.fc_mean.bias, p.fc_logstd.bias]).detach().contiguous())
+
+    def _pack_tensors(self):
+        return [pack_linear(self.w_ih), pack_linear(self.w_hh), self.b_ih.contiguous(),
+                self.b_hh.contiguous(), pack_linear(self.w1), self.b1.contiguous(),
+                pack_linear(self.wh), _pad_vec(self.bh, -(-2 * self.p.action_dim // 16) * 16)]
 
     def _pack(self):
         from . import _lib
         p = self.p
-        self._packed = [pack_linear(self.w_ih), pack_linear(self.w_hh), self.b_ih.contiguous(),
-                        self.b_hh.contiguous(), pack_linear(self.w1), self.b1.contiguous(),
-                        pack_linear(self.wh), _pad_vec(self.bh, -(-2 * p.action_dim // 16) * 16)]
+        self._packed = [t.clone() for t in self._pack_tensors()]  # own storage: stable pointers
         return _lib.SacActor(p.state_dim, p.gru_dim, p.hidden_dim, p.action_dim,
                              *[t.data_ptr() for t in self._packed], float(p.log_std_min),
                              float(p.log_std_max), float(p.action_scale), float(p.action_bias))
+
+    @torch.no_grad()
+    def sync_weights(self) -> None:
+        """Re-read the module's weights into the concatenated heads and the packed buffers, in
+        place (the kernel keeps its device pointers).  Called automatically before a launch when
+        a parameter changed (optimizer step, load_state_dict)."""
+        _copy_into((self.wh, self.bh), self._heads())
+        if self.kernel is not None:
+            _copy_into(self._packed, self._pack_tensors())
 
     @torch.no_grad()
     def __call__(self, state: torch.Tensor, hidden: torch.Tensor, deterministic: bool = False,
@@ -239,6 +284,8 @@ class FusedGRUPolicy:
         inplace: hidden_new is `hidden` itself, updated in place."""
         from . import _lib
         B, A = state.shape[0], self.p.action_dim
+        if self._watch.changed():
+            self.sync_weights()
         lib, stream = _lib_and_stream(state.device)
         action = torch.empty((B, A), dtype=torch.float32, device=state.device)
         log_std = torch.empty_like(action)
@@ -294,10 +341,22 @@ class FusedQMIXPolicy:
             raise ValueError("FusedQMIXPolicy: layer widths not built into lbsim_qmix_policy_step")
         self.A, self.n_actions, self.k = len(agents), n_actions, servers_per_agent
         self.H = agents[0].gru_dim
-        cat = lambda f: torch.cat([f(a).reshape(-1) for a in agents]).contiguous()  # noqa: E731
+        self.agents, self.mixer = list(agents), mixer
+        self._packed = [t.clone() for t in self._pack_tensors()]  # own storage: stable pointers
         m = mixer
+        self.net = _lib.QmixPolicy(self.A, agents[0].obs_dim, self.H, agents[0].hidden_dim,
+                                   n_actions, m.state_dim, m.mixing_embed_dim,
+                                   m.hypernet_embed_dim, servers_per_agent, float(epsilon),
+                                   *[t.data_ptr() for t in self._packed])
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.step_no = 0
+        self._watch = _ParamWatch(self.agents + [mixer])
+
+    def _pack_tensors(self):
+        agents, m = self.agents, self.mixer
+        cat = lambda f: torch.cat([f(a).reshape(-1) for a in agents]).contiguous()  # noqa: E731
         first = [m.hyper_w1[0], m.hyper_w2[0], m.hyper_b2[0], m.hyper_b1[0]]
-        self._packed = [
+        return [
             cat(lambda a: pack_linear(a.gru.weight_ih_l0)),
             cat(lambda a: pack_linear(a.gru.weight_hh_l0)),
             cat(lambda a: a.gru.bias_ih_l0.detach()), cat(lambda a: a.gru.bias_hh_l0.detach()),
@@ -309,12 +368,11 @@ class FusedQMIXPolicy:
             pack_linear(m.hyper_w1[2].weight), m.hyper_w1[2].bias.detach().contiguous(),
             pack_linear(m.hyper_w2[2].weight), m.hyper_w2[2].bias.detach().contiguous(),
             pack_linear(m.hyper_b2[2].weight, 16), _pad_vec(m.hyper_b2[2].bias, 16)]
-        self.net = _lib.QmixPolicy(self.A, agents[0].obs_dim, self.H, agents[0].hidden_dim,
-                                   n_actions, m.state_dim, m.mixing_embed_dim,
-                                   m.hypernet_embed_dim, servers_per_agent, float(epsilon),
-                                   *[t.data_ptr() for t in self._packed])
-        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
-        self.step_no = 0
+
+    @torch.no_grad()
+    def sync_weights(self) -> None:
+        """Repack the agents' and mixer's weights in place (automatic when they change)."""
+        _copy_into(self._packed, self._pack_tensors())
 
     @torch.no_grad()
     def __call__(self, obs: torch.Tensor, hidden: torch.Tensor, state: torch.Tensor,
@@ -325,6 +383,8 @@ class FusedQMIXPolicy:
         B, dev = obs.shape[0], obs.device
         if not (hidden.is_contiguous() and hidden.shape == (B, self.A, self.H)):
             raise ValueError("hidden must be a contiguous (B, A, gru) tensor")
+        if self._watch.changed():
+            self.sync_weights()
         lib, stream = _lib_and_stream(dev)
         acts = torch.empty((B, self.A), dtype=torch.int64, device=dev)
         sacts = torch.empty((B, self.A * self.k), dtype=torch.int32, device=dev)
@@ -346,22 +406,34 @@ class FusedAgentQNets:
     over the stacked agent weights, GRU gates in lbsim_gru_gates."""
 
     def __init__(self, agents):
-        st = lambda f: torch.stack([f(a).detach() for a in agents]).contiguous()  # noqa: E731
+        self.agents = list(agents)
         self.A = len(agents)
         self.H = agents[0].gru_dim
-        self.w_ih = st(lambda a: a.gru.weight_ih_l0.t())  # (A, I, 3H)
-        self.b_ih = st(lambda a: a.gru.bias_ih_l0).unsqueeze(1)
-        self.w_hh = st(lambda a: a.gru.weight_hh_l0.t())
-        self.b_hh = st(lambda a: a.gru.bias_hh_l0).unsqueeze(1)
-        self.w1, self.b1 = st(lambda a: a.fc1.weight.t()), st(lambda a: a.fc1.bias).unsqueeze(1)
-        self.w2, self.b2 = st(lambda a: a.fc2.weight.t()), st(lambda a: a.fc2.bias).unsqueeze(1)
-        self.w3, self.b3 = st(lambda a: a.fc3.weight.t()), st(lambda a: a.fc3.bias).unsqueeze(1)
+        (self.w_ih, self.b_ih, self.w_hh, self.b_hh, self.w1, self.b1, self.w2, self.b2,
+         self.w3, self.b3) = self._stacked()
+        self._watch = _ParamWatch(self.agents)
+
+    def _stacked(self):
+        st = lambda f: torch.stack([f(a).detach() for a in self.agents]).contiguous()  # noqa: E731
+        return (st(lambda a: a.gru.weight_ih_l0.t()),  # (A, I, 3H)
+                st(lambda a: a.gru.bias_ih_l0).unsqueeze(1),
+                st(lambda a: a.gru.weight_hh_l0.t()), st(lambda a: a.gru.bias_hh_l0).unsqueeze(1),
+                st(lambda a: a.fc1.weight.t()), st(lambda a: a.fc1.bias).unsqueeze(1),
+                st(lambda a: a.fc2.weight.t()), st(lambda a: a.fc2.bias).unsqueeze(1),
+                st(lambda a: a.fc3.weight.t()), st(lambda a: a.fc3.bias).unsqueeze(1))
+
+    @torch.no_grad()
+    def sync_weights(self) -> None:
+        _copy_into((self.w_ih, self.b_ih, self.w_hh, self.b_hh, self.w1, self.b1, self.w2,
+                    self.b2, self.w3, self.b3), self._stacked())
 
     @torch.no_grad()
     def __call__(self, obs: torch.Tensor, hidden: torch.Tensor):
         """obs (A, B, I), hidden (A, B, H) -> q (A, B, n_actions), hidden_new (A, B, H)."""
         from . import _lib
         A, B, H = obs.shape[0], obs.shape[1], self.H
+        if self._watch.changed():
+            self.sync_weights()
         lib, stream = _lib_and_stream(obs.device)
         gi = torch.baddbmm(self.b_ih, obs, self.w_ih)
         gh = torch.baddbmm(self.b_hh, hidden, self.w_hh)
@@ -379,20 +451,32 @@ class FusedQMixer:
 
     def __init__(self, mixer: QMixer):
         m = mixer
+        self.m = m
         self.A, self.E = m.num_agents, m.mixing_embed_dim
-        firsts = [m.hyper_w1[0], m.hyper_b1[0], m.hyper_w2[0], m.hyper_b2[0]]
-        self.w0 = torch.cat([l.weight for l in firsts]).detach().contiguous()
-        self.b0 = torch.cat([l.bias for l in firsts]).detach().contiguous()
+        self.w0, self.b0 = self._firsts()
         he = m.hypernet_embed_dim
         self.cuts = [he, he + self.E, 2 * he + self.E, 3 * he + self.E]
         self.w1, self.bw1 = m.hyper_w1[2].weight.detach(), m.hyper_w1[2].bias.detach()
         self.w2, self.bw2 = m.hyper_w2[2].weight.detach(), m.hyper_w2[2].bias.detach()
         self.wb2, self.bb2 = m.hyper_b2[2].weight.detach(), m.hyper_b2[2].bias.detach()
+        self._watch = _ParamWatch([m])
+
+    def _firsts(self):
+        m = self.m
+        firsts = [m.hyper_w1[0], m.hyper_b1[0], m.hyper_w2[0], m.hyper_b2[0]]
+        return (torch.cat([l.weight for l in firsts]).detach().contiguous(),
+                torch.cat([l.bias for l in firsts]).detach().contiguous())
+
+    @torch.no_grad()
+    def sync_weights(self) -> None:
+        _copy_into((self.w0, self.b0), self._firsts())  # the other layers are views
 
     @torch.no_grad()
     def __call__(self, agent_qs: torch.Tensor, state: torch.Tensor) -> torch.Tensor:
         from . import _lib
         B = agent_qs.shape[0]
+        if self._watch.changed():
+            self.sync_weights()
         lib, stream = _lib_and_stream(state.device)
         z = torch.addmm(self.b0, state, self.w0.t())  # [hw1 | b1 | hw2 | hb2] pre-activation
         c0, c1, c2, c3 = self.cuts

@@ -86,3 +86,21 @@ def test_two_rank_gpu_shards_equal_single_process_oracle(tmp_path, oracle_mod):
     obs, rew = single_process_reference(oracle_mod, 2)
     np.testing.assert_array_equal(res["obs"], obs)
     np.testing.assert_array_equal(res["rew"], rew)
+
+
+@pytest.mark.gpu
+def test_bench_self_launches_ranks():
+    """`bench.py --gpus 2` without torchrun starts its own two rank processes (the driver's
+    multi-GPU contract); gloo for the measurement collectives so both ranks may share one card.
+    Rank 0 prints exactly one JSON line with n_gpus = 2 and the global batch of both shards."""
+    import json
+    root = os.path.dirname(HERE)
+    env = dict(os.environ, LBSIM_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps",
+                        "3", "--warmup", "1", "--batch", "2048"], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 4096 and out["value"] > 0

@@ -232,3 +232,95 @@ def test_shm_mode_reads_published_frames():
         env.close()
     finally:
         pub.close()
+
+
+# ---- the 1 x 4 GPU facade against the oracle, episode/info semantics against the reference golden
+def test_single_env_facade_vs_oracle_and_episode_golden(oracle_mod, golden_dir):
+    """LoadBalanceEnv (B=1 on the GPU) stepped past max_steps equals oracle.OracleEnv(B=1) on
+    every observation and reward, and its done / info / info['episode'] follow the reference's
+    recorded episode (env_plumbing.json['episode'], env.py:262-286 with max_steps=5, 7 steps)."""
+    import json
+    import os
+
+    from marllb_amd import LoadBalanceEnv
+    from marllb_amd.env import make_config
+    gold = json.load(open(os.path.join(golden_dir, "env_plumbing.json")))["episode"]
+    env = make(num_servers=4, max_steps=5, seed=42, step_interval=0.0)
+    ora = oracle_mod.OracleEnv(make_config(1, 4, seed=42, max_steps=5), threads=1)
+    np.testing.assert_array_equal(env.reset(), ora.reset()[0])
+    total = 0.0
+    act = np.array([0, 1, 2, 1])
+    for g in gold:
+        obs, r, done, info = env.step(act)
+        oo, ro, do, _ = ora.step(act[None].astype(np.int64))
+        np.testing.assert_array_equal(obs, oo[0])
+        assert r == float(ro[0])
+        total += r
+        assert done == g["done"] and info["step"] == g["info_step"] == g["step"]
+        assert sorted(k for k in info if k != "episode") == \
+            [k for k in g["info_keys"] if k != "episode"]
+        assert ("episode" in info) == g["has_episode"]
+        if g["has_episode"]:
+            assert info["episode"]["l"] == g["episode_l"]
+            assert info["episode"]["r"] == pytest.approx(total, abs=0, rel=1e-12)
+        assert isinstance(env, LoadBalanceEnv)
+
+
+def test_single_env_normalized_matches_oracle(oracle_mod):
+    """normalize_obs through the single-transfer step path: obs normalised on the device, reward
+    and active servers from the raw row (oracle normalises with the same f64 statistics)."""
+    from marllb_amd.env import make_config
+    env = make(num_servers=4, normalize_obs=True, seed=9, action_type="continuous")
+    ora = oracle_mod.OracleEnv(make_config(1, 4, seed=9, normalize_obs=True,
+                                           action_type="continuous"), threads=1)
+    np.testing.assert_array_equal(env.reset(), ora.reset()[0])
+    rng = np.random.default_rng(4)
+    for _ in range(4):
+        a = rng.uniform(-1, 3, 4).astype(np.float32)
+        obs, r, _, info = env.step(a)
+        oo, ro, _, _ = ora.step(a[None])
+        np.testing.assert_array_equal(obs, oo[0])
+        assert r == float(ro[0])
+
+
+def test_shm_fallback_when_producer_is_idle():
+    """use_shm=True: a step that finds no new frame falls back to the simulator (env.py:246-254)
+    instead of raising; the SHM reset already reset the simulator."""
+    import uuid
+
+    from marllb_amd import LoadBalanceEnv, VecLoadBalanceEnv
+    from marllb_amd.shm import ShmPublisher
+    prefix = f"lbsim_f_{uuid.uuid4().hex[:8]}_"
+    vec = VecLoadBalanceEnv(1, 4, device="cuda:0", seed=3, autoreset=False)
+    pub = ShmPublisher(vec, prefix)
+    try:
+        pub.publish(vec.reset())
+        env = LoadBalanceEnv(num_servers=4, use_shm=True, shm_name=prefix + "0",
+                             step_interval=0.0, seed=1, normalize_obs=True)
+        env.reset()
+        for k in range(3):  # the producer never publishes again
+            obs, r, done, info = env.step(np.array([0, 1, 2, 1]))
+            assert obs.shape == (4, 11) and np.all(np.isfinite(obs)) and info["step"] == k + 1
+            assert isinstance(r, float) and np.isfinite(r)
+        assert env._norm[0] == 4  # one host running statistic over the frame and 3 fallbacks
+        env.close()
+    finally:
+        pub.close()
+
+
+def test_reset_mask_validation():
+    from marllb_amd import VecLoadBalanceEnv
+    env = VecLoadBalanceEnv(32, 4, device="cuda:0", seed=1)
+    env.reset()
+    with pytest.raises(ValueError, match="num_envs"):
+        env.reset(mask=torch.ones(16, dtype=torch.bool))
+    with pytest.raises(ValueError, match="bool or uint8"):
+        env.reset(mask=torch.ones(32, dtype=torch.float32))
+    env.reset(mask=torch.zeros(32, dtype=torch.bool, device="cuda:0"))
+    with pytest.raises(ValueError, match="expected 32 x 4"):
+        env.step(torch.zeros((32, 3), dtype=torch.int64))
+    strict = VecLoadBalanceEnv(8, 4, device="cuda:0", seed=1, strict_actions=True)
+    strict.reset()
+    with pytest.raises(IndexError):
+        strict.step(torch.full((8, 4), 3, dtype=torch.int64))
+    strict.step(torch.full((8, 4), -3, dtype=torch.int64))  # python indexing: -n is valid

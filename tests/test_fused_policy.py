@@ -177,3 +177,90 @@ def test_other_tile_forms_match_modules(env):
                        cwd=root, env={**os.environ, **env}, capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+@pytest.mark.gpu
+def test_fused_forms_follow_weight_updates(g):
+    """An optimizer step or load_state_dict on the torch modules reaches the packed copies the
+    fused kernels read (version-counter check before each launch; sync_weights() by hand)."""
+    dev = "cuda:0"
+    pol = load_prefixed(GRUPolicy(88, 8, 256, 128), g, "policy").to(dev)
+    gen = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(64, 88, device=dev, generator=gen)
+    h = torch.randn(64, 128, device=dev, generator=gen) * 0.5
+    for kernel in (True, False):
+        f = FusedGRUPolicy(pol, kernel=kernel)
+        a0, _, _ = f(x, h, deterministic=True)
+        opt = torch.optim.SGD(pol.parameters(), lr=0.5)
+        mean, _, _ = pol(x, h.unsqueeze(0))
+        mean.sum().backward()
+        opt.step()
+        opt.zero_grad()
+        a1, h1, ls1 = f(x, h, deterministic=True)
+        with torch.no_grad():
+            m1, l1, rh1 = pol(x, h.unsqueeze(0))
+        assert not torch.allclose(a0, a1)
+        close(a1, torch.tanh(m1))
+        close(h1, rh1[0])
+        close(ls1, l1)
+    agents = [load_prefixed(AgentQNet(128, 3, 128, 64), g, "agentq").to(dev) for _ in range(4)]
+    mix = load_prefixed(QMixer(4, 74, 32, 64), g, "mixer").to(dev)
+    B = 48
+    obs = torch.randn(B, 4, 128, device=dev, generator=gen)
+    hid = torch.randn(B, 4, 64, device=dev, generator=gen) * 0.5
+    state = torch.randn(B, 74, device=dev, generator=gen)
+    qp = FusedQMIXPolicy(agents, mix, 3, epsilon=0.0, seed=1, servers_per_agent=4)
+    _, _, qt0, q0 = qp(obs, hid.clone(), state, q_values=True)
+    new = QMixer(4, 74, 32, 64).to(dev)
+    mix.load_state_dict(new.state_dict())
+    with torch.no_grad():
+        agents[2].fc3.weight.mul_(-2.0)
+    acts, _, qt1, q1 = qp(obs, hid.clone(), state, q_values=True)
+    with torch.no_grad():
+        rq, _ = agents[2](obs[:, 2], hid[:, 2].unsqueeze(0).contiguous())
+        close(q1[:, 2], rq)
+        close(qt1, mix(q1.gather(2, acts.unsqueeze(2)).squeeze(2), state))
+    assert not torch.allclose(qt0, qt1)
+
+
+@pytest.mark.gpu
+def test_fused_kernels_full_shard_vs_modules(g):
+    """Full per-GPU shards of configs[3] and configs[4] (SAC-GRU 65536 x 8; QMIX 8192 envs x 4
+    agents over 16 servers) against the torch modules, every row, within 1e-5 (greedy actions;
+    argmax compared where the top two Q-values are 1e-4 apart)."""
+    dev = "cuda:0"
+    gen = torch.Generator(device=dev).manual_seed(11)
+    pol = load_prefixed(GRUPolicy(88, 8, 256, 128), g, "policy").to(dev)
+    B = 65536
+    x = torch.randn(B, 88, device=dev, generator=gen) * 2
+    h = torch.randn(B, 128, device=dev, generator=gen) * 0.5
+    mask = torch.rand(B, device=dev, generator=gen) < 0.1
+    with torch.no_grad():
+        mean, log_std, rh = pol(x, (h * (~mask).unsqueeze(1)).unsqueeze(0))
+    a, h1, ls = FusedGRUPolicy(pol)(x, h, deterministic=True, reset_mask=mask)
+    close(a, torch.tanh(mean))
+    close(h1, rh[0])
+    close(ls, log_std)
+    del x, h, mean, log_std, rh, a, h1, ls
+    agents = [load_prefixed(AgentQNet(128, 3, 128, 64), g, "agentq").to(dev) for _ in range(4)]
+    with torch.no_grad():
+        for k, ag in enumerate(agents[1:], 1):
+            for p in ag.parameters():
+                p.mul_(1.0 - 0.07 * k)
+    mix = load_prefixed(QMixer(4, 74, 32, 64), g, "mixer").to(dev)
+    B = 8192
+    obs = torch.randn(B, 4, 128, device=dev, generator=gen)
+    hid = torch.randn(B, 4, 64, device=dev, generator=gen) * 0.5
+    state = torch.randn(B, 74, device=dev, generator=gen)
+    qp = FusedQMIXPolicy(agents, mix, 3, epsilon=0.0, seed=3, servers_per_agent=4)
+    hk = hid.clone()
+    acts, _, q_tot, q = qp(obs, hk, state, q_values=True)
+    with torch.no_grad():
+        for ai, net in enumerate(agents):
+            rq, rh = net(obs[:, ai], hid[:, ai].unsqueeze(0).contiguous())
+            close(q[:, ai], rq)
+            close(hk[:, ai], rh[0])
+            top2 = rq.topk(2, dim=1).values
+            clear = (top2[:, 0] - top2[:, 1]) > 1e-4
+            assert torch.equal(acts[clear, ai], rq.argmax(1)[clear])
+        close(q_tot, mix(q.gather(2, acts.unsqueeze(2)).squeeze(2), state))

@@ -77,3 +77,47 @@ def test_vec_agent_obs_kernel_and_actions():
     st = envs[0].get_state()
     assert st.shape == (B, 74) and torch.all(st[:, -1] == 4)
     assert r1.shape == (B, A) and torch.all(r1 == r1[:, :1])
+
+
+def test_agent_obs_kernel_vs_reference_wrapper(golden_dir):
+    """lbsim_agent_obs on the global observations the reference wrapper saw equals
+    multi_agent_env.py:152-188's per-agent output (recorded by tests/golden/gen_plumbing.py)."""
+    import json
+    import os
+
+    from marllb_amd import VecMultiAgentLoadBalanceEnv
+    meta = json.load(open(os.path.join(golden_dir, "plumbing.json")))
+    for case in meta["multi_agent"]:
+        A, k = case["num_agents"], case["servers_per_agent"]
+        env = VecMultiAgentLoadBalanceEnv(4, A, k, device="cuda:0", seed=1)
+        g = torch.tensor(case["global_obs"], dtype=torch.float32, device="cuda:0")  # (T, S, 11)
+        got = env.agent_obs(g).cpu().numpy()
+        want = np.array([st["obs"] for st in case["steps"]], np.float64).astype(np.float32)
+        np.testing.assert_array_equal(got, want)
+        env.close()
+
+
+def test_vec_terminal_step_local_rewards():
+    """global_reward=False: on the step that ends an episode the local Jain rewards and
+    info['server_loads'] come from that step's raw n_flow_on, not from the auto-reset's next
+    first observation (and not from normalised values)."""
+    from marllb_amd import VecLoadBalanceEnv, VecMultiAgentLoadBalanceEnv
+    B, A, k, T = 64, 4, 4, 3
+    kw = dict(device="cuda:0", seed=21, action_type="discrete", max_steps=T, normalize_obs=True)
+    m = VecMultiAgentLoadBalanceEnv(B, A, k, global_reward=False, **kw)
+    ref = VecLoadBalanceEnv(B, A * k, autoreset=False, **kw)
+    m.reset()
+    ref.reset()
+    a = torch.randint(0, 3, (B, A), device="cuda:0", generator=torch.Generator("cuda").manual_seed(0))
+    for t in range(T + 1):
+        _, rew, done, info = m.step(a)
+        _, _, _, ri = ref.step(a.repeat_interleave(k, dim=1), raw_obs=True)
+        loads = ri["raw_obs"][:, :, 0]
+        if t == T - 1:
+            assert bool(done.all())
+        if t < T:  # ref (no autoreset) and m agree until m's envs restart
+            assert torch.equal(info["server_loads"], loads)
+            l = loads.double().view(B, A, k)
+            s, sq = l.sum(2), (l * l).sum(2)
+            want = torch.where(s == 0, torch.zeros_like(s), s * s / (k * sq + 1e-8)).float()
+            assert torch.equal(rew, want)
