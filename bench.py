@@ -127,7 +127,11 @@ def cpu_baseline(args, seconds: float):
 
     import oracle
     from marllb_amd.env import LoadBalanceEnv, make_config
-    model, threads, quota = _cpu_info()
+    model, affinity, quota = _cpu_info()
+    # every CPU this process may use: the affinity set, capped by the cgroup quota (on the GPU
+    # box the affinity mask lists the whole machine, 256, but cpu.max grants 16; 256 threads on
+    # 16 CPUs of quota run 4x slower than 16 threads: throttling, not the host's capability)
+    threads = affinity if quota is None else max(1, min(affinity, int(quota + 0.999)))
     nb = max(2048, 64 * threads)
     cfg = make_config(nb, args.servers, seed=args.seed, env_id_offset=0)
     ora = oracle.OracleEnv(cfg, threads=threads)
@@ -154,10 +158,11 @@ def cpu_baseline(args, seconds: float):
         m += 1
     pel = time.perf_counter() - t1
     return {"value": nb * n / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "cpu_model": model, "cgroup_cpu_quota": quota,
+            "cpu_model": model, "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
             "sample": f"{nb} of the {args.batch} envs (global ids 0-{nb - 1}), S={args.servers}, "
                       f"{n} random-policy steps, {el:.1f} s, oracle/lbsim_oracle.c "
-                      f"(OpenMP, {threads} threads = every core in sched_getaffinity) on {model}",
+                      f"(OpenMP, {threads} threads = every CPU available: sched_getaffinity "
+                      f"{affinity}, cgroup quota {quota}) on {model}",
             "reference_plumbing": {
                 "value": m / pel, "unit": "env-steps/s/core", "cores": 1, "kind": "port",
                 "what": "the reference's own LoadBalanceEnv.step in simulation mode (random "

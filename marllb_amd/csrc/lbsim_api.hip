@@ -263,13 +263,14 @@ void launch_dyn_policy(lbsim_t* h, bool g, const void* action, int dtype, int32_
 }
 
 // Mapping choice (LBSIM_DYN_AUTO): one lane per env when that fills every SIMD with at least one
-// wave and an env has at most 4 servers; otherwise one lane per server.  Measured
-// (profiles/r01s2e_group/mapping_sweep.txt): server-per-lane wins up to 32768 x 4 and at S = 16,
-// ties at 65536 x 8 and loses at 65536 x 4 (0.296 vs 0.256 ms).
+// wave and an env has at most 8 servers; otherwise one lane per server.  Measured
+// with the round-2 event loop (profiles/r02h_mapping.jsonl): env-per-lane wins at 65536 x 8
+// (Poisson 0.320 vs 0.392 ms, configs[2] trace replay 0.385 vs 0.430 ms) and 65536 x 4;
+// server-per-lane wins up to 32768 x 4 (0.200 vs 0.208 ms) and at S = 16.
 bool server_per_lane(const lbsim_t* h) {
   if (h->cfg.dyn_mapping == LBSIM_DYN_ENV_PER_LANE) return false;
   if (h->cfg.dyn_mapping == LBSIM_DYN_SERVER_PER_LANE) return true;
-  return h->S > 4 || (int64_t)(h->B + 63) / 64 < (int64_t)h->simds;
+  return h->S > 8 || (int64_t)(h->B + 63) / 64 < (int64_t)h->simds;
 }
 
 template <int MODE>

@@ -125,7 +125,7 @@ enum SrvField {
   F_TAIL = 0,  // t_complete of the last queued flow (valid if cnt > 0)
   F_RCNT,      // Algorithm R count of the server's reservoirs
   F_ASSIGNED,  // arrivals assigned this launch (assign_count_out)
-  F_SCALE,     // service-time scale (us per unit work) of the server, f32 bits
+  F_SCALE,     // (unused by the env-per-lane loop: service scales are VGPR constants)
   F_TAB0,      // ALIAS table of this step, active position s: odd (f32 bits)
   F_TAB1,      //   alias | server << 8
   F_NUM
@@ -378,6 +378,327 @@ __device__ __forceinline__ int reservoir_slot(uint32_t cres, const u32x4& d) {
 
 __device__ __forceinline__ uint32_t count_inc(uint32_t c) { return c != 0xFFFFFFFFu ? c + 1u : c; }
 
+// Loop constants of one step, pinned in VGPRs.  At one wave per SIMD most of the 512 VGPRs are
+// free, while SGPRs are scarce (the Philox round keys alone take 20): constants left in SGPRs were
+// re-loaded from the kernarg segment inside the loop (s_load + s_waitcnt lgkmcnt(0), which also
+// waits for every LDS access in flight).  vpin() makes a uniform value a VGPR the compiler cannot
+// rematerialise from memory.
+__device__ __forceinline__ uint32_t vpin(uint32_t x) {
+  uint32_t r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+__device__ __forceinline__ float vpin(float x) { return __uint_as_float(vpin(__float_as_uint(x))); }
+__device__ __forceinline__ int32_t vpin(int32_t x) { return (int32_t)vpin((uint32_t)x); }
+
+template <int MAXS>
+struct EvConst {
+  uint32_t rk0[10], rk1[10];  // Philox round keys
+  float mean_gap, scale[MAXS];
+  int32_t dt, S, Q;
+  uint32_t base_ms, base_rem;
+};
+
+template <int MAXS>
+__device__ __forceinline__ EvConst<MAXS> ev_const(const SimParams& p, uint32_t base_ms,
+                                                   uint32_t base_rem) {
+  EvConst<MAXS> c;
+  uint32_t k0 = p.key0, k1 = p.key1;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    c.rk0[r] = vpin(k0);
+    c.rk1[r] = vpin(k1);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  c.mean_gap = vpin(p.mean_gap_us);
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) c.scale[s] = vpin(s < p.S ? p.svc_scale[s] : 1.0f);
+  c.dt = vpin(p.dt_us);
+  c.S = p.S;
+  c.Q = p.Q;
+  c.base_ms = vpin(base_ms);
+  c.base_rem = vpin(base_rem);
+  return c;
+}
+
+// Philox4x32-10 with precomputed round keys (same bits as philox4x32_10).
+__device__ __forceinline__ u32x4 philox_rk(u32x4 c, const uint32_t (&rk0)[10],
+                                           const uint32_t (&rk1)[10]) {
+  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)M0 * c.x;
+    const uint64_t p1 = (uint64_t)M1 * c.z;
+    // hi ^ y ^ k as one v_bitop3_b32 (truth table 0x96 = a ^ b ^ c)
+    c = u32x4{(uint32_t)__builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c.y, rk0[r], 0x96),
+              (uint32_t)p1,
+              (uint32_t)__builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c.w, rk1[r], 0x96),
+              (uint32_t)p0};
+  }
+  return c;
+}
+
+// The event loop of sim_step (section 2, specification in the comment block below).
+//  * every server's next-head LDS read is issued at the top of the iteration, before anything
+//    branches, so the S reads are in flight together; the rare refill of a queue longer than the
+//    window is one branch for all servers;
+//  * the chosen server's tail, Algorithm R count and assignment count are register arrays
+//    selected like cnt (REGF, MAXS <= 8), not dependent LDS round trips; service scales are
+//    VGPR constants;
+//  * FAST (wave-uniform): every SED score finite, so no NaN fallback and no "first eligible"
+//    variant of the argmin.
+template <int MAXS, int POLICY, bool TRACE, bool FAST>
+__device__ __forceinline__ void event_loop(const DevState& st, const SimParams& p,
+                                           LaneState<MAXS>& L, const Lds& l,
+                                           const EvConst<MAXS>& ec, const double (&den)[MAXS],
+                                           const double (&rcp)[MAXS], int n_alias,
+                                           uint3* const my_res, int2* const my_ring) {
+  constexpr int WL = LaneState<MAXS>::WL;
+  constexpr bool REGF = MAXS <= 8;
+  constexpr bool two_choice = (POLICY == 1 || POLICY == 3);
+  constexpr bool alias = POLICY == kPolicyAlias;
+  constexpr bool lsq = (POLICY == 2 || POLICY == 3);
+  const int S = ec.S, Q = ec.Q;
+  const int32_t dt = ec.dt;
+  int32_t tail[MAXS], asg[MAXS];
+  uint32_t rcnt[MAXS];
+  // hs[s]: the head's window slot without the wrap (lh + pops so far); the slot is hs & (WL - 1)
+  // and the ring position head + (hs - lh) mod Q is needed only on the rare ring paths and at the
+  // end, so a pop is one add instead of the lh / head wrap-and-select pairs
+  // (rbase[s] + hs[s] + k) mod Q is the ring position of queue entry k
+  int32_t hs[MAXS], rbase[MAXS];
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) {
+    hs[s] = L.lh[s];
+    rbase[s] = L.head[s] - L.lh[s] + Q;  // >= 1: lh < WL <= Q
+  }
+  if constexpr (REGF) {
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) {
+      tail[s] = s < S ? fld<MAXS>(l, F_TAIL, s) : 0;
+      rcnt[s] = s < S ? (uint32_t)fld<MAXS>(l, F_RCNT, s) : 0u;
+      asg[s] = 0;
+    }
+  }
+  for (;;) {
+    const bool arrival_due = L.next_arr < dt;
+    const int32_t th = arrival_due ? L.next_arr : dt;  // a completion at the arrival time goes first
+    int32_t nt[MAXS];
+    bool due[MAXS];
+    bool refill = false;
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) {
+      nt[s] = qslot<MAXS>(l, s, (hs[s] + 1) & (WL - 1))->x;  // next head (valid if cnt > 1)
+      due[s] = (s < S) & (L.cnt[s] > 0) & (L.head_tc[s] <= th);
+      refill |= due[s] & (L.cnt[s] - 1 >= WL);
+    }
+    if (refill) {  // rare: bring queue entry WL (ring) into the slot the pop frees
+#pragma unroll
+      for (int s = 0; s < MAXS; ++s) {
+        if (due[s] && L.cnt[s] - 1 >= WL)
+          *qslot<MAXS>(l, s, hs[s] & (WL - 1)) =
+              my_ring[(uint32_t)s * (uint32_t)Q + (uint32_t)(rbase[s] + hs[s] + WL) % (uint32_t)Q];
+      }
+      __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);  // drain in the rare branch, not at the back-edge
+    }
+    bool more = false;
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) {  // pop each server's head if it completed by th
+      L.last[s] = due[s] ? L.head_tc[s] : L.last[s];
+      L.cnt[s] -= due[s] ? 1 : 0;
+      hs[s] += due[s] ? 1 : 0;
+      L.head_tc[s] = due[s] ? nt[s] : L.head_tc[s];
+      more |= due[s] & (L.cnt[s] > 0) & (nt[s] <= th);
+    }
+    if (!arrival_due && !more) break;
+    const bool arr = arrival_due & !more;
+
+    // ---- the arrival: choose a server (node.c:388-441); full servers are not eligible
+    const int32_t ta = L.next_arr;
+    float score[MAXS];
+    if constexpr (!alias) {
+      bool bad = false;
+#pragma unroll
+      for (int s = 0; s < MAXS; ++s) {
+        if constexpr (lsq) {
+          score[s] = (float)L.cnt[s];
+        } else {  // (cnt + 1) / den correctly rounded by Markstein's corrected quotient
+          const double c = (double)(L.cnt[s] + 1);
+          const double q0 = c * rcp[s];
+          const double q = fma(fma(-q0, den[s], c), rcp[s], q0);
+          if constexpr (!FAST) bad |= q != q;
+          score[s] = (float)q;
+        }
+      }
+      if (!FAST && !lsq && bad) {  // den 0 / inf / NaN: the division
+#pragma unroll
+        for (int s = 0; s < MAXS; ++s) {
+          const float q = score[s];
+          if (q != q) score[s] = (float)((double)(L.cnt[s] + 1) / den[s]);
+        }
+      }
+    }
+    int chosen = -1;
+    if constexpr (alias) {  // full server: the flow is dropped (ALIAS has no eligibility test)
+      if (n_alias > 0) {
+        const int a = alias_pick(FieldAliasTab<MAXS>{l}, n_alias, L.u2);
+        chosen = sel<MAXS>(L.cnt, a) < Q ? a : -1;
+      }
+    } else if constexpr (two_choice) {  // SED2 / LSQ2: keep the second candidate if strictly better
+      const int h1 = (int)__umulhi(L.u2, (uint32_t)S);  // (u * S) >> 32
+      const int h2 = (int)__umulhi(L.u3, (uint32_t)S);
+      float s1 = 0.f, s2 = 0.f;
+      bool ok1 = false, ok2 = false;
+#pragma unroll
+      for (int s = 0; s < MAXS; ++s) {
+        s1 = (s == h1) ? score[s] : s1;
+        ok1 = (s == h1) ? (L.cnt[s] < Q) : ok1;
+        s2 = (s == h2) ? score[s] : s2;
+        ok2 = (s == h2) ? (L.cnt[s] < Q) : ok2;
+      }
+      chosen = (ok1 && ok2) ? ((s2 < s1) ? h2 : h1) : (ok1 ? h1 : (ok2 ? h2 : -1));
+    } else {  // SED / LSQ: start at the hashed server, replace on strictly lower score
+      const int h = (int)__umulhi(L.u2, (uint32_t)S);  // (u * S) >> 32
+      float best = __uint_as_float(0x7f800000u);  // +inf: any finite score replaces it
+#pragma unroll
+      for (int s = 0; s < MAXS; ++s) {
+        const bool m = (s == h) & (L.cnt[s] < Q);
+        chosen = m ? s : chosen;
+        best = m ? score[s] : best;
+      }
+      if (FAST || lsq) {  // every score finite: "replace on strictly lower" from +inf is exact
+#pragma unroll
+        for (int s = 0; s < MAXS; ++s) {
+          const bool m = (s < S) & (L.cnt[s] < Q) & (score[s] < best);
+          chosen = m ? s : chosen;
+          best = m ? score[s] : best;
+        }
+      } else {  // NaN / inf scores: the first eligible server is taken whatever its score
+#pragma unroll
+        for (int s = 0; s < MAXS; ++s) {
+          const bool m = (s < S) & (L.cnt[s] < Q) & ((chosen < 0) | (score[s] < best));
+          chosen = m ? s : chosen;
+          best = m ? score[s] : best;
+        }
+      }
+    }
+    const bool push = arr && chosen >= 0;
+    L.dropped += (arr && chosen < 0) ? 1u : 0u;
+
+    // ---- the chosen server: FIFO service starts when its last queued flow ends
+    const int cs = push ? chosen : 0;
+    int32_t c_cnt = 0, c_hs = 0, c_rb = 0, c_tail = 0;
+    uint32_t cres = 0u;
+    float c_scale = 1.0f;
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) {
+      const bool m = s == cs;
+      c_cnt = m ? L.cnt[s] : c_cnt;
+      c_hs = m ? hs[s] : c_hs;
+      c_rb = m ? rbase[s] : c_rb;
+      c_scale = m ? ec.scale[s] : c_scale;
+      if constexpr (REGF) {
+        c_tail = m ? tail[s] : c_tail;
+        cres = m ? rcnt[s] : cres;
+      }
+    }
+    if constexpr (!REGF) {
+      c_tail = fld<MAXS>(l, F_TAIL, cs);
+      cres = (uint32_t)fld<MAXS>(l, F_RCNT, cs);
+    }
+    const int32_t start_a = c_cnt > 0 ? (c_tail > ta ? c_tail : ta) : ta;
+    int32_t svc = (int32_t)(L.next_work * c_scale);
+    svc = svc < 1 ? 1 : svc;
+    const int32_t tc_a = start_a + svc;
+    // completes in this step: its sample now (duration = tc - max(ta, predecessor's tc) = svc)
+    const bool ins = push && tc_a <= dt;
+
+    // ---- two Philox blocks: the pushed flow's Algorithm R draw, the next arrival's draw
+    const u32x4 dr = philox_rk(
+        u32x4{cres >> 1, L.gid, L.episode, (kStreamReservoir << 24) | (uint32_t)cs}, ec.rk0, ec.rk1);
+    const u32x4 d = philox_rk(u32x4{L.arr_idx + 1u, L.gid, L.episode, kStreamArrival << 24},
+                              ec.rk0, ec.rk1);
+    const int slot = reservoir_slot(cres, dr);
+    if (ins && slot >= 0) {
+      my_res[(uint32_t)cs * (uint32_t)K + (uint32_t)slot] =
+          make_uint3((uint32_t)(tc_a - ta), (uint32_t)svc,
+                     ec.base_ms + (ec.base_rem + (uint32_t)tc_a) / 1000u);
+    }
+    // queue index < WL: the LDS window (a push that does not happen writes the lane's scratch
+    // slot); beyond it: the HBM ring (overflow, rare)
+    *((push & (c_cnt < WL)) ? qslot<MAXS>(l, cs, (c_hs + c_cnt) & (WL - 1)) : qdummy<MAXS>(l)) =
+        make_int2(tc_a, ta);
+    if (push && c_cnt >= WL) {
+      const uint32_t pos = (uint32_t)(c_rb + c_hs + c_cnt) % (uint32_t)Q;
+      my_ring[(uint32_t)cs * (uint32_t)Q + pos] = make_int2(tc_a, ta);
+      // keeps the compiler from sinking the store into a flat (generic pointer) store shared with
+      // the window store, which counts in lgkmcnt too: every LDS wait would then wait on it
+      asm volatile("");
+    }
+    if constexpr (REGF) {
+#pragma unroll
+      for (int s = 0; s < MAXS; ++s) {
+        const bool m = push & (s == cs);
+        tail[s] = m ? tc_a : tail[s];
+        asg[s] += m ? 1 : 0;
+        rcnt[s] = (ins & (s == cs)) ? count_inc(cres) : rcnt[s];
+      }
+    } else {
+      fld<MAXS>(l, F_TAIL, cs) = push ? tc_a : c_tail;
+      atomicAdd(&fld<MAXS>(l, F_ASSIGNED, cs), push ? 1 : 0);  // ds_add_u32: no read-back
+      fld<MAXS>(l, F_RCNT, cs) = (int32_t)(ins ? count_inc(cres) : cres);
+    }
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) {
+      const bool m = push & (s == cs);
+      L.head_tc[s] = (m && c_cnt == 0) ? tc_a : L.head_tc[s];
+      L.cnt[s] += m ? 1 : 0;
+    }
+
+    // ---- next arrival (draw d belongs to arrival index arr_idx + 1)
+    int32_t na;
+    float nw;
+    uint32_t nu2, nu3;
+    if constexpr (TRACE) {  // the prefetched row; the next prefetch is issued one arrival ahead
+      na = ta + L.pf_gap;
+      nw = L.pf_work;
+      nu2 = d.z;
+      nu3 = d.w;
+      if (arr) {
+        L.row = (L.row + 1u == p.trace_rows) ? 0u : L.row + 1u;
+        L.pf_gap = (int32_t)st.trace_gap[L.row];
+        L.pf_work = st.trace_work[L.row];
+      }
+    } else {
+      na = ta + (int32_t)(-lb_logf(u01_open0(d.x)) * ec.mean_gap);
+      nw = -lb_logf(u01_open0(d.y));
+      nu2 = d.z;
+      nu3 = d.w;
+    }
+    L.next_arr = arr ? na : L.next_arr;
+    L.next_work = arr ? nw : L.next_work;
+    L.u2 = arr ? nu2 : L.u2;
+    L.u3 = arr ? nu3 : L.u3;
+    L.arr_idx += arr ? 1u : 0u;
+  }
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) {
+    L.head[s] = (int32_t)((uint32_t)(rbase[s] + hs[s]) % (uint32_t)Q);
+    L.lh[s] = hs[s] & (WL - 1);
+  }
+  if constexpr (REGF) {
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) {
+      if (s < S) {
+        fld<MAXS>(l, F_TAIL, s) = tail[s];
+        fld<MAXS>(l, F_RCNT, s) = (int32_t)rcnt[s];
+        fld<MAXS>(l, F_ASSIGNED, s) += asg[s];
+      }
+    }
+  }
+}
+
 // One simulated step of dt_us with server weights w[] (env.py:230-259 with real dynamics).
 //
 // Arrival-driven, as the oracle: a FIFO server fixes a flow's completion time when the flow is
@@ -407,7 +728,6 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
   const uint64_t base_us = (uint64_t)L.clock * (uint64_t)dt;
   const uint32_t base_ms = (uint32_t)(base_us / 1000u);
   const uint32_t base_rem = (uint32_t)(base_us - (uint64_t)base_ms * 1000u);
-  constexpr bool two_choice = (POLICY == 1 || POLICY == 3);
   constexpr bool alias = POLICY == kPolicyAlias;
   constexpr bool lsq = (POLICY == 2 || POLICY == 3);
   const uint32_t b0 = b * (uint32_t)S;
@@ -422,7 +742,6 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
   for (int s = 0; s < MAXS; ++s) {
     den[s] = 1.0;
     rcp[s] = 1.0;
-    if (s < S) fld<MAXS>(l, F_SCALE, s) = (int32_t)__float_as_uint(p.svc_scale[s]);
   }
   if constexpr (alias) {
     n_alias = build_alias<MAXS>(w, S, FieldAliasTab<MAXS>{l});
@@ -476,180 +795,14 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     }
   }
 
-  // ---- 2. one arrival per iteration (3. the final pops up to dt in the last iterations)
-  for (;;) {
-    const bool arrival_due = L.next_arr < dt;
-    const int32_t th = arrival_due ? L.next_arr : dt;  // a completion at the arrival time goes first
-    bool more = false;
-#pragma unroll
-    for (int s = 0; s < MAXS; ++s) {  // pop each server's head if it completed by th
-      const bool due = (s < S) & (L.cnt[s] > 0) & (L.head_tc[s] <= th);
-      const int nl = (L.lh[s] + 1) & (WL - 1);
-      const int nh = (L.head[s] + 1 == Q) ? 0 : L.head[s] + 1;
-      if (due && L.cnt[s] - 1 >= WL) {  // rare: bring queue entry WL (ring) into the freed slot
-        int pw = nh + WL - 1;
-        pw = pw >= Q ? pw - Q : pw;
-        *qslot<MAXS>(l, s, L.lh[s]) = my_ring[(uint32_t)s * (uint32_t)Q + (uint32_t)pw];
-        __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);  // drain in the rare branch, not at the back-edge
-      }
-      const int32_t nt = qslot<MAXS>(l, s, nl)->x;  // next head (valid if cnt > 1)
-      L.last[s] = due ? L.head_tc[s] : L.last[s];
-      L.cnt[s] -= due ? 1 : 0;
-      L.lh[s] = due ? nl : L.lh[s];
-      L.head[s] = due ? nh : L.head[s];
-      L.head_tc[s] = due ? nt : L.head_tc[s];
-      more |= due & (L.cnt[s] > 0) & (nt <= th);
-    }
-    if (!arrival_due && !more) break;
-    const bool arr = arrival_due & !more;
-
-    // ---- the arrival: choose a server (node.c:388-441); full servers are not eligible
-    const int32_t ta = L.next_arr;
-    float score[MAXS];
-    if constexpr (!alias) {
-      bool bad = false;
-#pragma unroll
-      for (int s = 0; s < MAXS; ++s) {
-        if constexpr (lsq) {
-          score[s] = (float)L.cnt[s];
-        } else {  // (cnt + 1) / den correctly rounded by Markstein's corrected quotient
-          const double c = (double)(L.cnt[s] + 1);
-          const double q0 = c * rcp[s];
-          const double q = fma(fma(-q0, den[s], c), rcp[s], q0);
-          bad |= q != q;
-          score[s] = (float)q;
-        }
-      }
-      if (!lsq && bad) {  // den 0 / inf / NaN: the division
-#pragma unroll
-        for (int s = 0; s < MAXS; ++s) {
-          const float q = score[s];
-          if (q != q) score[s] = (float)((double)(L.cnt[s] + 1) / den[s]);
-        }
-      }
-    }
-    int chosen = -1;
-    if constexpr (alias) {  // full server: the flow is dropped (ALIAS has no eligibility test)
-      if (n_alias > 0) {
-        const int a = alias_pick(FieldAliasTab<MAXS>{l}, n_alias, L.u2);
-        chosen = sel<MAXS>(L.cnt, a) < Q ? a : -1;
-      }
-    } else if constexpr (two_choice) {  // SED2 / LSQ2: keep the second candidate if strictly better
-      const int h1 = (int)__umulhi(L.u2, (uint32_t)S);  // (u * S) >> 32
-      const int h2 = (int)__umulhi(L.u3, (uint32_t)S);
-      float s1 = 0.f, s2 = 0.f;
-      bool ok1 = false, ok2 = false;
-#pragma unroll
-      for (int s = 0; s < MAXS; ++s) {
-        s1 = (s == h1) ? score[s] : s1;
-        ok1 = (s == h1) ? (L.cnt[s] < Q) : ok1;
-        s2 = (s == h2) ? score[s] : s2;
-        ok2 = (s == h2) ? (L.cnt[s] < Q) : ok2;
-      }
-      chosen = (ok1 && ok2) ? ((s2 < s1) ? h2 : h1) : (ok1 ? h1 : (ok2 ? h2 : -1));
-    } else {  // SED / LSQ: start at the hashed server, replace on strictly lower score
-      const int h = (int)__umulhi(L.u2, (uint32_t)S);  // (u * S) >> 32
-      float best = __uint_as_float(0x7f800000u);  // +inf: any finite score replaces it
-#pragma unroll
-      for (int s = 0; s < MAXS; ++s) {
-        const bool m = (s == h) & (L.cnt[s] < Q);
-        chosen = m ? s : chosen;
-        best = m ? score[s] : best;
-      }
-      if (finite_scores) {  // every score finite: "replace on strictly lower" from +inf is exact
-#pragma unroll
-        for (int s = 0; s < MAXS; ++s) {
-          const bool m = (s < S) & (L.cnt[s] < Q) & (score[s] < best);
-          chosen = m ? s : chosen;
-          best = m ? score[s] : best;
-        }
-      } else {  // NaN / inf scores: the first eligible server is taken whatever its score
-#pragma unroll
-        for (int s = 0; s < MAXS; ++s) {
-          const bool m = (s < S) & (L.cnt[s] < Q) & ((chosen < 0) | (score[s] < best));
-          chosen = m ? s : chosen;
-          best = m ? score[s] : best;
-        }
-      }
-    }
-    const bool push = arr && chosen >= 0;
-    L.dropped += (arr && chosen < 0) ? 1u : 0u;
-
-    // ---- the chosen server: FIFO service starts when its last queued flow ends
-    const int cs = push ? chosen : 0;
-    int32_t c_cnt = 0, c_lh = 0, c_head = 0;
-#pragma unroll
-    for (int s = 0; s < MAXS; ++s) {
-      const bool m = s == cs;
-      c_cnt = m ? L.cnt[s] : c_cnt;
-      c_lh = m ? L.lh[s] : c_lh;
-      c_head = m ? L.head[s] : c_head;
-    }
-    const int32_t c_tail = fld<MAXS>(l, F_TAIL, cs);
-    const uint32_t cres = (uint32_t)fld<MAXS>(l, F_RCNT, cs);
-    const float c_scale = __uint_as_float((uint32_t)fld<MAXS>(l, F_SCALE, cs));
-    const int32_t start_a = c_cnt > 0 ? (c_tail > ta ? c_tail : ta) : ta;
-    int32_t svc = (int32_t)(L.next_work * c_scale);
-    svc = svc < 1 ? 1 : svc;
-    const int32_t tc_a = start_a + svc;
-    // completes in this step: its sample now (duration = tc - max(ta, predecessor's tc) = svc)
-    const bool ins = push && tc_a <= dt;
-
-    // ---- two Philox blocks: the pushed flow's Algorithm R draw, the next arrival's draw
-    const u32x4 dr = philox4x32_10(
-        u32x4{cres >> 1, L.gid, L.episode, (kStreamReservoir << 24) | (uint32_t)cs}, p.key0, p.key1);
-    const u32x4 d = philox4x32_10(u32x4{L.arr_idx + 1u, L.gid, L.episode, kStreamArrival << 24},
-                                  p.key0, p.key1);
-    const int slot = reservoir_slot(cres, dr);
-    if (ins && slot >= 0) {
-      my_res[(uint32_t)cs * (uint32_t)K + (uint32_t)slot] =
-          make_uint3((uint32_t)(tc_a - ta), (uint32_t)svc, base_ms + (base_rem + (uint32_t)tc_a) / 1000u);
-    }
-    // queue index < WL: the LDS window (a push that does not happen writes the lane's scratch
-    // slot); beyond it: the HBM ring (overflow, rare)
-    *((push & (c_cnt < WL)) ? qslot<MAXS>(l, cs, (c_lh + c_cnt) & (WL - 1)) : qdummy<MAXS>(l)) =
-        make_int2(tc_a, ta);
-    if (push && c_cnt >= WL) {
-      int pos = c_head + c_cnt;
-      pos = pos >= Q ? pos - Q : pos;
-      my_ring[(uint32_t)cs * (uint32_t)Q + (uint32_t)pos] = make_int2(tc_a, ta);
-      // keeps the compiler from sinking the store into a flat (generic pointer) store shared with
-      // the window store, which counts in lgkmcnt too: every LDS wait would then wait on it
-      asm volatile("");
-    }
-    fld<MAXS>(l, F_TAIL, cs) = push ? tc_a : c_tail;
-    atomicAdd(&fld<MAXS>(l, F_ASSIGNED, cs), push ? 1 : 0);  // ds_add_u32: no read-back, no wait
-    fld<MAXS>(l, F_RCNT, cs) = (int32_t)(ins ? count_inc(cres) : cres);
-#pragma unroll
-    for (int s = 0; s < MAXS; ++s) {
-      const bool m = push & (s == cs);
-      L.head_tc[s] = (m && c_cnt == 0) ? tc_a : L.head_tc[s];
-      L.cnt[s] += m ? 1 : 0;
-    }
-
-    // ---- next arrival (draw d belongs to arrival index arr_idx + 1)
-    int32_t na;
-    float nw;
-    uint32_t nu2, nu3;
-    if constexpr (TRACE) {  // the prefetched row; the next prefetch is issued one arrival ahead
-      na = ta + L.pf_gap;
-      nw = L.pf_work;
-      nu2 = d.z;
-      nu3 = d.w;
-      if (arr) {
-        L.row = (L.row + 1u == p.trace_rows) ? 0u : L.row + 1u;
-        L.pf_gap = (int32_t)st.trace_gap[L.row];
-        L.pf_work = st.trace_work[L.row];
-      }
-    } else {
-      arrival_from_draw(p, d, ta, na, nw, nu2, nu3);
-    }
-    L.next_arr = arr ? na : L.next_arr;
-    L.next_work = arr ? nw : L.next_work;
-    L.u2 = arr ? nu2 : L.u2;
-    L.u3 = arr ? nu3 : L.u3;
-    L.arr_idx += arr ? 1u : 0u;
-  }
+  // ---- 2. one arrival per iteration (3. the final pops up to dt in the last iterations).  The
+  //      SED/SED2 scores can only be NaN when some den is 0 / inf / NaN: a wave whose envs all
+  //      have finite scores runs the loop without the NaN fallbacks (a wave-uniform choice).
+  const EvConst<MAXS> ec = ev_const<MAXS>(p, base_ms, base_rem);
+  if (lsq || alias || __all(finite_scores))
+    event_loop<MAXS, POLICY, TRACE, true>(st, p, L, l, ec, den, rcp, n_alias, my_res, my_ring);
+  else
+    event_loop<MAXS, POLICY, TRACE, false>(st, p, L, l, ec, den, rcp, n_alias, my_res, my_ring);
 
   // ---- rebase relative times to the next step's start: the LDS window in place, the HBM ring
   //      entries beyond it read-modify-written (queues longer than WL only)

@@ -7,7 +7,7 @@ var = "-"
 for line in open(sys.argv[1]):
     d = json.loads(line)
     if "variant" in d:
-        var = d["variant"]
+        var = d["variant"] + ("" if "round" not in d else f"/{d['round']}")
         continue
     c = d["config"]
     k = d["roofline"]["kernel_avg_ms"]
