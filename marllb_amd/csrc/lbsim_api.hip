@@ -168,7 +168,7 @@ std::vector<Section> sections(lbsim_t* h) {
       {(void**)&s.clock, B * 4},      {(void**)&s.ep_step, B * 4},   {(void**)&s.dropped, B * 4},
       {(void**)&s.norm_count, B * 4}, {(void**)&s.ep_return, B * 8}, {(void**)&s.hc, BS * 4},
       {(void**)&s.last_tc, BS * 4},   {(void**)&s.res_count, BS * 4}, {(void**)&s.ring, BSQ * 8},
-      {(void**)&s.res, BSK * 12},
+      {(void**)&s.res, BSK * 12},     {(void**)&s.chg, BS * 16},      {(void**)&s.fcache, BS * 40},
   };
   if (h->cfg.normalize_obs) {
     v.push_back({(void**)&s.norm_mean, BS * NF * 8});

@@ -89,6 +89,7 @@ __device__ __forceinline__ uint32_t group_bits(uint64_t m, int gbase) {
 struct SrvLane {
   int32_t cnt, head_tc, head, lh, tail, last, assigned;
   uint32_t rcnt;
+  uint32_t chg[4];  // reservoir slots written this launch (DevState::chg)
   float score, scale;
   double den, rcp;
   bool act;  // s < S
@@ -129,6 +130,13 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
     V.rcp = 1.0 / V.den;
   }
   auto wslot = [&](int i) -> int2* { return win + i * 64 + lane; };
+  auto mark = [&](int slot) {  // the slot's bit in the lane's 128-bit written-slot mask
+    const uint32_t bit = 1u << (slot & 31), w = (uint32_t)slot >> 5;
+    V.chg[0] |= w == 0 ? bit : 0u;
+    V.chg[1] |= w == 1 ? bit : 0u;
+    V.chg[2] |= w == 2 ? bit : 0u;
+    V.chg[3] |= w == 3 ? bit : 0u;
+  };
 
   // ---- 1. this lane's carried-in flows that complete in this step: samples in FIFO order
   if (V.act && V.cnt > 0 && V.head_tc <= dt) {
@@ -141,10 +149,12 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
       const u32x4 d = philox4x32_10(
           u32x4{rc >> 1, E.gid, E.episode, (kStreamReservoir << 24) | (uint32_t)s}, p.key0, p.key1);
       const int slot = reservoir_slot(rc, d);
-      if (slot >= 0)
+      if (slot >= 0) {
         my_res[(uint32_t)slot] =
             make_uint3((uint32_t)(etc - eta), (uint32_t)(etc - (eta > prev ? eta : prev)),
                        base_ms + (base_rem + (uint32_t)etc) / 1000u);
+        mark(slot);
+      }
       prev = etc;
       rc = count_inc(rc);
       if (++i >= V.cnt) break;
@@ -247,9 +257,11 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
     const u32x4 da = u32x4{(uint32_t)__shfl((int)d.x, src, 64), (uint32_t)__shfl((int)d.y, src, 64),
                            (uint32_t)__shfl((int)d.z, src, 64), (uint32_t)__shfl((int)d.w, src, 64)};
     const int slot = reservoir_slot(V.rcnt, d);
-    if (ins && slot >= 0)
+    if (ins && slot >= 0) {
       my_res[(uint32_t)slot] = make_uint3((uint32_t)(tc_a - ta), (uint32_t)svc,
                                           base_ms + (base_rem + (uint32_t)tc_a) / 1000u);
+      mark(slot);
+    }
     if (mine) {
       const int2 e = make_int2(tc_a, ta);
       if (V.cnt < WL) {
@@ -344,6 +356,8 @@ __global__ void __launch_bounds__(64)
   V.score = 0.f;
   V.assigned = 0;
   V.lh = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) V.chg[w] = 0u;
   const uint32_t sb = b * (uint32_t)S + (uint32_t)s;
   float wall[G];
   float w_own = 1.0f;
@@ -424,6 +438,8 @@ __global__ void __launch_bounds__(64)
     st.hc[sb] = (uint32_t)V.head | ((uint32_t)V.cnt << 16);
     st.last_tc[sb] = V.last;
     st.res_count[sb] = V.rcnt;
+    *reinterpret_cast<uint4*>(st.chg + (size_t)sb * 4) =
+        make_uint4(V.chg[0], V.chg[1], V.chg[2], V.chg[3]);
     if (MODE != kModeReset && assign_out != nullptr) assign_out[sb] = V.assigned;
   }
   if (s == 0) {

@@ -55,6 +55,13 @@ struct DevState {
   // feature value of a sample is (float)us * 1e-6f seconds, us_to_seconds)
   uint3* res;           // [B*S*K] slot records {fct us, duration us, timestamp ms}: an insert is
                         // one 12-B store (one partial line, not three), observe reads dwordx3
+  // unchanged-reservoir skip of observe: chg[(b*S + s)*4 + w] bit i set if slot
+  // 32 w + i of server s was written by the last dynamics launch (its two reservoirs share every
+  // replacement decision); fcache[(b*S + s)*10 + f] = the server's 10 reservoir features at the
+  // last observe.  A server whose reservoirs were not written keeps the same features (values,
+  // timestamps and n = min(count, K) are unchanged: count only grows without a write once full).
+  uint32_t* chg;
+  float* fcache;
   // stateless features API only: caller's separate value / timestamp arrays [n*K]
   const uint32_t* feat_vals;
   const uint32_t* feat_ts;
@@ -154,7 +161,14 @@ struct Lds {
   int2* q;       // queue window [server][slot][lane]
   int32_t* f;    // per-server fields [field][server][lane]
   int lane;
+  uint32_t* m;   // slots written this launch [server][word][lane] (DevState::chg), or nullptr
 };
+
+// Record that reservoir slot `slot` of server s was written (ds_or_b32, no return value).
+template <int MAXS>
+__device__ __forceinline__ void mark_slot(const Lds& l, int s, int slot) {
+  atomicOr(&l.m[(s * 4 + (slot >> 5)) * 64 + l.lane], 1u << (slot & 31));
+}
 
 template <int MAXS>
 __device__ __forceinline__ int32_t& fld(const Lds& l, int field, int s) {
@@ -332,6 +346,8 @@ __device__ __forceinline__ void load_servers(const DevState& st, const SimParams
       L.last[s] = st.last_tc[sb];
       fld<MAXS>(l, F_RCNT, s) = (int32_t)st.res_count[sb];
       fld<MAXS>(l, F_ASSIGNED, s) = 0;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) l.m[(s * 4 + w) * 64 + l.lane] = 0u;
       int32_t tail = 0;
       for (int i = 0; i < WL && i < L.cnt[s]; ++i) {
         int pos = head + i;
@@ -363,6 +379,8 @@ __device__ __forceinline__ void clear_servers(const SimParams& p, LaneState<MAXS
     L.last[s] = kLastNone;
     fld<MAXS>(l, F_RCNT, s) = 0;
     fld<MAXS>(l, F_ASSIGNED, s) = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) l.m[(s * 4 + w) * 64 + l.lane] = 0u;
   }
 }
 
@@ -624,6 +642,7 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
       my_res[(uint32_t)cs * (uint32_t)K + (uint32_t)slot] =
           make_uint3((uint32_t)(tc_a - ta), (uint32_t)svc,
                      ec.base_ms + (ec.base_rem + (uint32_t)tc_a) / 1000u);
+      mark_slot<MAXS>(l, cs, slot);
     }
     // queue index < WL: the LDS window (a push that does not happen writes the lane's scratch
     // slot); beyond it: the HBM ring (overflow, rare)
@@ -770,10 +789,12 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
         const u32x4 d = philox4x32_10(
             u32x4{rc >> 1, L.gid, L.episode, (kStreamReservoir << 24) | (uint32_t)s}, p.key0, p.key1);
         const int slot = reservoir_slot(rc, d);
-        if (slot >= 0)
+        if (slot >= 0) {
           my_res[(uint32_t)s * (uint32_t)K + (uint32_t)slot] =
               make_uint3((uint32_t)(etc - eta), (uint32_t)(etc - (eta > prev ? eta : prev)),
                          base_ms + (base_rem + (uint32_t)etc) / 1000u);
+          mark_slot<MAXS>(l, s, slot);
+        }
         prev = etc;
         rc = count_inc(rc);
         if (++i >= c) break;
@@ -859,6 +880,9 @@ __device__ __forceinline__ void store_servers(const DevState& st, const SimParam
       st.last_tc[sb] = L.last[s];
       st.res_count[sb] = (uint32_t)fld<MAXS>(l, F_RCNT, s);
       if (assign_out != nullptr) assign_out[sb] = fld<MAXS>(l, F_ASSIGNED, s);
+      *reinterpret_cast<uint4*>(st.chg + (size_t)sb * 4) =
+          make_uint4(l.m[(s * 4 + 0) * 64 + l.lane], l.m[(s * 4 + 1) * 64 + l.lane],
+                     l.m[(s * 4 + 2) * 64 + l.lane], l.m[(s * 4 + 3) * 64 + l.lane]);
     }
   }
 }
@@ -900,7 +924,8 @@ __global__ void __launch_bounds__(64 * kDynWaves<MAXS>)
   const int wv = (int)(threadIdx.x >> 6);
   __shared__ int2 qwin[kDynWaves<MAXS>][(MAXS * Win<MAXS>::WL + 1) * 64];  // + scratch slots
   __shared__ int32_t fields[kDynWaves<MAXS>][F_NUM * MAXS * 64];
-  const Lds l{qwin[wv], fields[wv], (int)(threadIdx.x & 63u)};
+  __shared__ uint32_t chgw[kDynWaves<MAXS>][MAXS * 4 * 64];
+  const Lds l{qwin[wv], fields[wv], (int)(threadIdx.x & 63u), chgw[wv]};
   if (b >= (uint32_t)p.B) return;
   const int S = p.S;
   LaneState<MAXS> L;
@@ -1171,13 +1196,28 @@ constexpr uint32_t kPackLimit = (1u << 25) - 1u;
 // The 11-column observation rows (features.py:256-286) of servers [s_base, s_base + S), S <= 4,
 // of env b into obs_out.  Slot-order sums follow numpy exactly (reservoir.py:143-155); order
 // statistics come from the sorted keys (reservoir.py:144, 165-196).
-template <bool US>
+// INC (step mode with state): a chunk none of whose reservoirs this step's dynamics wrote
+// (DevState::chg all zero) takes its features from DevState::fcache instead of recomputing them;
+// every computed chunk refreshes the cache (US: reset and step modes).
+template <bool US, bool INC>
 __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParams& p, size_t b,
                                               int s_base, int S, ObsScratch& sc, float* obs_out,
                                               int lane) {
   const size_t srow = b * (size_t)p.S + (size_t)s_base;  // first (env, server) of the chunk
   const int R = 2 * S;
   const int g = lane >> 3, j = lane & 7;
+  if constexpr (INC) {
+    const uint32_t w = lane < 4 * S ? st.chg[(srow + (size_t)(lane >> 2)) * 4 + (lane & 3)] : 0u;
+    if (!__any(w != 0u)) {  // no reservoir of the chunk changed: the cached features
+      for (int e = lane; e < S * NF; e += 64) {
+        const int s = e / NF, c = e - s * NF;
+        obs_out[s_base * NF + e] = c == 0 ? (float)(st.hc[srow + (size_t)s] >> 16)
+                                          : st.fcache[(srow + (size_t)s) * 10 + (size_t)(c - 1)];
+      }
+      __syncthreads();
+      return;
+    }
+  }
   // ---- phase 1: reservoirs into LDS, decay weights relative to each server's newest sample.
   //      Loads of 4 servers are issued before any is consumed (memory-level parallelism).
   for (int s0 = 0; s0 < S; s0 += 4) {
@@ -1389,6 +1429,7 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
       const int r = 2 * s + (c >= 6 ? 1 : 0);
       const int f = (c - 1) % 5;
       v = f == 0 ? sc.mean[r] : f == 1 ? sc.p90[r] : f == 2 ? sc.sd[r] : f == 3 ? sc.md[r] : sc.p90d[r];
+      if constexpr (US) st.fcache[(srow + (size_t)s) * 10 + (size_t)(c - 1)] = v;
     }
     obs_out[s_base * NF + e] = v;
   }
@@ -1396,15 +1437,15 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
 }
 
 // The (S, 11) observation of env b into obs_out, 4 servers at a time.
-template <int MAXS, bool US>
+template <int MAXS, bool US, bool INC>
 __device__ __forceinline__ void observe_env(const DevState& st, const SimParams& p, size_t b,
                                             ObsScratch& sc, float* obs_out, int lane) {
   if constexpr (MAXS <= kObsChunk) {
-    observe_chunk<US>(st, p, b, 0, p.S, sc, obs_out, lane);
+    observe_chunk<US, INC>(st, p, b, 0, p.S, sc, obs_out, lane);
   } else {
     for (int s0 = 0; s0 < p.S; s0 += kObsChunk)
-      observe_chunk<US>(st, p, b, s0, p.S - s0 < kObsChunk ? p.S - s0 : kObsChunk, sc, obs_out,
-                        lane);
+      observe_chunk<US, INC>(st, p, b, s0, p.S - s0 < kObsChunk ? p.S - s0 : kObsChunk, sc,
+                             obs_out, lane);
   }
 }
 
@@ -1536,7 +1577,7 @@ __global__ void __launch_bounds__(64, kObsWaves<MAXS>)
   __shared__ ObsScratch sc;
   __shared__ float s_obs[MAXS * NF];
   const int S = p.S;
-  observe_env<MAXS, true>(st, p, b, sc, s_obs, lane);
+  observe_env<MAXS, true, mode == kModeStep>(st, p, b, sc, s_obs, lane);
 
   // active servers (any column > 0): lane s scans its row, one ballot
   bool act = false;
@@ -1605,7 +1646,7 @@ __global__ void __launch_bounds__(64)
   p.S = S;
   p.decay_c = decay_c;
   __syncthreads();
-  observe_env<4, false>(st, p, 0, sc, fobs, lane);
+  observe_env<4, false, false>(st, p, 0, sc, fobs, lane);
   for (int e = lane; e < S * 5; e += 64) {
     const int s = e / 5, f = e - s * 5;
     out[(r0 + s) * 5 + f] = fobs[s * NF + 1 + f];
@@ -1618,7 +1659,7 @@ __global__ void __launch_bounds__(64)
     alias_tables_kernel(const float* weights, int64_t n, int S, float* odd_out,
                         int32_t* alias_out, int32_t* active_out) {
   __shared__ int32_t fields[F_NUM * MAX_S * 64];
-  const Lds l{nullptr, fields, (int)threadIdx.x};
+  const Lds l{nullptr, fields, (int)threadIdx.x, nullptr};
   const int64_t r = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (r >= n) return;
   float w[MAX_S];

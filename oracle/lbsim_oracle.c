@@ -306,6 +306,10 @@ typedef struct oracle {
   /* reservoir slot records [B*S*K][3] = {fct us, duration us, timestamp ms}; the feature value
    * of a sample is (float)us * 1e-6f */
   uint32_t* res;
+  /* unchanged-reservoir skip of observe: slots written by the last dynamics
+   * launch (a 128-bit mask per server) and the server's 10 reservoir features at the last
+   * observe */
+  uint32_t* chg; float* fcache;
   double* norm_mean; double* norm_std;
   /* TRACE arrivals (lbsim_set_trace semantics): us gap before each row, mean-1 work */
   uint32_t* trace_gap; float* trace_work; uint32_t trace_rows;
@@ -331,7 +335,7 @@ oracle_t* oracle_create(const lbsim_config_t* cfg) {
   o->threads = 1;
   const size_t B = o->B, BS = (size_t)o->B * o->S, BSQ = BS * o->Q, BSK = BS * K;
   const size_t sz[] = {B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4,
-                       B * 8, BS * 4, BS * 4, BS * 4, BSQ * 8, BSK * 12,
+                       B * 8, BS * 4, BS * 4, BS * 4, BSQ * 8, BSK * 12, BS * 16, BS * 40,
                        cfg->normalize_obs ? BS * NF * 8 : 0, cfg->normalize_obs ? BS * NF * 8 : 0};
   size_t total = 0;
   for (size_t i = 0; i < sizeof(sz) / sizeof(sz[0]); ++i) total += sz[i];
@@ -344,7 +348,8 @@ oracle_t* oracle_create(const lbsim_config_t* cfg) {
                    (void**)&o->clock, (void**)&o->ep_step, (void**)&o->dropped,
                    (void**)&o->norm_count, (void**)&o->ep_return, (void**)&o->hc,
                    (void**)&o->last_tc, (void**)&o->res_count, (void**)&o->ring,
-                   (void**)&o->res, (void**)&o->norm_mean, (void**)&o->norm_std};
+                   (void**)&o->res, (void**)&o->chg, (void**)&o->fcache, (void**)&o->norm_mean,
+                   (void**)&o->norm_std};
   for (size_t i = 0; i < sizeof(sz) / sizeof(sz[0]); ++i) {
     *ptrs[i] = sz[i] ? (void*)p : NULL;
     p += sz[i];
@@ -470,6 +475,7 @@ static void reservoir_add(env_ctx* e, int s, uint32_t fct, uint32_t dur, uint32_
     o->res[3 * r + 0] = fct;
     o->res[3 * r + 1] = dur;
     o->res[3 * r + 2] = ts_ms;
+    o->chg[sb * 4 + (size_t)(slot >> 5)] |= 1u << (slot & 31);
   }
   if (c != 0xFFFFFFFFu) o->res_count[sb] = c + 1u;
 }
@@ -674,6 +680,7 @@ static void observe(oracle_t* o, size_t b, float* obs_out, float* reward_out, ui
     }
     features_one(vf, w, wq, n, ff);
     features_one(vd, w, wq, n, fd);
+    for (int f = 0; f < 5; ++f) { o->fcache[sb * 10 + (size_t)f] = ff[f]; o->fcache[sb * 10 + 5 + (size_t)f] = fd[f]; }
     raw[s * NF + 0] = (float)ring_count(o, sb);
     for (int f = 0; f < 5; ++f) { raw[s * NF + 1 + f] = ff[f]; raw[s * NF + 6 + f] = fd[f]; }
   }
@@ -708,6 +715,7 @@ static void reset_env(oracle_t* o, size_t b) {
     o->hc[sb] = 0u;
     o->last_tc[sb] = LAST_NONE;
     o->res_count[sb] = 0u;
+    for (int w = 0; w < 4; ++w) o->chg[sb * 4 + (size_t)w] = 0u;
   }
   float w1[LBSIM_MAX_SERVERS];
   for (int s = 0; s < LBSIM_MAX_SERVERS; ++s) w1[s] = 1.0f;
@@ -741,6 +749,7 @@ int oracle_step(oracle_t* o, const void* action, int dtype, float* obs_out, floa
     e.o = o; e.b = (size_t)b; e.gid = (uint32_t)(o->cfg.env_id_offset + (int64_t)b);
     float w[LBSIM_MAX_SERVERS];
     for (int s = 0; s < S; ++s) w[s] = action_weight(o, action, dtype, (size_t)b * S + (size_t)s);
+    for (size_t i = 0; i < (size_t)S * 4; ++i) o->chg[(size_t)b * S * 4 + i] = 0u;
     sim_step(&e, w);
     if (assign_out)
       for (int s = 0; s < S; ++s) assign_out[(size_t)b * S + (size_t)s] = e.assigned[s];

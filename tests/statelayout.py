@@ -11,7 +11,7 @@ def sections(B, S, Q, normalize):
            ("clock", np.uint32, B), ("ep_step", np.int32, B), ("dropped", np.uint32, B),
            ("norm_count", np.int32, B), ("ep_return", np.float64, B), ("hc", np.uint32, BS),
            ("last_tc", np.int32, BS), ("res_count", np.uint32, BS), ("ring", np.int32, BS * Q * 2),
-           ("res", np.uint32, BS * K * 3)]
+           ("res", np.uint32, BS * K * 3), ("chg", np.uint32, BS * 4), ("fcache", np.float32, BS * 10)]
     if normalize:
         out += [("norm_mean", np.float64, BS * NF), ("norm_std", np.float64, BS * NF)]
     return out

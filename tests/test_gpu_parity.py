@@ -138,6 +138,11 @@ CONFIGS = [
     dict(B=50, S=4, kw={"trace": "short", "assign_policy": "sed2", "step_interval": 0.5}),
     # NaN continuous actions pass np.clip (env.py:349-351): NaN SED scores take the exact scan
     dict(B=60, S=5, kw={"action_type": "continuous", "_nan_actions": 0.15}),
+    # observe's unchanged-reservoir skip: sparse arrivals -> many env-steps write
+    # no reservoir slot (cached features) next to env-steps that do; a flood -> >= 64 written
+    # slots per server-step
+    dict(B=64, S=4, kw={"arrival_rate": 6.0, "server_rates": [3.0, 4.0, 5.0, 6.0]}),
+    dict(B=48, S=8, kw={"arrival_rate": 3000.0, "warmup_steps": 1}),
 ]
 
 
