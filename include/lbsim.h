@@ -32,8 +32,9 @@
 extern "C" {
 #endif
 
-#define LBSIM_ABI_VERSION 1
-#define LBSIM_MAX_SERVERS 16   /* S <= 16 (QMIX config C5 uses 4 agents x 4 servers)        */
+#define LBSIM_ABI_VERSION 2
+#define LBSIM_MAX_SERVERS 64   /* S <= 64: BASELINE configs[4] read literally is 4 agents x 16 */
+                               /* servers = 64 (S > 16: server-per-lane dynamics only)       */
 #define LBSIM_RESERVOIR_K 128  /* reservoir.py:31 capacity=128, reservoir.h:24               */
 #define LBSIM_NUM_FEATURES 11  /* env.py:46-48 (S, 11) observation                           */
 #define LBSIM_MAX_DISCRETE 8

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liblbsim.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "lbsim.h")
 
-MAX_SERVERS = 16
+MAX_SERVERS = 64
 RESERVOIR_K = 128
 NUM_FEATURES = 11
 MAX_DISCRETE = 8

@@ -121,6 +121,9 @@ int validate(const lbsim_config_t* c, char* msg, size_t n) {
   if (c->warmup_steps < 0 || c->warmup_steps > 100000) return bad("warmup_steps out of range");
   if (c->dyn_mapping < LBSIM_DYN_AUTO || c->dyn_mapping > LBSIM_DYN_SERVER_PER_LANE)
     return bad("unknown dyn_mapping %d", c->dyn_mapping);
+  if (c->dyn_mapping == LBSIM_DYN_ENV_PER_LANE && c->num_servers > 16)
+    return bad("the env-per-lane dynamics mapping takes at most 16 servers (got %d)",
+               c->num_servers);
   return LBSIM_OK;
 #undef bad
 }
@@ -270,7 +273,21 @@ void launch_dyn_policy(lbsim_t* h, bool g, const void* action, int dtype, int32_
 bool server_per_lane(const lbsim_t* h) {
   if (h->cfg.dyn_mapping == LBSIM_DYN_ENV_PER_LANE) return false;
   if (h->cfg.dyn_mapping == LBSIM_DYN_SERVER_PER_LANE) return true;
-  return h->S > 8 || (int64_t)(h->B + 63) / 64 < (int64_t)h->simds;
+  return h->S > 8 || (int64_t)(h->B + 63) / 64 < (int64_t)h->simds;  // S > 16: always
+}
+
+// S > 16: server-per-lane only (32 or 64 lanes per env; the env-per-lane kernel keeps its
+// per-server state in registers / LDS rows sized for at most 16 servers).
+template <int G, int MODE>
+void launch_dyn_group_policy(lbsim_t* h, const void* action, int dtype, int32_t* assign,
+                             const uint8_t* mask, hipStream_t stream) {
+  switch (h->prm.policy) {
+    case LBSIM_POLICY_SED: launch_dyn_group<G, MODE, 0>(h, action, dtype, assign, mask, stream); break;
+    case LBSIM_POLICY_SED2: launch_dyn_group<G, MODE, 1>(h, action, dtype, assign, mask, stream); break;
+    case LBSIM_POLICY_LSQ: launch_dyn_group<G, MODE, 2>(h, action, dtype, assign, mask, stream); break;
+    case LBSIM_POLICY_LSQ2: launch_dyn_group<G, MODE, 3>(h, action, dtype, assign, mask, stream); break;
+    default: launch_dyn_group<G, MODE, 4>(h, action, dtype, assign, mask, stream); break;
+  }
 }
 
 template <int MODE>
@@ -279,7 +296,9 @@ void launch_dynamics_t(lbsim_t* h, const void* action, int dtype, int32_t* assig
   const bool g = server_per_lane(h);
   if (h->S <= 4) launch_dyn_policy<4, MODE>(h, g, action, dtype, assign, mask, stream);
   else if (h->S <= 8) launch_dyn_policy<8, MODE>(h, g, action, dtype, assign, mask, stream);
-  else launch_dyn_policy<16, MODE>(h, g, action, dtype, assign, mask, stream);
+  else if (h->S <= 16) launch_dyn_policy<16, MODE>(h, g, action, dtype, assign, mask, stream);
+  else if (h->S <= 32) launch_dyn_group_policy<32, MODE>(h, action, dtype, assign, mask, stream);
+  else launch_dyn_group_policy<64, MODE>(h, action, dtype, assign, mask, stream);
 }
 
 int launch_dynamics(lbsim_t* h, const void* action, int dtype, int32_t* assign,
@@ -297,8 +316,10 @@ void launch_observe_t(lbsim_t* h, const ObsOutputs& o, const uint8_t* mask, hipS
     hipLaunchKernelGGL((observe_kernel<4, MODE>), grid, block, 0, stream, h->st, h->prm, o, mask);
   else if (h->S <= 8)
     hipLaunchKernelGGL((observe_kernel<8, MODE>), grid, block, 0, stream, h->st, h->prm, o, mask);
-  else
+  else if (h->S <= 16)
     hipLaunchKernelGGL((observe_kernel<16, MODE>), grid, block, 0, stream, h->st, h->prm, o, mask);
+  else
+    hipLaunchKernelGGL((observe_kernel<64, MODE>), grid, block, 0, stream, h->st, h->prm, o, mask);
 }
 
 int launch_observe(lbsim_t* h, const ObsOutputs& o, const uint8_t* mask, int mode,

@@ -61,6 +61,17 @@ __device__ __forceinline__ void group_min2(int32_t& a, int32_t& b) {
   if constexpr (G >= 4) gmin_step<0x4E>(a, b);    // quad_perm [2,3,0,1]
   if constexpr (G >= 8) gmin_step<0x141>(a, b);   // row_half_mirror
   if constexpr (G >= 16) gmin_step<0x140>(a, b);  // row_mirror
+  if constexpr (G >= 32) {  // across DPP rows (S > 16): crossbar shuffles
+    int32_t oa = __shfl_xor(a, 16, 64), ob = __shfl_xor(b, 16, 64);
+    a = oa < a ? oa : a;
+    b = ob < b ? ob : b;
+    if constexpr (G >= 64) {
+      oa = __shfl_xor(a, 32, 64);
+      ob = __shfl_xor(b, 32, 64);
+      a = oa < a ? oa : a;
+      b = ob < b ? ob : b;
+    }
+  }
 }
 template <int G>
 __device__ __forceinline__ int32_t group_min_i32(int32_t v) {
@@ -69,6 +80,8 @@ __device__ __forceinline__ int32_t group_min_i32(int32_t v) {
   if constexpr (G >= 4) { o = (int32_t)gdpp<0x4E>((uint32_t)v); v = o < v ? o : v; }
   if constexpr (G >= 8) { o = (int32_t)gdpp<0x141>((uint32_t)v); v = o < v ? o : v; }
   if constexpr (G >= 16) { o = (int32_t)gdpp<0x140>((uint32_t)v); v = o < v ? o : v; }
+  if constexpr (G >= 32) { o = __shfl_xor(v, 16, 64); v = o < v ? o : v; }
+  if constexpr (G >= 64) { o = __shfl_xor(v, 32, 64); v = o < v ? o : v; }
   return v;
 }
 template <int G>
@@ -77,12 +90,14 @@ __device__ __forceinline__ uint32_t group_or(uint32_t v) {
   if constexpr (G >= 4) v |= gdpp<0x4E>(v);
   if constexpr (G >= 8) v |= gdpp<0x141>(v);
   if constexpr (G >= 16) v |= gdpp<0x140>(v);
+  if constexpr (G >= 32) v |= (uint32_t)__shfl_xor((int)v, 16, 64);
+  if constexpr (G >= 64) v |= (uint32_t)__shfl_xor((int)v, 32, 64);
   return v;
 }
 // This lane's group's bits of a wave ballot.
 template <int G>
-__device__ __forceinline__ uint32_t group_bits(uint64_t m, int gbase) {
-  return (uint32_t)(m >> gbase) & (uint32_t)((1u << G) - 1u);
+__device__ __forceinline__ uint64_t group_bits(uint64_t m, int gbase) {
+  return G == 64 ? m : (m >> gbase) & ((1ull << (G & 63)) - 1ull);
 }
 
 // The server this lane owns (fields of DESIGN.md §4, in registers).
@@ -191,7 +206,7 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
     V.head = due ? ((V.head + 1 == Q) ? 0 : V.head + 1) : V.head;
     V.lh = due ? nl : V.lh;
     V.head_tc = due ? nt : V.head_tc;
-    const bool more = group_bits<G>(__ballot(due && V.cnt > 0 && nt <= th), gbase) != 0u;
+    const bool more = group_bits<G>(__ballot(due && V.cnt > 0 && nt <= th), gbase) != 0ull;
     if (!arrival_due && !more) break;  // group-uniform
     const bool arr = arrival_due && !more;
 
@@ -212,7 +227,7 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
       }
     }
     const bool elig = V.act && V.cnt < Q;
-    const uint32_t em = group_bits<G>(__ballot(elig), gbase);
+    const uint64_t em = group_bits<G>(__ballot(elig), gbase);
     int chosen = -1;
     if constexpr (alias) {
       if (n_alias > 0) {
@@ -231,10 +246,10 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
       const bool num = elig && V.score == V.score;
       const float m = key_f32(group_min_i32<G>(num ? f32_key(V.score) : 0x7f800000));
       const int h = (int)__umulhi(E.u2, (uint32_t)S);
-      const int c0 = ((em >> h) & 1u) ? h : (em ? __builtin_ctz(em) : -1);
-      const uint32_t tie = group_bits<G>(__ballot(num && V.score == m), gbase);
-      const uint32_t nan = group_bits<G>(__ballot(V.score != V.score), gbase);
-      chosen = c0 < 0 ? -1 : ((((tie | nan) >> c0) & 1u) ? c0 : (tie ? __builtin_ctz(tie) : -1));
+      const int c0 = ((em >> h) & 1u) ? h : (em ? __builtin_ctzll(em) : -1);
+      const uint64_t tie = group_bits<G>(__ballot(num && V.score == m), gbase);
+      const uint64_t nan = group_bits<G>(__ballot(V.score != V.score), gbase);
+      chosen = c0 < 0 ? -1 : ((((tie | nan) >> c0) & 1u) ? c0 : (tie ? __builtin_ctzll(tie) : -1));
     }
     const bool push = arr && chosen >= 0;
     E.dropped += (arr && chosen < 0) ? 1u : 0u;
@@ -331,7 +346,8 @@ template <int G, int MODE, int POLICY, bool TRACE>
 __global__ void __launch_bounds__(64)
     dynamics_group_kernel(DevState st, SimParams p, const void* action, int action_dtype,
                           int32_t* assign_out, const uint8_t* reset_mask) {
-  static_assert(G == 2 || G == 4 || G == 8 || G == 16, "group = one DPP row or a part of it");
+  static_assert(G == 2 || G == 4 || G == 8 || G == 16 || G == 32 || G == 64,
+                "group = a power of two lanes of the wave");
   constexpr int WL = kGroupWL;
   constexpr bool alias = POLICY == kPolicyAlias;
   __shared__ int2 win[WL * 64];

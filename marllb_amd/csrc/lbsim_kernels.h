@@ -25,7 +25,7 @@ namespace lbk {
 
 constexpr int K = 128;   // reservoir slots (reservoir.py:31)
 constexpr int NF = 11;   // observation columns (env.py:46-48)
-constexpr int MAX_S = 16;
+constexpr int MAX_S = 64;  // LBSIM_MAX_SERVERS (S > 16: the server-per-lane dynamics only)
 constexpr int32_t kLastNone = -(1 << 30);
 constexpr int kModeStep = 0;
 // s_waitcnt immediate with vmcnt = 0 and expcnt/lgkmcnt left at their maxima (gfx9 encoding).
@@ -1471,32 +1471,11 @@ __device__ __forceinline__ double pw_sum64(int n, F term) {
   return res;
 }
 
-// RewardFunction.compute on one (S, 11) observation (rewards.py:329-381): values of the active
-// servers (any column > 0, env.py:410-413) at column `field`, metric in float64.  The active
-// servers' indices are packed into a 64-bit nibble list so no runtime-indexed local array (and
-// hence no scratch memory) is needed.
-// Active servers of an (S, 11) row as a bit mask, one thread.
-__device__ __forceinline__ uint32_t active_mask_seq(const float* obs, int S) {
-  uint32_t m = 0;
-  for (int s = 0; s < S; ++s) {
-    bool active = false;
-    for (int f = 0; f < NF; ++f) active |= obs[s * NF + f] > 0.0f;
-    m |= active ? 1u << s : 0u;
-  }
-  return m;
-}
-
-// `act` = the active-server mask.  Inlined, so an LDS row is read with ds_read (no flat loads).
-__device__ __forceinline__ double reward_masked(const float* obs, uint32_t act, int S, int metric,
-                                                int field) {
-  if (field < 0 || field >= NF) return 0.0;
-  uint64_t ids = 0;
-  int n = 0;
-  for (int s = 0; s < S; ++s) {
-    if ((act >> s) & 1u) { ids |= (uint64_t)s << (4 * n); ++n; }
-  }
+// RewardFunction.compute (rewards.py:329-381) over the n values x(0..n-1): the reward field of
+// the active servers (any column > 0, env.py:410-413) in server order, metric in float64.
+template <typename X>
+__device__ __forceinline__ double reward_values(int n, X x, int metric) {
   if (n == 0) return 0.0;
-  auto x = [&](int i) { return (double)obs[(int)((ids >> (4 * i)) & 15u) * NF + field]; };
   const double eps = 1e-10;
   auto var = [&]() {
     const double mean = pw_sum64(n, x) / (double)n;
@@ -1547,8 +1526,29 @@ __device__ __forceinline__ double reward_masked(const float* obs, uint32_t act, 
   }
 }
 
+// Active servers of an (S, 11) row as a bit mask, one thread.
+__device__ __forceinline__ uint64_t active_mask_seq(const float* obs, int S) {
+  uint64_t m = 0;
+  for (int s = 0; s < S; ++s) {
+    bool active = false;
+    for (int f = 0; f < NF; ++f) active |= obs[s * NF + f] > 0.0f;
+    m |= active ? 1ull << s : 0ull;
+  }
+  return m;
+}
+
+// Position of the i-th set bit of m (i < popcount(m)).
+__device__ __forceinline__ int nth_bit(uint64_t m, int i) {
+  for (; i > 0; --i) m &= m - 1ull;
+  return __builtin_ctzll(m);
+}
+
+// One thread, one (S, 11) row (the stateless lbsim_reward entry point).
 __device__ double reward_of(const float* obs, int S, int metric, int field) {
-  return reward_masked(obs, active_mask_seq(obs, S), S, metric, field);
+  if (field < 0 || field >= NF) return 0.0;  // no value has the field (rewards.py:375-376)
+  const uint64_t act = active_mask_seq(obs, S);
+  return reward_values(__popcll(act),
+                       [&](int i) { return (double)obs[nth_bit(act, i) * NF + field]; }, metric);
 }
 
 // ================================================================ observe (one wave = one env)
@@ -1576,16 +1576,23 @@ __global__ void __launch_bounds__(64, kObsWaves<MAXS>)
   if (mode == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
   __shared__ ObsScratch sc;
   __shared__ float s_obs[MAXS * NF];
+  __shared__ float s_act[MAXS];
   const int S = p.S;
   observe_env<MAXS, true, mode == kModeStep>(st, p, b, sc, s_obs, lane);
 
-  // active servers (any column > 0): lane s scans its row, one ballot
+  // active servers (any column > 0): lane s scans its row, one ballot; their reward-field values
+  // compacted into s_act in server order
   bool act = false;
   if (lane < S)
     for (int f = 0; f < NF; ++f) act |= s_obs[lane * NF + f] > 0.0f;
-  const uint32_t act_mask = (uint32_t)__ballot(act);
+  const uint64_t act_mask = __ballot(act);
+  const bool fok = p.reward_field >= 0 && p.reward_field < NF;
+  if (act && fok) s_act[__popcll(act_mask & ((1ull << lane) - 1ull))] = s_obs[lane * NF + p.reward_field];
+  __syncthreads();
   if (mode == kModeStep && lane == 0) {
-    const double r = reward_masked(s_obs, act_mask, S, p.reward_metric, p.reward_field);
+    const double r = fok ? reward_values(__popcll(act_mask), [&](int i) { return (double)s_act[i]; },
+                                         p.reward_metric)
+                         : 0.0;
     out.reward[b] = (float)r;
     const int32_t es = st.ep_step[b] + 1;
     const double er = st.ep_return[b] + r;
@@ -1658,19 +1665,20 @@ __global__ void __launch_bounds__(64)
 __global__ void __launch_bounds__(64)
     alias_tables_kernel(const float* weights, int64_t n, int S, float* odd_out,
                         int32_t* alias_out, int32_t* active_out) {
-  __shared__ int32_t fields[F_NUM * MAX_S * 64];
-  const Lds l{nullptr, fields, (int)threadIdx.x, nullptr};
+  __shared__ int32_t tabw[2 * MAX_S * 64];  // table words [f][k][lane]
+  const int lane = (int)threadIdx.x;
+  auto tab = [&](int f, int k) -> int32_t& { return tabw[(f * MAX_S + k) * 64 + lane]; };
   const int64_t r = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (r >= n) return;
   float w[MAX_S];
 #pragma unroll
   for (int s = 0; s < MAX_S; ++s) w[s] = s < S ? weights[r * S + s] : 0.0f;
-  const int na = build_alias<MAX_S>(w, S, FieldAliasTab<MAX_S>{l});
+  const int na = build_alias<MAX_S>(w, S, tab);
   for (int k = 0; k < S; ++k) {
     const bool v = k < na;
-    odd_out[r * S + k] = v ? __uint_as_float((uint32_t)fld<MAX_S>(l, F_TAB0, k)) : 1.0f;
-    alias_out[r * S + k] = v ? (fld<MAX_S>(l, F_TAB1, k) & 0xFF) : 0;
-    active_out[r * S + k] = v ? (fld<MAX_S>(l, F_TAB1, k) >> 8) : -1;
+    odd_out[r * S + k] = v ? __uint_as_float((uint32_t)tab(0, k)) : 1.0f;
+    alias_out[r * S + k] = v ? (tab(1, k) & 0xFF) : 0;
+    active_out[r * S + k] = v ? (tab(1, k) >> 8) : -1;
   }
 }
 

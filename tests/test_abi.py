@@ -19,7 +19,7 @@ def test_library_loads_and_exports_every_header_symbol():
 def test_version_and_layout_sizes():
     lib = _lib.load()
     assert lib.lbsim_version().startswith(b"lbsim")
-    assert lib.lbsim_abi_version() == 1
+    assert lib.lbsim_abi_version() == 2
     assert lib.lbsim_config_size() == ctypes.sizeof(_lib.LbsimConfig)
     assert lib.lbsim_step_outputs_size() == ctypes.sizeof(_lib.StepOutputs)
 
@@ -37,7 +37,7 @@ def test_defaults_mirror_reference_kwargs():
 @pytest.mark.parametrize("field,value,msg", [
     ("reward_metric", 9, "Unsupported metric"),
     ("action_type", 2, "Unknown action_type"),
-    ("num_servers", 17, "num_servers"),
+    ("num_servers", 65, "num_servers"),
     ("num_servers", 0, "num_servers"),
     ("queue_capacity", 65, "queue_capacity"),
     ("step_interval", 0.0, "step_interval"),

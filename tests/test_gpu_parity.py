@@ -143,6 +143,10 @@ CONFIGS = [
     # slots per server-step
     dict(B=64, S=4, kw={"arrival_rate": 6.0, "server_rates": [3.0, 4.0, 5.0, 6.0]}),
     dict(B=48, S=8, kw={"arrival_rate": 3000.0, "warmup_steps": 1}),
+    # S > 16 (server-per-lane only: 32 / 64 lanes per env): configs[4] read literally, 4 agents x
+    # 16 servers = 64, and a 20-server env on a 32-lane group with two-choice SED
+    dict(B=24, S=64, kw={"arrival_rate": 1600.0}),
+    dict(B=40, S=20, kw={"assign_policy": "sed2", "arrival_rate": 800.0, "normalize_obs": True}),
 ]
 
 
@@ -184,6 +188,10 @@ def test_simulator_bit_exact_vs_oracle(lib, oracle_mod, case, mapping):
     from marllb_amd.env import VecLoadBalanceEnv, make_config
     c = CONFIGS[case]
     B, S, kw = c["B"], c["S"], resolve_kw(c["kw"])
+    if mapping == "env" and S > 16:
+        with pytest.raises(ValueError, match="at most 16 servers"):
+            VecLoadBalanceEnv(B, S, device="cuda:0", dyn_mapping=mapping, **kw)
+        return
     kw.setdefault("seed", 1000 + case)
     akw = dict(c["kw"])  # action options (incl. test-only '_' keys)
     env = VecLoadBalanceEnv(B, S, device="cuda:0", autoreset=False, dyn_mapping=mapping, **kw)
