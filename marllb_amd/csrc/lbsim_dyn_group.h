@@ -16,9 +16,9 @@
 //     minimum or NaN, else the lowest eligible server holding the minimum — one DPP min reduction
 //     inside the group's row and two ballots;
 //   SED2 / LSQ2: the two candidates' scores broadcast by OR-reducing a one-hot word.
-// One Philox block per lane per iteration: the chosen server's lane draws its Algorithm R block
-// (the pushed flow's sample is inserted at once if it completes in this step), every other lane
-// the next arrival's block, which the group reads from a lane that is not the chosen one.
+// One Philox block per iteration, the next arrival's (every lane of the group draws the same
+// block); the pushed flow's sample is inserted at once if it completes in this step, with its
+// arrival's draw word as the Algorithm R draw (reservoir_slot_r32).
 // Per-server fields are plain registers (one server per lane); the queue window lives in LDS
 // [slot][lane].
 #pragma once
@@ -235,8 +235,8 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
         chosen = ((em >> a) & 1u) ? a : -1;
       }
     } else if constexpr (two_choice) {
-      const int h1 = (int)__umulhi(E.u2, (uint32_t)S);
-      const int h2 = (int)__umulhi(E.u3, (uint32_t)S);
+      const int h1 = two_choice_h1(E.u2, S);
+      const int h2 = two_choice_h2(E.u2, S);
       const uint32_t bits = __float_as_uint(V.score);
       const float s1 = __uint_as_float(group_or<G>(s == h1 ? bits : 0u));
       const float s2 = __uint_as_float(group_or<G>(s == h2 ? bits : 0u));
@@ -262,16 +262,11 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
     const int32_t tc_a = start_a + svc;
     const bool ins = mine && tc_a <= dt;  // completes in this step: its sample now
 
-    // ---- one Philox block per lane: the chosen lane draws its reservoir block, the others the
-    //      next arrival's, which the group then reads from a lane that is not the chosen one
-    const u32x4 d = philox4x32_10(
-        mine ? u32x4{V.rcnt >> 1, E.gid, E.episode, (kStreamReservoir << 24) | (uint32_t)s}
-             : u32x4{E.arr_idx + 1u, E.gid, E.episode, kStreamArrival << 24},
-        p.key0, p.key1);
-    const int src = gbase + (chosen == 0 ? 1 : 0);  // never the chosen lane (G >= 2)
-    const u32x4 da = u32x4{(uint32_t)__shfl((int)d.x, src, 64), (uint32_t)__shfl((int)d.y, src, 64),
-                           (uint32_t)__shfl((int)d.z, src, 64), (uint32_t)__shfl((int)d.w, src, 64)};
-    const int slot = reservoir_slot(V.rcnt, d);
+    // ---- the next arrival's Philox block (the same in every lane of the group); the pushed
+    //      flow's Algorithm R draw is this arrival's word r (E.u3)
+    const u32x4 da = philox4x32_10(u32x4{E.arr_idx + 1u, E.gid, E.episode, kStreamArrival << 24},
+                                   p.key0, p.key1);
+    const int slot = reservoir_slot_r32(V.rcnt, E.u3);
     if (ins && slot >= 0) {
       my_res[(uint32_t)slot] = make_uint3((uint32_t)(tc_a - ta), (uint32_t)svc,
                                           base_ms + (base_rem + (uint32_t)tc_a) / 1000u);

@@ -36,8 +36,8 @@ struct DevState {
   // per env [B]
   int32_t* next_arr;    // relative us of the next arrival (>= 0 after rebase)
   float* next_work;     // Exp(1) work of the next arrival
-  uint32_t* next_u2;    // hash word of the next arrival (SED start / first 2-choice candidate)
-  uint32_t* next_u3;    // second 2-choice candidate
+  uint32_t* next_u2;    // hash word of the next arrival (SED start; 2-choice: both candidates)
+  uint32_t* next_u3;    // Algorithm R draw word of the next arrival's flow (reservoir_slot_r32)
   uint32_t* arr_idx;    // Philox counter of the next arrival
   uint32_t* episode;    // episode index (RNG counter word z)
   uint32_t* clock;      // simulated steps since reset (warm-up included)
@@ -384,15 +384,30 @@ __device__ __forceinline__ void clear_servers(const SimParams& p, LaneState<MAXS
   }
 }
 
-// Algorithm R slot (reservoir.py:64-85) of the sample that makes count cres + 1: slot cres while
-// the reservoir fills, else j = randint(0, cres + 1) from the 64-bit half (cres & 1) of the Philox
-// block d of index cres >> 1, kept if j < K (-1: not stored).
+// Algorithm R slot (reservoir.py:64-85) of the sample that makes count cres + 1, for a flow
+// carried in from an earlier step: slot cres while the reservoir fills, else j = randint(0,
+// cres + 1) from the 64-bit half (cres & 1) of the reservoir-stream Philox block d of index
+// cres >> 1, kept if j < K (-1: not stored).
 __device__ __forceinline__ int reservoir_slot(uint32_t cres, const u32x4& d) {
   const uint32_t hi = (cres & 1u) ? d.w : d.y;
   const uint32_t lo = (cres & 1u) ? d.z : d.x;
   const uint64_t j = mulhi64_by_u33(hi, lo, (uint64_t)cres + 1u);
   return cres < (uint32_t)K ? (int)cres : (j < (uint64_t)K ? (int)j : -1);
 }
+
+// Algorithm R slot of a flow that arrives and completes in the same step: the draw is its arrival's
+// word r (word w of the arrival's Philox block, drawn when the arrival was), j = floor(r (cres + 1)
+// / 2^32) (Lemire multiply-shift; r·cres + r is one v_mad_u64_u32 and never overflows 64 bits;
+// bias <= (cres + 1) / 2^32).  No Philox block per insert.
+__device__ __forceinline__ int reservoir_slot_r32(uint32_t cres, uint32_t r) {
+  const uint32_t j = (uint32_t)(((uint64_t)r * cres + r) >> 32);
+  return cres < (uint32_t)K ? (int)cres : (j < (uint32_t)K ? (int)j : -1);
+}
+
+// SED2 / LSQ2 candidates from the arrival's hash word u: the high and the low 16 bits, each
+// mapped to [0, S) by multiply-shift (node.c:409-441's two hashes).
+__device__ __forceinline__ int two_choice_h1(uint32_t u, int S) { return (int)(((u >> 16) * (uint32_t)S) >> 16); }
+__device__ __forceinline__ int two_choice_h2(uint32_t u, int S) { return (int)(((u & 0xFFFFu) * (uint32_t)S) >> 16); }
 
 __device__ __forceinline__ uint32_t count_inc(uint32_t c) { return c != 0xFFFFFFFFu ? c + 1u : c; }
 
@@ -564,8 +579,8 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
         chosen = sel<MAXS>(L.cnt, a) < Q ? a : -1;
       }
     } else if constexpr (two_choice) {  // SED2 / LSQ2: keep the second candidate if strictly better
-      const int h1 = (int)__umulhi(L.u2, (uint32_t)S);  // (u * S) >> 32
-      const int h2 = (int)__umulhi(L.u3, (uint32_t)S);
+      const int h1 = two_choice_h1(L.u2, S);
+      const int h2 = two_choice_h2(L.u2, S);
       float s1 = 0.f, s2 = 0.f;
       bool ok1 = false, ok2 = false;
 #pragma unroll
@@ -632,12 +647,11 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
     // completes in this step: its sample now (duration = tc - max(ta, predecessor's tc) = svc)
     const bool ins = push && tc_a <= dt;
 
-    // ---- two Philox blocks: the pushed flow's Algorithm R draw, the next arrival's draw
-    const u32x4 dr = philox_rk(
-        u32x4{cres >> 1, L.gid, L.episode, (kStreamReservoir << 24) | (uint32_t)cs}, ec.rk0, ec.rk1);
+    // ---- one Philox block, the next arrival's; the pushed flow's Algorithm R draw is this
+    //      arrival's word r (L.u3)
     const u32x4 d = philox_rk(u32x4{L.arr_idx + 1u, L.gid, L.episode, kStreamArrival << 24},
                               ec.rk0, ec.rk1);
-    const int slot = reservoir_slot(cres, dr);
+    const int slot = reservoir_slot_r32(cres, L.u3);
     if (ins && slot >= 0) {
       my_res[(uint32_t)cs * (uint32_t)K + (uint32_t)slot] =
           make_uint3((uint32_t)(tc_a - ta), (uint32_t)svc,
@@ -733,8 +747,8 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
 //      now if it completes in this step (Algorithm R draw of the server's count);
 //   3. after the last arrival, the pops up to dt; then the rebase.
 // The body is straight-line and predicated, so the 64 lanes (64 envs) stay converged; an iteration
-// costs one arrival's work (two Philox blocks: the next arrival's draw and the pushed flow's
-// Algorithm R draw), and a lane iterates ~arrivals times instead of arrivals + completions.  Every
+// costs one arrival's work (one Philox block, the next arrival's draw, whose word w is also that
+// flow's Algorithm R draw), and a lane iterates ~arrivals times instead of arrivals + completions.  Every
 // reservoir gets the same insert sequence as the oracle's event order, so the state is bit-identical.
 template <int MAXS, int POLICY, bool TRACE>
 __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,

@@ -59,6 +59,7 @@ def load() -> ctypes.CDLL:
         "oracle_gen_alias": (None, [_P, ctypes.c_int, _P, _P]),
         "oracle_algr_slot": (ctypes.c_long, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                              ctypes.c_uint32, _P]),
+        "oracle_algr_slot_r32": (ctypes.c_long, [ctypes.c_uint32, ctypes.c_uint32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -313,6 +313,9 @@ typedef struct oracle {
   double* norm_mean; double* norm_std;
   /* TRACE arrivals (lbsim_set_trace semantics): us gap before each row, mean-1 work */
   uint32_t* trace_gap; float* trace_work; uint32_t trace_rows;
+  /* not state: the Algorithm R draw word of each queued flow that arrived in the current step,
+   * [B*S*Q] by ring position (written at the push, read at the pop in the same step) */
+  uint32_t* flow_r;
 } oracle_t;
 
 static void derive(oracle_t* o) {
@@ -356,6 +359,8 @@ oracle_t* oracle_create(const lbsim_config_t* cfg) {
   }
   if (cfg->normalize_obs)
     for (size_t i = 0; i < BS * NF; ++i) o->norm_std[i] = 1.0; /* env.py:153 */
+  o->flow_r = (uint32_t*)calloc(BSQ ? BSQ : 1, 4);
+  if (!o->flow_r) { free(o->buf); free(o); return NULL; }
   return o;
 }
 
@@ -363,6 +368,7 @@ void oracle_destroy(oracle_t* o) {
   if (!o) return;
   free(o->trace_gap);
   free(o->trace_work);
+  free(o->flow_r);
   free(o->buf);
   free(o);
 }
@@ -448,17 +454,31 @@ static void ring_set(oracle_t* o, size_t sb, int head, int cnt) {
   o->hc[sb] = (uint32_t)head | ((uint32_t)cnt << 16);
 }
 
-/* Algorithm R insert of one completion into both reservoirs of server s (shared decision). */
 /* A reservoir sample in seconds from its integer-microsecond form (env.py reports seconds). */
 static float us_to_seconds(uint32_t us) { return (float)us * 1.0e-6f; }
 
-static void reservoir_add(env_ctx* e, int s, uint32_t fct, uint32_t dur, uint32_t ts_ms) {
+/* Algorithm R slot for a flow that arrived in the step it completes in: the draw
+ * is its arrival's word r (word 3 of the arrival's Philox block), j = floor(r (c + 1) / 2^32)
+ * (reservoir.py:76 randint(0, count + 1), Lemire multiply-shift). */
+long oracle_algr_slot_r32(uint32_t count, uint32_t r) {
+  if (count < (uint32_t)K) return (long)count;
+  const uint64_t j = ((uint64_t)r * ((uint64_t)count + 1u)) >> 32;
+  return j < (uint64_t)K ? (long)j : -1;
+}
+
+/* Algorithm R insert of one completion into both reservoirs of server s (shared decision).  A
+ * flow that arrived in this step (has_r) uses its arrival's draw word r; a flow carried in from an
+ * earlier step uses the reservoir stream's block (count >> 1), half (count & 1). */
+static void reservoir_add(env_ctx* e, int s, uint32_t fct, uint32_t dur, uint32_t ts_ms, int has_r,
+                          uint32_t r) {
   oracle_t* o = e->o;
   const size_t sb = e->b * (size_t)o->S + (size_t)s;
   const uint32_t c = o->res_count[sb];
   long slot;
   if (c < (uint32_t)K) {
     slot = (long)c;
+  } else if (has_r) {
+    slot = oracle_algr_slot_r32(c, r);
   } else {
     const uint32_t ctr[4] = {c >> 1, e->gid, o->episode[e->b], (2u << 24) | (uint32_t)s};
     uint32_t d[4];
@@ -493,7 +513,8 @@ static void pop_until(env_ctx* e, int s, int32_t t, uint64_t base_us, double den
     const uint32_t dur = (uint32_t)(tc - start);
     o->last_tc[sb] = tc;
     const uint32_t ts_ms = (uint32_t)((base_us + (uint64_t)(int64_t)tc) / 1000u);
-    reservoir_add(e, s, fct, dur, ts_ms);
+    /* ta >= 0: arrived in this step (times are relative to the step start) */
+    reservoir_add(e, s, fct, dur, ts_ms, ta >= 0, o->flow_r[sb * o->Q + (size_t)head]);
     head = head + 1 == o->Q ? 0 : head + 1;
     cnt -= 1;
   }
@@ -566,9 +587,10 @@ static void sim_step(env_ctx* e, const float* w) {
         if (cnt[act[k]] < Q) chosen = act[k];
       }
     } else if (policy == LBSIM_POLICY_SED2 || policy == LBSIM_POLICY_LSQ2) {
-      /* node.c:409-417 / 433-441: two candidates, keep the second only if strictly better */
-      const int h1 = (int)(((uint64_t)o->next_u2[b] * (uint64_t)S) >> 32);
-      const int h2 = (int)(((uint64_t)o->next_u3[b] * (uint64_t)S) >> 32);
+      /* node.c:409-417 / 433-441: two candidates, keep the second only if strictly better; the
+       * candidates are the hash word's high and low 16 bits mapped to [0, S) */
+      const int h1 = (int)(((o->next_u2[b] >> 16) * (uint32_t)S) >> 16);
+      const int h2 = (int)(((o->next_u2[b] & 0xFFFFu) * (uint32_t)S) >> 16);
       const int ok1 = cnt[h1] < Q, ok2 = cnt[h2] < Q;
       if (ok1 && ok2) chosen = sc[h2] < sc[h1] ? h2 : h1;
       else if (ok1) chosen = h1;
@@ -600,6 +622,7 @@ static void sim_step(env_ctx* e, const float* w) {
       if (pos >= Q) pos -= Q;
       o->ring[(sb * Q + (size_t)pos) * 2] = start + svc;
       o->ring[(sb * Q + (size_t)pos) * 2 + 1] = ta;
+      o->flow_r[sb * Q + (size_t)pos] = o->next_u3[b];
       ring_set(o, sb, head, c + 1);
       e->assigned[s] += 1;
     }

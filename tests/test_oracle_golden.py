@@ -124,6 +124,38 @@ def test_algorithm_r_acceptance_rate(oracle_mod):
         assert abs(acc / 20000 - p) < 5 * math.sqrt(p * (1 - p) / 20000) + 1e-4
 
 
+def test_algorithm_r_arrival_draw_rule(oracle_mod):
+    """The in-step rule (a flow that arrives and completes in one step): j = floor(r (c + 1) /
+    2^32) from its arrival's Philox word 3: exact edges, then every stream
+    element kept with probability K/N and the acceptance rate K/(c + 1)."""
+    lib = oracle_mod.load()
+    K = 128
+    assert lib.oracle_algr_slot_r32(5, 0xFFFFFFFF) == 5          # filling: slot = count
+    assert lib.oracle_algr_slot_r32(K, 0) == 0
+    assert lib.oracle_algr_slot_r32(K, 0xFFFFFFFF) == -1         # j = count = 128: not kept
+    assert lib.oracle_algr_slot_r32(2 ** 32 - 1, 127) == 127     # c + 1 = 2^32: j = r
+    key = np.array([12345, 678], np.uint32)
+    N, trials = 1000, 500
+    counts = np.zeros(N)
+    for t in range(trials):
+        slots = np.arange(K)
+        for c in range(K, N):  # the arrival block of arrival c of "env" t
+            r = int(oracle_mod.philox(np.array([c, t, 1, 1 << 24], np.uint32), key)[3])
+            j = lib.oracle_algr_slot_r32(c, r)
+            if j >= 0:
+                slots[j] = c
+        counts[slots] += 1
+    expected = trials * K / N
+    chi2 = np.sum((counts - expected) ** 2 / expected)
+    assert chi2 < 1100, chi2
+    for count in (128, 1000, 100000, 2 ** 31 - 5):
+        acc = sum(lib.oracle_algr_slot_r32(
+            count, int(oracle_mod.philox(np.array([e, 7, 3, 1 << 24], np.uint32), key)[3])) >= 0
+            for e in range(20000))
+        p = 128 / (count + 1)
+        assert abs(acc / 20000 - p) < 5 * math.sqrt(p * (1 - p) / 20000) + 1e-4
+
+
 def test_gen_alias_matches_reference(oracle_mod, golden_dir):
     """oracle_gen_alias == the reference gen_alias (src/lb/shm_proxy.py:127-146) bit for bit in
     float64, on 137 weight vectors (n = 1..16, ties with the mean, the SURVEY §8a example)."""
