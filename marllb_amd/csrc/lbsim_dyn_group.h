@@ -16,9 +16,11 @@
 //     minimum or NaN, else the lowest eligible server holding the minimum — one DPP min reduction
 //     inside the group's row and two ballots;
 //   SED2 / LSQ2: the two candidates' scores broadcast by OR-reducing a one-hot word.
-// One Philox block per iteration, the next arrival's (every lane of the group draws the same
-// block); the pushed flow's sample is inserted at once if it completes in this step, with its
-// arrival's draw word as the Algorithm R draw (reservoir_slot_r32).
+// Arrivals are drawn ahead, G at a time: every G iterations lane j of a group draws the group's
+// arrival cbase + j (Philox block, gap, work) into LDS, so the Philox block and its two logs cost
+// one pass per G iterations (the loop is latency-bound at small batches: these were the longest
+// chain of an iteration).  The pushed flow's sample is inserted at once if it completes in this
+// step, with its arrival's draw word as the Algorithm R draw (reservoir_slot_r32).
 // Per-server fields are plain registers (one server per lane); the queue window lives in LDS
 // [slot][lane].
 #pragma once
@@ -118,18 +120,204 @@ struct GroupAliasTab {
   __device__ int32_t& operator()(int f, int k) const { return t[f * 64 + gbase + k]; }
 };
 
+// Loop constants of one step (as dynamics_kernel's EvConst): Philox round keys and the scalars the
+// loop reads, pinned in VGPRs so the loop never reloads them from the kernarg segment.
+struct GroupConst {
+  uint32_t rk0[10], rk1[10];
+  float mean_gap;
+  int32_t dt;
+  uint32_t base_ms, base_rem;
+};
+__device__ __forceinline__ GroupConst group_const(const SimParams& p, uint32_t base_ms,
+                                                  uint32_t base_rem) {
+  GroupConst c;
+  uint32_t k0 = p.key0, k1 = p.key1;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    c.rk0[r] = vpin(k0);
+    c.rk1[r] = vpin(k1);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  c.mean_gap = vpin(p.mean_gap_us);
+  c.dt = vpin(p.dt_us);
+  c.base_ms = vpin(base_ms);
+  c.base_rem = vpin(base_rem);
+  return c;
+}
+
+// The event loop of sim_step_group (section 2).  FAST (wave-uniform): every SED score finite, so no
+// NaN fallback division and no NaN ballot.
+template <int G, int POLICY, bool TRACE, bool FAST>
+__device__ __forceinline__ void group_event_loop(const DevState& st, const SimParams& p,
+                                                 LaneState<1>& E, SrvLane& V, int s, int gbase,
+                                                 int n_alias, const GroupConst& gc, int2* win,
+                                                 int32_t* atab, int4* acache, uint3* const my_res,
+                                                 int2* const my_ring) {
+  constexpr int WL = kGroupWL;
+  constexpr bool two_choice = (POLICY == 1 || POLICY == 3);
+  constexpr bool alias = POLICY == kPolicyAlias;
+  constexpr bool lsq = (POLICY == 2 || POLICY == 3);
+  const int S = p.S, Q = p.Q;
+  const int32_t dt = gc.dt;
+  const GroupAliasTab tab{atab, gbase};
+  const int lane = gbase + s;
+  auto wslot = [&](int i) -> int2* { return win + i * 64 + lane; };
+  auto mark = [&](int slot) {  // the slot's bit in the lane's 128-bit written-slot mask
+    const uint32_t bit = 1u << (slot & 31), w = (uint32_t)slot >> 5;
+    V.chg[0] |= w == 0 ? bit : 0u;
+    V.chg[1] |= w == 1 ? bit : 0u;
+    V.chg[2] |= w == 2 ? bit : 0u;
+    V.chg[3] |= w == 3 ? bit : 0u;
+  };
+  // Draw-ahead: every G iterations (a wave-uniform schedule: all active groups loop in step) lane
+  // j of a group draws arrival cbase + j (cbase = the group's next undrawn arrival) -- its Philox
+  // block, gap and work -- into the group's slots acache[gbase + j].  One arrival at most is
+  // consumed per iteration, so the G slots last until the next refill, and the Philox block and
+  // the two logs cost one pass per G iterations instead of one per iteration.
+  uint32_t cbase = 0u;
+  uint32_t it = 0u;
+  for (;;) {
+    if ((it & (uint32_t)(G - 1)) == 0u) {
+      cbase = E.arr_idx + 1u;
+      const uint32_t k = cbase + (uint32_t)s;
+      const u32x4 d = philox_rk(u32x4{k, E.gid, E.episode, kStreamArrival << 24}, gc.rk0, gc.rk1);
+      int32_t gap;
+      float wk;
+      if constexpr (TRACE) {
+        const uint32_t r = trace_row(p, E.gid, E.episode, k);
+        gap = (int32_t)st.trace_gap[r];
+        wk = st.trace_work[r];
+      } else {
+        gap = (int32_t)(-lb_logf(u01_open0(d.x)) * gc.mean_gap);
+        wk = -lb_logf(u01_open0(d.y));
+      }
+      acache[lane] = make_int4(gap, __float_as_int(wk), (int)d.z, (int)d.w);
+      __builtin_amdgcn_wave_barrier();
+    }
+    ++it;
+    const bool arrival_due = E.next_arr < dt;  // the same in every lane of the group
+    const int32_t th = arrival_due ? E.next_arr : dt;
+    const bool due = V.act && V.cnt > 0 && V.head_tc <= th;
+    if (due && V.cnt > WL) {  // rare: the slot the pop frees takes queue entry WL from the ring
+      int pw = V.head + WL;
+      pw = pw >= Q ? pw - Q : pw;
+      *wslot(V.lh) = my_ring[(uint32_t)pw];
+      __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+    }
+    const int nl = (V.lh + 1) & (WL - 1);
+    const int32_t nt = wslot(nl)->x;  // next head (valid if cnt > 1)
+    V.last = due ? V.head_tc : V.last;
+    V.cnt -= due ? 1 : 0;
+    V.head = due ? ((V.head + 1 == Q) ? 0 : V.head + 1) : V.head;
+    V.lh = due ? nl : V.lh;
+    V.head_tc = due ? nt : V.head_tc;
+    const bool more = group_bits<G>(__ballot(due && V.cnt > 0 && nt <= th), gbase) != 0ull;
+    if (!arrival_due && !more) break;  // group-uniform
+    const bool arr = arrival_due && !more;
+
+    // ---- the arrival: choose a server (node.c:388-441); full servers are not eligible
+    const int32_t ta = E.next_arr;
+    if constexpr (!alias) {
+      if constexpr (lsq) {
+        V.score = (float)V.cnt;
+      } else {  // (cnt + 1) / den correctly rounded (Markstein), division for den 0 / inf / NaN
+        const double c = (double)(V.cnt + 1);
+        const double q0 = c * V.rcp;
+        double q = fma(fma(-q0, V.den, c), V.rcp, q0);
+        if (!FAST && q != q) {
+          asm volatile("");
+          q = c / V.den;
+        }
+        V.score = (float)q;
+      }
+    }
+    const bool elig = V.act && V.cnt < Q;
+    const uint64_t em = group_bits<G>(__ballot(elig), gbase);
+    int chosen = -1;
+    if constexpr (alias) {
+      if (n_alias > 0) {
+        const int a = alias_pick(tab, n_alias, E.u2);
+        chosen = ((em >> a) & 1u) ? a : -1;
+      }
+    } else if constexpr (two_choice) {
+      const int h1 = two_choice_h1(E.u2, S);
+      const int h2 = two_choice_h2(E.u2, S);
+      const uint32_t bits = __float_as_uint(V.score);
+      const float s1 = __uint_as_float(group_or<G>(s == h1 ? bits : 0u));
+      const float s2 = __uint_as_float(group_or<G>(s == h2 ? bits : 0u));
+      const bool ok1 = (em >> h1) & 1u, ok2 = (em >> h2) & 1u;
+      chosen = (ok1 && ok2) ? ((s2 < s1) ? h2 : h1) : (ok1 ? h1 : (ok2 ? h2 : -1));
+    } else {
+      const bool num = elig && V.score == V.score;
+      const float m = key_f32(group_min_i32<G>(num ? f32_key(V.score) : 0x7f800000));
+      const int h = (int)__umulhi(E.u2, (uint32_t)S);
+      const int c0 = ((em >> h) & 1u) ? h : (em ? __builtin_ctzll(em) : -1);
+      const uint64_t tie = group_bits<G>(__ballot(num && V.score == m), gbase);
+      const uint64_t nan = FAST ? 0ull : group_bits<G>(__ballot(V.score != V.score), gbase);
+      chosen = c0 < 0 ? -1 : ((((tie | nan) >> c0) & 1u) ? c0 : (tie ? __builtin_ctzll(tie) : -1));
+    }
+    const bool push = arr && chosen >= 0;
+    E.dropped += (arr && chosen < 0) ? 1u : 0u;
+    const bool mine = push && s == chosen;
+
+    // ---- FIFO service on the chosen server (its lane)
+    const int32_t start_a = V.cnt > 0 ? (V.tail > ta ? V.tail : ta) : ta;
+    int32_t svc = (int32_t)(E.next_work * V.scale);
+    svc = svc < 1 ? 1 : svc;
+    const int32_t tc_a = start_a + svc;
+    const bool ins = mine && tc_a <= dt;  // completes in this step: its sample now
+
+    // ---- the pushed flow's Algorithm R draw is this arrival's word r (E.u3)
+    const int slot = reservoir_slot_r32(V.rcnt, E.u3);
+    if (ins && slot >= 0) {
+      my_res[(uint32_t)slot] = make_uint3((uint32_t)(tc_a - ta), (uint32_t)svc,
+                                          gc.base_ms + (gc.base_rem + (uint32_t)tc_a) / 1000u);
+      mark(slot);
+    }
+    if (mine) {
+      const int2 e = make_int2(tc_a, ta);
+      if (V.cnt < WL) {
+        *wslot((V.lh + V.cnt) & (WL - 1)) = e;
+      } else {
+        int pos = V.head + V.cnt;
+        pos = pos >= Q ? pos - Q : pos;
+        my_ring[(uint32_t)pos] = e;
+        asm volatile("");  // no flat store (see dynamics_kernel)
+      }
+      V.tail = tc_a;
+      V.assigned += 1;
+      V.head_tc = V.cnt == 0 ? tc_a : V.head_tc;
+      V.cnt += 1;
+      V.rcnt = ins ? count_inc(V.rcnt) : V.rcnt;
+    }
+
+    // ---- next arrival (identical in every lane of the group): arrival arr_idx + 1 from the
+    //      group's draw-ahead slots
+    const int4 nx = acache[gbase + (int)(E.arr_idx + 1u - cbase)];
+    const int32_t na = ta + nx.x;
+    const float nw = __int_as_float(nx.y);
+    const uint32_t nu2 = (uint32_t)nx.z, nu3 = (uint32_t)nx.w;
+    E.next_arr = arr ? na : E.next_arr;
+    E.next_work = arr ? nw : E.next_work;
+    E.u2 = arr ? nu2 : E.u2;
+    E.u3 = arr ? nu3 : E.u3;
+    E.arr_idx += arr ? 1u : 0u;
+  }
+
+}
+
 template <int G, int POLICY, bool TRACE>
 __device__ __forceinline__ void sim_step_group(const DevState& st, const SimParams& p,
                                                LaneState<1>& E, SrvLane& V, uint32_t b, int s,
                                                int gbase, float w_own, const float (&wall)[G],
-                                               int2* win, int32_t* atab) {
+                                               int2* win, int32_t* atab, int4* acache) {
   constexpr int WL = kGroupWL;
   const int S = p.S, Q = p.Q;
   const int32_t dt = p.dt_us;
   const uint64_t base_us = (uint64_t)E.clock * (uint64_t)dt;
   const uint32_t base_ms = (uint32_t)(base_us / 1000u);
   const uint32_t base_rem = (uint32_t)(base_us - (uint64_t)base_ms * 1000u);
-  constexpr bool two_choice = (POLICY == 1 || POLICY == 3);
   constexpr bool alias = POLICY == kPolicyAlias;
   constexpr bool lsq = (POLICY == 2 || POLICY == 3);
   const uint32_t sb = b * (uint32_t)S + (uint32_t)s;  // valid when V.act
@@ -188,130 +376,18 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
     V.rcnt = rc;
   }
 
-  // ---- 2. one arrival per iteration (as dynamics_kernel's sim_step), the group in step
-  for (;;) {
-    const bool arrival_due = E.next_arr < dt;  // the same in every lane of the group
-    const int32_t th = arrival_due ? E.next_arr : dt;
-    const bool due = V.act && V.cnt > 0 && V.head_tc <= th;
-    if (due && V.cnt > WL) {  // rare: the slot the pop frees takes queue entry WL from the ring
-      int pw = V.head + WL;
-      pw = pw >= Q ? pw - Q : pw;
-      *wslot(V.lh) = my_ring[(uint32_t)pw];
-      __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
-    }
-    const int nl = (V.lh + 1) & (WL - 1);
-    const int32_t nt = wslot(nl)->x;  // next head (valid if cnt > 1)
-    V.last = due ? V.head_tc : V.last;
-    V.cnt -= due ? 1 : 0;
-    V.head = due ? ((V.head + 1 == Q) ? 0 : V.head + 1) : V.head;
-    V.lh = due ? nl : V.lh;
-    V.head_tc = due ? nt : V.head_tc;
-    const bool more = group_bits<G>(__ballot(due && V.cnt > 0 && nt <= th), gbase) != 0ull;
-    if (!arrival_due && !more) break;  // group-uniform
-    const bool arr = arrival_due && !more;
-
-    // ---- the arrival: choose a server (node.c:388-441); full servers are not eligible
-    const int32_t ta = E.next_arr;
-    if constexpr (!alias) {
-      if constexpr (lsq) {
-        V.score = (float)V.cnt;
-      } else {  // (cnt + 1) / den correctly rounded (Markstein), division for den 0 / inf / NaN
-        const double c = (double)(V.cnt + 1);
-        const double q0 = c * V.rcp;
-        double q = fma(fma(-q0, V.den, c), V.rcp, q0);
-        if (q != q) {
-          asm volatile("");
-          q = c / V.den;
-        }
-        V.score = (float)q;
-      }
-    }
-    const bool elig = V.act && V.cnt < Q;
-    const uint64_t em = group_bits<G>(__ballot(elig), gbase);
-    int chosen = -1;
-    if constexpr (alias) {
-      if (n_alias > 0) {
-        const int a = alias_pick(tab, n_alias, E.u2);
-        chosen = ((em >> a) & 1u) ? a : -1;
-      }
-    } else if constexpr (two_choice) {
-      const int h1 = two_choice_h1(E.u2, S);
-      const int h2 = two_choice_h2(E.u2, S);
-      const uint32_t bits = __float_as_uint(V.score);
-      const float s1 = __uint_as_float(group_or<G>(s == h1 ? bits : 0u));
-      const float s2 = __uint_as_float(group_or<G>(s == h2 ? bits : 0u));
-      const bool ok1 = (em >> h1) & 1u, ok2 = (em >> h2) & 1u;
-      chosen = (ok1 && ok2) ? ((s2 < s1) ? h2 : h1) : (ok1 ? h1 : (ok2 ? h2 : -1));
-    } else {
-      const bool num = elig && V.score == V.score;
-      const float m = key_f32(group_min_i32<G>(num ? f32_key(V.score) : 0x7f800000));
-      const int h = (int)__umulhi(E.u2, (uint32_t)S);
-      const int c0 = ((em >> h) & 1u) ? h : (em ? __builtin_ctzll(em) : -1);
-      const uint64_t tie = group_bits<G>(__ballot(num && V.score == m), gbase);
-      const uint64_t nan = group_bits<G>(__ballot(V.score != V.score), gbase);
-      chosen = c0 < 0 ? -1 : ((((tie | nan) >> c0) & 1u) ? c0 : (tie ? __builtin_ctzll(tie) : -1));
-    }
-    const bool push = arr && chosen >= 0;
-    E.dropped += (arr && chosen < 0) ? 1u : 0u;
-    const bool mine = push && s == chosen;
-
-    // ---- FIFO service on the chosen server (its lane)
-    const int32_t start_a = V.cnt > 0 ? (V.tail > ta ? V.tail : ta) : ta;
-    int32_t svc = (int32_t)(E.next_work * V.scale);
-    svc = svc < 1 ? 1 : svc;
-    const int32_t tc_a = start_a + svc;
-    const bool ins = mine && tc_a <= dt;  // completes in this step: its sample now
-
-    // ---- the next arrival's Philox block (the same in every lane of the group); the pushed
-    //      flow's Algorithm R draw is this arrival's word r (E.u3)
-    const u32x4 da = philox4x32_10(u32x4{E.arr_idx + 1u, E.gid, E.episode, kStreamArrival << 24},
-                                   p.key0, p.key1);
-    const int slot = reservoir_slot_r32(V.rcnt, E.u3);
-    if (ins && slot >= 0) {
-      my_res[(uint32_t)slot] = make_uint3((uint32_t)(tc_a - ta), (uint32_t)svc,
-                                          base_ms + (base_rem + (uint32_t)tc_a) / 1000u);
-      mark(slot);
-    }
-    if (mine) {
-      const int2 e = make_int2(tc_a, ta);
-      if (V.cnt < WL) {
-        *wslot((V.lh + V.cnt) & (WL - 1)) = e;
-      } else {
-        int pos = V.head + V.cnt;
-        pos = pos >= Q ? pos - Q : pos;
-        my_ring[(uint32_t)pos] = e;
-        asm volatile("");  // no flat store (see dynamics_kernel)
-      }
-      V.tail = tc_a;
-      V.assigned += 1;
-      V.head_tc = V.cnt == 0 ? tc_a : V.head_tc;
-      V.cnt += 1;
-      V.rcnt = ins ? count_inc(V.rcnt) : V.rcnt;
-    }
-
-    // ---- next arrival (identical in every lane of the group)
-    int32_t na;
-    float nw;
-    uint32_t nu2, nu3;
-    if constexpr (TRACE) {
-      na = ta + E.pf_gap;
-      nw = E.pf_work;
-      nu2 = da.z;
-      nu3 = da.w;
-      if (arr) {
-        E.row = (E.row + 1u == p.trace_rows) ? 0u : E.row + 1u;
-        E.pf_gap = (int32_t)st.trace_gap[E.row];
-        E.pf_work = st.trace_work[E.row];
-      }
-    } else {
-      arrival_from_draw(p, da, ta, na, nw, nu2, nu3);
-    }
-    E.next_arr = arr ? na : E.next_arr;
-    E.next_work = arr ? nw : E.next_work;
-    E.u2 = arr ? nu2 : E.u2;
-    E.u3 = arr ? nu3 : E.u3;
-    E.arr_idx += arr ? 1u : 0u;
-  }
+  // ---- 2. one arrival per iteration (as dynamics_kernel's sim_step), the group in step.  SED /
+  //      SED2 scores can only be NaN when some den is 0 / inf / NaN: a wave whose servers all have
+  //      finite scores runs the loop without the NaN fallbacks (a wave-uniform choice).
+  const GroupConst gc = group_const(p, base_ms, base_rem);
+  const bool finite = lsq || alias || !V.act ||
+                      (fabs(V.den) >= 1e-30 && fabs(V.den) <= 1e300);  // false for NaN
+  if (__all(finite))
+    group_event_loop<G, POLICY, TRACE, true>(st, p, E, V, s, gbase, n_alias, gc, win, atab, acache, my_res,
+                                             my_ring);
+  else
+    group_event_loop<G, POLICY, TRACE, false>(st, p, E, V, s, gbase, n_alias, gc, win, atab, acache, my_res,
+                                              my_ring);
 
   // ---- rebase to the next step's start (this lane's server)
   E.next_arr -= dt;
@@ -347,6 +423,7 @@ __global__ void __launch_bounds__(64)
   constexpr bool alias = POLICY == kPolicyAlias;
   __shared__ int2 win[WL * 64];
   __shared__ int32_t atab[alias ? 2 * 64 : 1];
+  __shared__ int4 acache[64];  // draw-ahead arrival slots, [group][G]
   const int lane = (int)threadIdx.x;
   const int s = lane & (G - 1);
   const int gbase = lane & ~(G - 1);
@@ -379,7 +456,6 @@ __global__ void __launch_bounds__(64)
     E.dropped = 0u;
     E.arr_idx = 0u;
     draw_arrival<1>(st, p, E, 0);
-    trace_prefetch<1>(st, p, E);
     V.cnt = 0;
     V.head_tc = 0;
     V.head = 0;
@@ -389,7 +465,7 @@ __global__ void __launch_bounds__(64)
 #pragma unroll
     for (int k = 0; k < G; ++k) wall[k] = 1.0f;
     for (int k = 0; k < p.warmup_steps; ++k)
-      sim_step_group<G, POLICY, TRACE>(st, p, E, V, b, s, gbase, 1.0f, wall, win, atab);
+      sim_step_group<G, POLICY, TRACE>(st, p, E, V, b, s, gbase, 1.0f, wall, win, atab, acache);
     if (s == 0) {
       st.ep_step[b] = 0;
       st.ep_return[b] = 0.0;
@@ -403,7 +479,6 @@ __global__ void __launch_bounds__(64)
     E.next_work = st.next_work[b];
     E.u2 = st.next_u2[b];
     E.u3 = st.next_u3[b];
-    trace_prefetch<1>(st, p, E);
     V.cnt = 0;
     V.head_tc = 0;
     V.head = 0;
@@ -434,7 +509,7 @@ __global__ void __launch_bounds__(64)
       for (int k = 0; k < G; ++k)
         wall[k] = k < S ? action_weight(p, action, action_dtype, (size_t)b * S + (size_t)k) : 1.0f;
     }
-    sim_step_group<G, POLICY, TRACE>(st, p, E, V, b, s, gbase, w_own, wall, win, atab);
+    sim_step_group<G, POLICY, TRACE>(st, p, E, V, b, s, gbase, w_own, wall, win, atab, acache);
   }
 
   // ---- this lane's server back to HBM (window into the ring), then the env words (lane 0)
