@@ -301,10 +301,14 @@ def main():
 
     if rank == 0:
         value = lbdist.throughput(shard, args.steps, elapsed)
-        names = ["dynamics_kernel", "observe_kernel"]
+        # the dynamics launch runs dynamics_group_kernel (one lane per server, the default) or
+        # dynamics_kernel (one lane per env, --dyn-mapping env); lbsim_profile times either
+        dyn = "dynamics_kernel" if args.dyn_mapping == "env" else "dynamics_group_kernel"
+        names = [dyn, "observe_kernel"]
         avg = {names[i]: ms[i] / max(1, cnt[i]) for i in range(2)}
         rate = tr.rate if tr is not None else ARRIVAL_RATE
         abytes = algorithmic_bytes(S, rate * STEP_INTERVAL)
+        abytes[dyn] = abytes.pop("dynamics_kernel")
         per_kernel = {}
         for k in names:
             ab_k = abytes[k] * B

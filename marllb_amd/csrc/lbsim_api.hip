@@ -265,15 +265,13 @@ void launch_dyn_policy(lbsim_t* h, bool g, const void* action, int dtype, int32_
   }
 }
 
-// Mapping choice (LBSIM_DYN_AUTO): one lane per env when that fills every SIMD with at least one
-// wave and an env has at most 8 servers; otherwise one lane per server.  Measured
-// with the round-2 event loop (profiles/r02h_mapping.jsonl): env-per-lane wins at 65536 x 8
-// (Poisson 0.320 vs 0.392 ms, configs[2] trace replay 0.385 vs 0.430 ms) and 65536 x 4;
-// server-per-lane wins up to 32768 x 4 (0.200 vs 0.208 ms) and at S = 16.
+// Mapping choice (LBSIM_DYN_AUTO): one lane per server.  With arrivals drawn G at a
+// time (lbsim_dyn_group.h) it is faster than one lane per env at every measured shape
+// (profiles/r02_round2/mapping_sweep.jsonl): 65536 x 4 0.182 vs 0.214 ms, 131072 x 4 0.316 vs
+// 0.402, 65536 x 8 0.267 vs 0.320, configs[2] trace replay 0.317 vs 0.381, 16384 x 4 0.117 vs
+// 0.198.  The env-per-lane kernel stays selectable (LBSIM_DYN_ENV_PER_LANE).
 bool server_per_lane(const lbsim_t* h) {
-  if (h->cfg.dyn_mapping == LBSIM_DYN_ENV_PER_LANE) return false;
-  if (h->cfg.dyn_mapping == LBSIM_DYN_SERVER_PER_LANE) return true;
-  return h->S > 8 || (int64_t)(h->B + 63) / 64 < (int64_t)h->simds;  // S > 16: always
+  return h->cfg.dyn_mapping != LBSIM_DYN_ENV_PER_LANE;
 }
 
 // S > 16: server-per-lane only (32 or 64 lanes per env; the env-per-lane kernel keeps its
@@ -294,7 +292,8 @@ template <int MODE>
 void launch_dynamics_t(lbsim_t* h, const void* action, int dtype, int32_t* assign,
                        const uint8_t* mask, hipStream_t stream) {
   const bool g = server_per_lane(h);
-  if (h->S <= 4) launch_dyn_policy<4, MODE>(h, g, action, dtype, assign, mask, stream);
+  if (g && h->S <= 2) launch_dyn_group_policy<2, MODE>(h, action, dtype, assign, mask, stream);
+  else if (h->S <= 4) launch_dyn_policy<4, MODE>(h, g, action, dtype, assign, mask, stream);
   else if (h->S <= 8) launch_dyn_policy<8, MODE>(h, g, action, dtype, assign, mask, stream);
   else if (h->S <= 16) launch_dyn_policy<16, MODE>(h, g, action, dtype, assign, mask, stream);
   else if (h->S <= 32) launch_dyn_group_policy<32, MODE>(h, action, dtype, assign, mask, stream);

@@ -46,8 +46,13 @@ def main():
     sq = {**load(a.dir, "sq1"), **load(a.dir, "sq2")}
     S = a.servers
     m = 4 if S <= 4 else 8 if S <= 8 else 16
-    # step-mode launches: dynamics_kernel<MAXS, 0, POLICY, TRACE>, observe_kernel<MAXS, 0>
-    prefixes = {"dynamics_kernel": f"dynamics_kernel<{m}, 0", "observe_kernel": f"observe_kernel<{m}, 0"}
+    g = 2 if S <= 2 else m if S <= 16 else 32 if S <= 32 else 64
+    # step-mode launches: dynamics_group_kernel<G, 0, POLICY, TRACE> (default mapping) or
+    # dynamics_kernel<MAXS, 0, POLICY, TRACE> (env per lane), observe_kernel<MAXS, 0>
+    prefixes = {"dynamics_group_kernel": f"dynamics_group_kernel<{g}, 0",
+                "dynamics_kernel": f"dynamics_kernel<{m}, 0", "observe_kernel": f"observe_kernel<{m}, 0"}
+    prefixes = {n: pfx for n, pfx in prefixes.items()
+                if any(k.startswith(pfx) for k, _ in load(a.dir, "fetch"))}
 
     def match(agg, prefix):
         names = sorted({k for k, _ in agg if k.startswith(prefix)})

@@ -10,7 +10,7 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    for key in ("dynamics_kernel", "observe_kernel", "features_kernel", "reward_kernel"):
+    for key in ("dynamics_kernel", "dynamics_group_kernel", "observe_kernel", "features_kernel", "reward_kernel"):
         if key in name:
             return name.split("(")[0].replace("void ", "").replace("lbk::", "")
     return name[:60]
