@@ -310,15 +310,18 @@ int launch_dynamics(lbsim_t* h, const void* action, int dtype, int32_t* assign,
 
 template <int MODE>
 void launch_observe_t(lbsim_t* h, const ObsOutputs& o, const uint8_t* mask, hipStream_t stream) {
-  const dim3 grid((unsigned)h->B), block(64);
+  // one wave per 4-server chunk, each with its own ObsScratch in dynamic LDS
+  const int nw = (h->S + kObsChunk - 1) / kObsChunk;
+  const dim3 grid((unsigned)h->B), block((unsigned)(64 * nw));
+  const size_t lds = (size_t)nw * sizeof(ObsScratch);
   if (h->S <= 4)
-    hipLaunchKernelGGL((observe_kernel<4, MODE>), grid, block, 0, stream, h->st, h->prm, o, mask);
+    hipLaunchKernelGGL((observe_kernel<4, MODE>), grid, block, lds, stream, h->st, h->prm, o, mask);
   else if (h->S <= 8)
-    hipLaunchKernelGGL((observe_kernel<8, MODE>), grid, block, 0, stream, h->st, h->prm, o, mask);
+    hipLaunchKernelGGL((observe_kernel<8, MODE>), grid, block, lds, stream, h->st, h->prm, o, mask);
   else if (h->S <= 16)
-    hipLaunchKernelGGL((observe_kernel<16, MODE>), grid, block, 0, stream, h->st, h->prm, o, mask);
+    hipLaunchKernelGGL((observe_kernel<16, MODE>), grid, block, lds, stream, h->st, h->prm, o, mask);
   else
-    hipLaunchKernelGGL((observe_kernel<64, MODE>), grid, block, 0, stream, h->st, h->prm, o, mask);
+    hipLaunchKernelGGL((observe_kernel<64, MODE>), grid, block, lds, stream, h->st, h->prm, o, mask);
 }
 
 int launch_observe(lbsim_t* h, const ObsOutputs& o, const uint8_t* mask, int mode,

@@ -519,12 +519,7 @@ __global__ void __launch_bounds__(256) qmix_policy_kernel(QmixArgs p) {
   qmix_mixer<MT>(p, lds, chosen, row0, wave, lane);
 }
 
-// Wave-local LDS ordering: a wave's own writes are visible to its later reads (no workgroup barrier).
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+// (wave_sync, lbsim_kernels.h: wave-local LDS ordering, no workgroup barrier)
 
 // The same step with one WAVE per agent (agents w, w + 4, ...) over a 16-env tile: each wave runs
 // its agent's whole network in its own LDS region [16][lda] with no workgroup barrier between

@@ -1023,6 +1023,25 @@ __device__ __forceinline__ uint32_t xor_lane_u32(uint32_t v, int lane) {
   else if constexpr (M == 8) return dpp_u32<0x128>(v);
   else return shfl_xor_u32(v, M);
 }
+// The same exchanges for code where every lane of the row is active (sort networks, the full-
+// reservoir observe path): mov_dpp with bound_ctrl and full masks has no tied "old" operand, so
+// the DPP move writes a fresh register instead of a copy + in-place move (one VALU op, not two).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dppz_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+template <int M>
+__device__ __forceinline__ uint32_t xor_lane_z(uint32_t v, int lane) {
+  if constexpr (M == 1) return dppz_u32<0xB1>(v);
+  else if constexpr (M == 2) return dppz_u32<0x4E>(v);
+  else if constexpr (M == 4) {  // lanes whose row_shl/row_shr source is out of the row select the other
+    const uint32_t up = dppz_u32<0x104>(v), dn = dppz_u32<0x114>(v);
+    return (lane & 4) ? dn : up;
+  } else if constexpr (M == 3) return dppz_u32<0x1B>(v);
+  else if constexpr (M == 7) return dppz_u32<0x141>(v);
+  else if constexpr (M == 8) return dppz_u32<0x128>(v);
+  else return shfl_xor_u32(v, M);
+}
 template <int M>
 __device__ __forceinline__ float xor_lane_f32(float v, int lane) {
   return __uint_as_float(xor_lane_u32<M>(__float_as_uint(v), lane));
@@ -1038,6 +1057,15 @@ __device__ __forceinline__ float xor_lane(float v, int lane, int m) {
 }
 __device__ __forceinline__ double xor_lane(double v, int lane, int m) {
   return m == 1 ? xor_lane_f64<1>(v, lane) : m == 2 ? xor_lane_f64<2>(v, lane) : xor_lane_f64<4>(v, lane);
+}
+
+// Orders one wave's LDS accesses (the observe scratch is private to a wave): a compiler fence and
+// a wave barrier.  A wave's LDS instructions execute in issue order, so no s_barrier (which would
+// meet the other waves of a multi-wave workgroup) and no counter wait are needed.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v, int lane) {
@@ -1119,8 +1147,8 @@ __device__ __forceinline__ T pairwise8x2(int n, int j, T& second, F term) {
 // groups hit distinct banks.
 constexpr int KP = K + 8;
 
-// Scratch of one chunk of up to 4 servers (observe_env walks an env's servers in chunks, so the LDS
-// footprint -- and the occupancy -- is the same at S = 4, 8 and 16).
+// Scratch of one chunk of up to 4 servers (observe_kernel gives every chunk of an env its own wave
+// and scratch, so the per-wave LDS footprint -- and the occupancy -- is the same at every S).
 constexpr int kObsChunk = 4;
 
 struct ObsScratch {
@@ -1144,7 +1172,7 @@ __device__ __forceinline__ void cross_step_keys(uint32_t (&key)[16], int t, int 
   const uint32_t bound = (t & lowbit) ? 0xFFFFFFFFu : 0u;
   uint32_t pk[16];
 #pragma unroll
-  for (int e = 0; e < 16; ++e) pk[e] = xor_lane_u32<M>(key[FLIP ? (e ^ 15) : e], t);
+  for (int e = 0; e < 16; ++e) pk[e] = xor_lane_z<M>(key[FLIP ? (e ^ 15) : e], t);
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const uint32_t a = key[e], b = pk[e];
@@ -1207,6 +1235,185 @@ __device__ __forceinline__ float sample_value(uint32_t raw) {
 // us << 7 | slot must stay below the 0xFFFFFFFF filler of empty slots.
 constexpr uint32_t kPackLimit = (1u << 25) - 1u;
 
+// p90 of a full reservoir (numpy 'linear', float32 virtual index (K - 1) * 0.9f): sorted
+// positions 114 and 115, both in lane 7 of the sorting group (sorted position 16 t + e).
+constexpr int kP90Lo = (K - 1) * 9 / 10;
+static_assert(kP90Lo == 114 && (kP90Lo & 15) != 15, "p90 pair inside one lane");
+
+// observe_chunk for the steady state of the simulator: every reservoir of the chunk (<= 4 servers)
+// full (n = K) and every sample below kPackLimit.  Lane (g, j), g = 2 u + r, owns reservoir r
+// (0 fct, 1 duration) of server s_base + u and holds its slots 8 e + j, e = 0..15 -- at n = K
+// exactly numpy's pairwise accumulator j (reservoir.py:143-155) -- in registers through every
+// phase: no LDS image, no per-element loops.  The two groups of a server (lanes 16 u .. 16 u + 15,
+// one DPP row) compute half of the decay weights each and swap halves by row_ror:8.  LDS holds only
+// the 2^-48 fixed-point weights by slot, gathered after the sort.  Same operations in the same
+// order as the general path, so the same bits.  Returns false (nothing written) when the chunk
+// does not qualify.
+template <bool INC>
+__device__ __forceinline__ bool observe_chunk_full(const DevState& st, const SimParams& p, size_t b,
+                                                   int s_base, int S, ObsScratch& sc,
+                                                   float* obs_out, int lane) {
+  const size_t srow = b * (size_t)p.S + (size_t)s_base;
+  const int g = lane >> 3, j = lane & 7, u = g >> 1, r = g & 1;
+  const bool act = u < S;
+  const size_t sb = srow + (size_t)(act ? u : 0);
+  if (__any(act && st.res_count[sb] < (uint32_t)K)) return false;
+  // values of reservoir r (the 12-B record is {fct, duration, ts}); timestamps of the half of the
+  // slots whose weights this group computes, 8 (q + 8 r) + j -- the pair's other group reads the
+  // other half, and the newest timestamp is a max over the 16 lanes of the pair
+  const uint32_t* rec = reinterpret_cast<const uint32_t*>(st.res + sb * K + (size_t)j);
+  uint32_t key[16], th[8];
+  {
+    // qualification pass; its loads are dropped and re-issued below (L1/L2 hits) so that no
+    // value stays live across the branch into the general path (which would spill at 96 VGPRs)
+    uint32_t vmax = 0;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const uint32_t v = rec[24 * e + r];
+      vmax = v > vmax ? v : vmax;
+    }
+    if (__any(act && vmax >= kPackLimit)) return false;
+    __asm__ volatile("" ::: "memory");
+  }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) key[e] = rec[24 * e + r];
+  const uint32_t* rts = rec + 2 + 192 * r;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) th[q] = rts[24 * q];
+  uint32_t tmax = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) tmax = th[q] > tmax ? th[q] : tmax;
+  uint32_t o = xor_lane_z<1>(tmax, lane);
+  tmax = o > tmax ? o : tmax;
+  o = xor_lane_z<2>(tmax, lane);
+  tmax = o > tmax ? o : tmax;
+  o = xor_lane_z<4>(tmax, lane);
+  tmax = o > tmax ? o : tmax;
+  o = xor_lane_z<8>(tmax, lane);
+  tmax = o > tmax ? o : tmax;
+
+  // decay weights: group r computes slots 8 (q + 8 r) + j, q < 8, swaps halves with its partner
+  float wh[8], w[16];
+  uint64_t* wfix = reinterpret_cast<uint64_t*>(&sc.vals[0][0]) + u * K;  // [4][K] u64
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    wh[q] = lb_exp2f((float)(tmax - th[q]) * p.decay_c);
+    if (act) wfix[8 * (q + 8 * r) + j] = (uint64_t)(wh[q] * 281474976710656.0f);
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float pw = __uint_as_float(xor_lane_z<8>(__float_as_uint(wh[q]), lane));
+    w[q] = r ? pw : wh[q];
+    w[q + 8] = r ? wh[q] : pw;
+  }
+
+  // numpy-order sums (pairwise8 / pairwise8x2 at n = K): accumulator j over e, xor-combine
+  float vf[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) vf[e] = sample_value<true>(key[e]);
+  float acc = vf[0];
+#pragma unroll
+  for (int e = 1; e < 16; ++e) acc += vf[e];
+  acc = acc + xor_lane_f32<1>(acc, lane);
+  acc = acc + xor_lane_f32<2>(acc, lane);
+  acc = acc + xor_lane_f32<4>(acc, lane);
+  const float mean = acc / (float)K;
+  double svw = (double)vf[0] * (double)w[0], sw = (double)w[0];
+#pragma unroll
+  for (int e = 1; e < 16; ++e) {
+    const double wi = (double)w[e];
+    svw += (double)vf[e] * wi;
+    sw += wi;
+  }
+  svw = svw + xor_lane_f64<1>(svw, lane);
+  sw = sw + xor_lane_f64<1>(sw, lane);
+  svw = svw + xor_lane_f64<2>(svw, lane);
+  sw = sw + xor_lane_f64<2>(sw, lane);
+  svw = svw + xor_lane_f64<4>(svw, lane);
+  sw = sw + xor_lane_f64<4>(sw, lane);
+  float ss;
+  {
+    float dv = vf[0] - mean;
+    ss = dv * dv;
+#pragma unroll
+    for (int e = 1; e < 16; ++e) {
+      dv = vf[e] - mean;
+      ss += dv * dv;
+    }
+  }
+  ss = ss + xor_lane_f32<1>(ss, lane);
+  ss = ss + xor_lane_f32<2>(ss, lane);
+  ss = ss + xor_lane_f32<4>(ss, lane);
+  const float sd = sqrtf(ss / (float)K);
+  const float md = (float)(svw / sw);
+
+  // order statistics: one key-only sort of (us << 7 | slot)
+#pragma unroll
+  for (int e = 0; e < 16; ++e) key[e] = (key[e] << 7) | (uint32_t)(8 * e + j);
+  bitonic128_keys_g8(key, j);
+  wave_sync();  // wfix complete
+  uint64_t incl[16];
+  uint64_t run = 0;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    run += wfix[key[e] & 127u];
+    incl[e] = run;
+    key[e] >>= 7;
+  }
+  uint64_t excl = 0;
+#pragma unroll
+  for (int dd = 1; dd < 8; dd <<= 1) {
+    const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)(run + excl), (unsigned)dd, 8);
+    const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)((run + excl) >> 32), (unsigned)dd, 8);
+    if (j >= dd) excl += ((uint64_t)hi << 32) | lo;
+  }
+  const uint64_t tot_incl = run + excl;
+  const uint32_t tlo = (uint32_t)__shfl((int)(uint32_t)tot_incl, (lane & ~7) | 7, 64);
+  const uint32_t thi = (uint32_t)__shfl((int)(uint32_t)(tot_incl >> 32), (lane & ~7) | 7, 64);
+  const uint64_t thr = ((((uint64_t)thi << 32) | tlo) * 9u + 9u) / 10u;
+  const uint64_t thr_lane = thr > excl ? thr - excl : 0u;
+  // the first e with incl[e] >= thr_lane holds this lane's smallest such key (keys ascend with
+  // e): a min instead of a register-indexed read; past the last position: position 127
+  uint32_t cand = 0xFFFFFFFFu;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const uint32_t c = incl[e] >= thr_lane ? key[e] : 0xFFFFFFFFu;
+    cand = c < cand ? c : cand;
+  }
+  const bool crosses = incl[15] >= thr_lane;
+  const uint64_t m = __ballot(crosses);
+  const uint32_t gm = (uint32_t)(m >> (lane & ~7)) & 0xFFu;
+  const int tstar = gm ? __builtin_ctz(gm) : 7;
+  cand = crosses ? cand : key[15];
+  const float p90d = sample_value<true>(shfl_u32(cand, (lane & ~7) | tstar));
+  // p90: positions kP90Lo, kP90Lo + 1 of lane 7 (reservoir.py:144, numpy 2 'linear' in float32)
+  float p90;
+  {
+    const float hidx = (float)(K - 1) * 0.9f;
+    const float fl = floorf(hidx);
+    const float gg = hidx - fl;
+    const float va = sample_value<true>(key[kP90Lo & 15]);
+    const float vb = sample_value<true>(key[(kP90Lo & 15) + 1]);
+    const float diff = vb - va;
+    p90 = (gg >= 0.5f) ? (vb - diff * (1.0f - gg)) : (va + diff * gg);
+    p90 = __uint_as_float(shfl_u32(__float_as_uint(p90), (lane & ~7) | 7));
+  }
+  // row of server u: lane j < 5 of group r writes feature j of reservoir r; lane 5 of the fct
+  // group writes n_flow_on
+  if (act) {
+    const size_t so = srow + (size_t)u;
+    if (j < 5) {
+      const float v = j == 0 ? mean : j == 1 ? p90 : j == 2 ? sd : j == 3 ? md : p90d;
+      obs_out[(s_base + u) * NF + 1 + 5 * r + j] = v;
+      st.fcache[so * 10 + (size_t)(5 * r + j)] = v;
+    } else if (j == 5 && r == 0) {
+      obs_out[(s_base + u) * NF] = (float)(st.hc[so] >> 16);
+    }
+  }
+  wave_sync();
+  return true;
+}
+
 // The 11-column observation rows (features.py:256-286) of servers [s_base, s_base + S), S <= 4,
 // of env b into obs_out.  Slot-order sums follow numpy exactly (reservoir.py:143-155); order
 // statistics come from the sorted keys (reservoir.py:144, 165-196).
@@ -1228,9 +1435,12 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
         obs_out[s_base * NF + e] = c == 0 ? (float)(st.hc[srow + (size_t)s] >> 16)
                                           : st.fcache[(srow + (size_t)s) * 10 + (size_t)(c - 1)];
       }
-      __syncthreads();
+      wave_sync();
       return;
     }
+  }
+  if constexpr (US) {
+    if (observe_chunk_full<INC>(st, p, b, s_base, S, sc, obs_out, lane)) return;
   }
   // ---- phase 1: reservoirs into LDS, decay weights relative to each server's newest sample.
   //      Loads of 4 servers are issued before any is consumed (memory-level parallelism).
@@ -1278,7 +1488,7 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
       }
     }
   }
-  __syncthreads();
+  wave_sync();
 
   // ---- phase 2: numpy-order sums, one job per 8-lane group
   for (int job0 = 0; job0 < R; job0 += 8) {  // float32 means
@@ -1303,7 +1513,7 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
       if ((r & 1) == 0) sc.swt[r >> 1] = sw;  // the two reservoirs of a server share w
     }
   }
-  __syncthreads();
+  wave_sync();
   for (int job0 = 0; job0 < R; job0 += 8) {  // float32 sum (v - mean)^2
     const int r = job0 + g;
     const int n = r < R ? sc.n[r] : 0;
@@ -1318,7 +1528,7 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
       sc.md[r] = n > 0 ? (float)(sc.svw[r] / sc.swt[r >> 1]) : 0.0f;
     }
   }
-  __syncthreads();
+  wave_sync();
 
   // ---- phase 3: order statistics, 8 reservoirs per pass (one per 8-lane group)
   for (int r0 = 0; r0 < R; r0 += 8) {
@@ -1411,7 +1621,7 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
 #pragma unroll
     for (int e = 0; e < 16; ++e)
       if (act) sc.vals[rr][e * 8 + j] = key[e];  // sorted position 16 j + e, transposed
-    __syncthreads();
+    wave_sync();
     if (j == 0 && act) {
       float p90 = 0.0f, p90d = 0.0f;
       if (n > 0) {
@@ -1430,7 +1640,7 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
       sc.p90[r] = p90;
       sc.p90d[r] = p90d;
     }
-    __syncthreads();
+    wave_sync();
   }
 
   // ---- observation rows: [n_flow_on, fct x5, duration x5]
@@ -1447,21 +1657,9 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
     }
     obs_out[s_base * NF + e] = v;
   }
-  __syncthreads();
+  wave_sync();
 }
 
-// The (S, 11) observation of env b into obs_out, 4 servers at a time.
-template <int MAXS, bool US, bool INC>
-__device__ __forceinline__ void observe_env(const DevState& st, const SimParams& p, size_t b,
-                                            ObsScratch& sc, float* obs_out, int lane) {
-  if constexpr (MAXS <= kObsChunk) {
-    observe_chunk<US, INC>(st, p, b, 0, p.S, sc, obs_out, lane);
-  } else {
-    for (int s0 = 0; s0 < p.S; s0 += kObsChunk)
-      observe_chunk<US, INC>(st, p, b, s0, p.S - s0 < kObsChunk ? p.S - s0 : kObsChunk, sc,
-                             obs_out, lane);
-  }
-}
 
 // ================================================================ reward (rewards.py)
 
@@ -1576,54 +1774,65 @@ struct ObsOutputs {
   double* ep_ret;
 };
 
-// Waves per SIMD the LDS footprint allows (ObsScratch of one 4-server chunk, ~8 KB at every S);
-// caps the kernel at 96 VGPRs.
+// One wave per 4-server chunk (kObsChunk), all chunks of an env in one workgroup: S = 4 -> one
+// wave, 8 -> 2, 16 -> 4, 64 -> 16.  Each wave computes its chunk in its own ObsScratch (dynamic
+// LDS, nw * sizeof(ObsScratch) bytes at launch) with wave-level ordering only; the workgroup meets
+// once, then wave 0 computes the reward and every wave writes outputs.  5 waves per SIMD at every
+// S (96 VGPRs): the work per wave is the same chunk whatever S is.
 template <int MAXS>
-constexpr int kObsWaves = MAXS <= kObsChunk ? 5 : 4;
+constexpr int kObsWavesPerEnv = MAXS <= kObsChunk ? 1 : MAXS / kObsChunk;
 
 template <int MAXS, int MODE>
-__global__ void __launch_bounds__(64, kObsWaves<MAXS>)
+__global__ void __launch_bounds__(64 * kObsWavesPerEnv<MAXS>, 5)
     observe_kernel(DevState st, SimParams p, ObsOutputs out, const uint8_t* reset_mask) {
   constexpr int mode = MODE;
   const size_t b = blockIdx.x;
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nthr = blockDim.x;
   if (mode == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
-  __shared__ ObsScratch sc;
+  extern __shared__ double obs_dyn[];
+  ObsScratch& sc = reinterpret_cast<ObsScratch*>(obs_dyn)[wv];
   __shared__ float s_obs[MAXS * NF];
   __shared__ float s_act[MAXS];
   const int S = p.S;
-  observe_env<MAXS, true, mode == kModeStep>(st, p, b, sc, s_obs, lane);
-
-  // active servers (any column > 0): lane s scans its row, one ballot; their reward-field values
-  // compacted into s_act in server order
-  bool act = false;
-  if (lane < S)
-    for (int f = 0; f < NF; ++f) act |= s_obs[lane * NF + f] > 0.0f;
-  const uint64_t act_mask = __ballot(act);
-  const bool fok = p.reward_field >= 0 && p.reward_field < NF;
-  if (act && fok) s_act[__popcll(act_mask & ((1ull << lane) - 1ull))] = s_obs[lane * NF + p.reward_field];
+  {
+    const int s0 = wv * kObsChunk;  // the launch has ceil(S / 4) waves
+    observe_chunk<true, mode == kModeStep>(st, p, b, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk,
+                                           sc, s_obs, lane);
+  }
   __syncthreads();
-  if (mode == kModeStep && lane == 0) {
-    const double r = fok ? reward_values(__popcll(act_mask), [&](int i) { return (double)s_act[i]; },
-                                         p.reward_metric)
-                         : 0.0;
-    out.reward[b] = (float)r;
-    const int32_t es = st.ep_step[b] + 1;
-    const double er = st.ep_return[b] + r;
-    st.ep_step[b] = es;
-    st.ep_return[b] = er;
-    out.done[b] = (uint8_t)(es >= p.max_steps ? 1 : 0);
-    if (out.ep_len != nullptr) out.ep_len[b] = es;
-    if (out.ep_ret != nullptr) out.ep_ret[b] = er;
+
+  // active servers (any column > 0): lane s of wave 0 scans its row, one ballot; their
+  // reward-field values compacted into s_act in server order
+  if (wv == 0) {
+    bool act = false;
+    if (lane < S)
+      for (int f = 0; f < NF; ++f) act |= s_obs[lane * NF + f] > 0.0f;
+    const uint64_t act_mask = __ballot(act);
+    const bool fok = p.reward_field >= 0 && p.reward_field < NF;
+    if (act && fok) s_act[__popcll(act_mask & ((1ull << lane) - 1ull))] = s_obs[lane * NF + p.reward_field];
+    wave_sync();
+    if (mode == kModeStep && lane == 0) {
+      const double r = fok ? reward_values(__popcll(act_mask), [&](int i) { return (double)s_act[i]; },
+                                           p.reward_metric)
+                           : 0.0;
+      out.reward[b] = (float)r;
+      const int32_t es = st.ep_step[b] + 1;
+      const double er = st.ep_return[b] + r;
+      st.ep_step[b] = es;
+      st.ep_return[b] = er;
+      out.done[b] = (uint8_t)(es >= p.max_steps ? 1 : 0);
+      if (out.ep_len != nullptr) out.ep_len[b] = es;
+      if (out.ep_ret != nullptr) out.ep_ret[b] = er;
+    }
   }
 
   const int nobs = S * NF;
   float* orow = out.obs + b * (size_t)nobs;
   if (out.raw_obs != nullptr)
-    for (int e = lane; e < nobs; e += 64) out.raw_obs[b * (size_t)nobs + e] = s_obs[e];
+    for (int e = tid; e < nobs; e += nthr) out.raw_obs[b * (size_t)nobs + e] = s_obs[e];
   if (p.normalize) {  // env.py:460-468, float64 running statistics
     const int32_t cnt = st.norm_count[b] + 1;
-    for (int e = lane; e < nobs; e += 64) {
+    for (int e = tid; e < nobs; e += nthr) {
       const size_t gi = b * (size_t)nobs + (size_t)e;
       const double o = (double)s_obs[e];
       double m = st.norm_mean[gi];
@@ -1638,16 +1847,16 @@ __global__ void __launch_bounds__(64, kObsWaves<MAXS>)
       st.norm_std[gi] = ns;
       orow[e] = (float)((o - m) / (ns + 1e-8));
     }
-    if (lane == 0) st.norm_count[b] = cnt;
+    if (tid == 0) st.norm_count[b] = cnt;
   } else {
-    for (int e = lane; e < nobs; e += 64) orow[e] = s_obs[e];
+    for (int e = tid; e < nobs; e += nthr) orow[e] = s_obs[e];
   }
 }
 
 // ================================================================ stateless entry points
 
 // Reservoir features of caller-given reservoirs: 4 reservoirs per block, each presented to
-// observe_env as one "server" whose fct and duration arrays are both the given values.
+// observe_chunk as one "server" whose fct and duration arrays are both the given values.
 __global__ void __launch_bounds__(64)
     features_kernel(const float* values, const uint32_t* ts, const uint32_t* counts, int64_t n,
                     float decay_c, float* out) {
@@ -1667,7 +1876,7 @@ __global__ void __launch_bounds__(64)
   p.S = S;
   p.decay_c = decay_c;
   __syncthreads();
-  observe_env<4, false, false>(st, p, 0, sc, fobs, lane);
+  observe_chunk<false, false>(st, p, 0, 0, S, sc, fobs, lane);
   for (int e = lane; e < S * 5; e += 64) {
     const int s = e / 5, f = e - s * 5;
     out[(r0 + s) * 5 + f] = fobs[s * NF + 1 + f];

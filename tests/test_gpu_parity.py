@@ -147,6 +147,11 @@ CONFIGS = [
     # 16 servers = 64, and a 20-server env on a 32-lane group with two-choice SED
     dict(B=24, S=64, kw={"arrival_rate": 1600.0}),
     dict(B=40, S=20, kw={"assign_policy": "sed2", "arrival_rate": 800.0, "normalize_obs": True}),
+    # overloaded servers with long queues: reservoirs fill (>= 128 samples) while flows start to
+    # wait > 33 s -- full 4-server chunks holding a sample >= 2^25 - 1 us (observe's general path
+    # with the two-pass sort, after steps on its register-resident path)
+    dict(B=32, S=4, kw={"arrival_rate": 12.0, "server_rates": [1.2, 1.4, 1.6, 1.8],
+                        "step_interval": 10.0, "queue_capacity": 64}),
 ]
 
 
