@@ -288,11 +288,27 @@ void launch_dyn_group_policy(lbsim_t* h, const void* action, int dtype, int32_t*
   }
 }
 
+// Lanes per env of the server-per-lane mapping: LBSIM_DYN_GROUP_LANES = 8 | 16 | 32 | 64 widens
+// the group past pow2 >= S (experiments; the extra lanes draw arrivals ahead, hold no server).
+int forced_group_lanes() {
+  static const int g = [] {
+    const char* s = std::getenv("LBSIM_DYN_GROUP_LANES");
+    return s ? std::atoi(s) : 0;
+  }();
+  return g;
+}
+
 template <int MODE>
 void launch_dynamics_t(lbsim_t* h, const void* action, int dtype, int32_t* assign,
                        const uint8_t* mask, hipStream_t stream) {
   const bool g = server_per_lane(h);
-  if (g && h->S <= 2) launch_dyn_group_policy<2, MODE>(h, action, dtype, assign, mask, stream);
+  const int fg = g ? forced_group_lanes() : 0;
+  if (fg >= h->S && (fg == 8 || fg == 16 || fg == 32 || fg == 64)) {
+    if (fg == 8) launch_dyn_group_policy<8, MODE>(h, action, dtype, assign, mask, stream);
+    else if (fg == 16) launch_dyn_group_policy<16, MODE>(h, action, dtype, assign, mask, stream);
+    else if (fg == 32) launch_dyn_group_policy<32, MODE>(h, action, dtype, assign, mask, stream);
+    else launch_dyn_group_policy<64, MODE>(h, action, dtype, assign, mask, stream);
+  } else if (g && h->S <= 2) launch_dyn_group_policy<2, MODE>(h, action, dtype, assign, mask, stream);
   else if (h->S <= 4) launch_dyn_policy<4, MODE>(h, g, action, dtype, assign, mask, stream);
   else if (h->S <= 8) launch_dyn_policy<8, MODE>(h, g, action, dtype, assign, mask, stream);
   else if (h->S <= 16) launch_dyn_policy<16, MODE>(h, g, action, dtype, assign, mask, stream);
@@ -314,6 +330,12 @@ void launch_observe_t(lbsim_t* h, const ObsOutputs& o, const uint8_t* mask, hipS
   const int nw = (h->S + kObsChunk - 1) / kObsChunk;
   const dim3 grid((unsigned)h->B), block((unsigned)(64 * nw));
   const size_t lds = (size_t)nw * sizeof(ObsScratch);
+  if (lds > 65536) {  // S > 32: 9-16 chunk waves
+    static const bool ok = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&observe_kernel<64, MODE>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, 16 * (int)sizeof(ObsScratch)) == hipSuccess;
+    (void)ok;
+  }
   if (h->S <= 4)
     hipLaunchKernelGGL((observe_kernel<4, MODE>), grid, block, lds, stream, h->st, h->prm, o, mask);
   else if (h->S <= 8)

@@ -248,6 +248,16 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
       const float s2 = __uint_as_float(group_or<G>(s == h2 ? bits : 0u));
       const bool ok1 = (em >> h1) & 1u, ok2 = (em >> h2) & 1u;
       chosen = (ok1 && ok2) ? ((s2 < s1) ? h2 : h1) : (ok1 ? h1 : (ok2 ? h2 : -1));
+    } else if constexpr (FAST) {
+      // finite scores: the scan's result is the eligible minimum, h among equal minima, else the
+      // lowest such server -- a lexicographic (score, rank) minimum with rank 0 for h and s + 1
+      // otherwise, as two DPP min reductions (no ballots, no 64-bit group masks)
+      const int32_t key = elig ? f32_key(V.score) : 0x7FFFFFFF;  // finite keys < 0x7f800001
+      const int32_t mk = group_min_i32<G>(key);
+      const int h = (int)__umulhi(E.u2, (uint32_t)S);
+      const int32_t rk = (elig && key == mk) ? (s == h ? 0 : s + 1) : 0xFF;
+      const int32_t mr = group_min_i32<G>(rk);
+      chosen = mr == 0xFF ? -1 : (mr == 0 ? h : mr - 1);
     } else {
       const bool num = elig && V.score == V.score;
       const float m = key_f32(group_min_i32<G>(num ? f32_key(V.score) : 0x7f800000));

@@ -1043,6 +1043,16 @@ __device__ __forceinline__ uint32_t xor_lane_z(uint32_t v, int lane) {
   else return shfl_xor_u32(v, M);
 }
 template <int M>
+__device__ __forceinline__ float xor_f32_z(float v, int lane) {
+  return __uint_as_float(xor_lane_z<M>(__float_as_uint(v), lane));
+}
+template <int M>
+__device__ __forceinline__ double xor_f64_z(double v, int lane) {
+  const uint32_t lo = xor_lane_z<M>((uint32_t)__double2loint(v), lane);
+  const uint32_t hi = xor_lane_z<M>((uint32_t)__double2hiint(v), lane);
+  return __hiloint2double((int)hi, (int)lo);
+}
+template <int M>
 __device__ __forceinline__ float xor_lane_f32(float v, int lane) {
   return __uint_as_float(xor_lane_u32<M>(__float_as_uint(v), lane));
 }
@@ -1208,11 +1218,31 @@ __device__ __forceinline__ void inreg_steps_keys(uint32_t (&key)[16], int kflip,
   }
 }
 
+// Ascending sort of a lane's 16 keys by Green's 60-comparator, 10-layer network (Knuth TAOCP
+// 5.3.4; checked for all 2^16 0-1 inputs) instead of the 80 comparators of the bitonic stages
+// k = 2..16: any network that sorts the lane's keys ascending leaves the same keys.
+__device__ __forceinline__ void sort16_keys(uint32_t (&key)[16]) {
+  constexpr int8_t net[60][2] = {
+      {0, 13}, {1, 12}, {2, 15}, {3, 14}, {4, 8},  {5, 6},   {7, 11},  {9, 10},
+      {0, 5},  {1, 7},  {2, 9},  {3, 4},  {6, 13}, {8, 14},  {10, 15}, {11, 12},
+      {0, 1},  {2, 3},  {4, 5},  {6, 8},  {7, 9},  {10, 11}, {12, 13}, {14, 15},
+      {0, 2},  {1, 3},  {4, 10}, {5, 11}, {6, 7},  {8, 9},   {12, 14}, {13, 15},
+      {1, 2},  {3, 12}, {4, 6},  {5, 7},  {8, 10}, {9, 11},  {13, 14},
+      {1, 4},  {2, 6},  {5, 8},  {7, 10}, {9, 13}, {11, 14},
+      {2, 4},  {3, 6},  {9, 12}, {11, 13},
+      {3, 5},  {6, 8},  {7, 9},  {10, 12},
+      {3, 4},  {5, 6},  {7, 8},  {9, 10}, {11, 12},
+      {6, 7},  {8, 9}};
+#pragma unroll
+  for (int c = 0; c < 60; ++c) {
+    const uint32_t a = key[net[c][0]], b = key[net[c][1]];
+    key[net[c][0]] = a < b ? a : b;
+    key[net[c][1]] = a < b ? b : a;
+  }
+}
+
 __device__ __forceinline__ void bitonic128_keys_g8(uint32_t (&key)[16], int t) {
-  inreg_steps_keys(key, 2, 0);
-  inreg_steps_keys(key, 4, 1);
-  inreg_steps_keys(key, 8, 2);
-  inreg_steps_keys(key, 16, 4);
+  sort16_keys(key);                      // k = 2 .. 16 (each lane's 16 keys ascending)
   cross_step_keys<1, true>(key, t, 1);   // k = 32
   inreg_steps_keys(key, 0, 8);
   cross_step_keys<3, true>(key, t, 2);   // k = 64
@@ -1314,9 +1344,9 @@ __device__ __forceinline__ bool observe_chunk_full(const DevState& st, const Sim
   float acc = vf[0];
 #pragma unroll
   for (int e = 1; e < 16; ++e) acc += vf[e];
-  acc = acc + xor_lane_f32<1>(acc, lane);
-  acc = acc + xor_lane_f32<2>(acc, lane);
-  acc = acc + xor_lane_f32<4>(acc, lane);
+  acc = acc + xor_f32_z<1>(acc, lane);
+  acc = acc + xor_f32_z<2>(acc, lane);
+  acc = acc + xor_f32_z<4>(acc, lane);
   const float mean = acc / (float)K;
   double svw = (double)vf[0] * (double)w[0], sw = (double)w[0];
 #pragma unroll
@@ -1325,12 +1355,12 @@ __device__ __forceinline__ bool observe_chunk_full(const DevState& st, const Sim
     svw += (double)vf[e] * wi;
     sw += wi;
   }
-  svw = svw + xor_lane_f64<1>(svw, lane);
-  sw = sw + xor_lane_f64<1>(sw, lane);
-  svw = svw + xor_lane_f64<2>(svw, lane);
-  sw = sw + xor_lane_f64<2>(sw, lane);
-  svw = svw + xor_lane_f64<4>(svw, lane);
-  sw = sw + xor_lane_f64<4>(sw, lane);
+  svw = svw + xor_f64_z<1>(svw, lane);
+  sw = sw + xor_f64_z<1>(sw, lane);
+  svw = svw + xor_f64_z<2>(svw, lane);
+  sw = sw + xor_f64_z<2>(sw, lane);
+  svw = svw + xor_f64_z<4>(svw, lane);
+  sw = sw + xor_f64_z<4>(sw, lane);
   float ss;
   {
     float dv = vf[0] - mean;
@@ -1341,9 +1371,9 @@ __device__ __forceinline__ bool observe_chunk_full(const DevState& st, const Sim
       ss += dv * dv;
     }
   }
-  ss = ss + xor_lane_f32<1>(ss, lane);
-  ss = ss + xor_lane_f32<2>(ss, lane);
-  ss = ss + xor_lane_f32<4>(ss, lane);
+  ss = ss + xor_f32_z<1>(ss, lane);
+  ss = ss + xor_f32_z<2>(ss, lane);
+  ss = ss + xor_f32_z<4>(ss, lane);
   const float sd = sqrtf(ss / (float)K);
   const float md = (float)(svw / sw);
 

@@ -77,7 +77,9 @@ __device__ __forceinline__ float lb_logf(float x) {
 // 2^x for x <= 0 (x < -60 -> 0): x = n + f, n = floor(x + 1/2), f in [-1/2, 1/2), degree-7
 // Taylor of e^(f ln2) (truncation error < 6e-9) in fmaf Horner form, times 2^n.
 __device__ __forceinline__ float lb_exp2f(float x) {
-  if (x < -60.0f) return 0.0f;
+  // branch-free: x < -60 selects 0 at the end (the polynomial of a clamped x is discarded)
+  const bool under = x < -60.0f;
+  x = under ? 0.0f : x;
   const float fl = floorf(x + 0.5f);  /* exact for |x| <= 60 */
   const int n = (int)fl;
   const float f = x - fl;             /* exact, in [-0.5, 0.5) */
@@ -89,7 +91,8 @@ __device__ __forceinline__ float lb_exp2f(float x) {
   p = fmaf(p, f, 0.240226507f);
   p = fmaf(p, f, 0.693147182f);
   p = fmaf(p, f, 1.0f);
-  return p * as_f32((uint32_t)(n + 127) << 23);
+  const float r = p * as_f32((uint32_t)(n + 127) << 23);
+  return under ? 0.0f : r;
 }
 
 // floor(r64 * n / 2^64) for n <= 2^32: uniform integer in [0, n) (Lemire multiply-shift, 64-bit
