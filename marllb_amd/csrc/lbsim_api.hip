@@ -374,13 +374,14 @@ int fused_mt(int64_t) {
 }
 
 template <typename Args>
-int launch_fused(void (*kern)(Args), int64_t B, int mt, size_t lds, hipStream_t s, Args a) {
+int launch_fused(void (*kern)(Args), int64_t B, int mt, size_t lds, hipStream_t s, Args a,
+                 unsigned threads = 256) {
   const void* f = reinterpret_cast<const void*>(kern);
   if (lds > 65536 &&
       hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return LBSIM_EDEVICE;
   void* args[] = {&a};
-  const dim3 grid((unsigned)((B + 16 * mt - 1) / (16 * mt))), block(256);
+  const dim3 grid((unsigned)((B + 16 * mt - 1) / (16 * mt))), block(threads);
   return hipLaunchKernel(f, grid, block, args, lds, s) == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
 }
 
@@ -779,12 +780,20 @@ int lbsim_qmix_policy_step(const lbsim_qmix_policy_t* n, const float* obs, float
   int mt = fused_mt(B);
   while (mt > 1 && lds_of(mt) > kFusedLdsMax) mt >>= 1;
   const hipStream_t s = (hipStream_t)stream;
-  static const bool tile_form = [] {
+  // LBSIM_QMIX_KERNEL = tile | wave | pair (default: pair when A = 4, else wave)
+  static const int form = [] {
     const char* e = std::getenv("LBSIM_QMIX_KERNEL");
-    return e != nullptr && std::strcmp(e, "tile") == 0;
+    if (e != nullptr && std::strcmp(e, "tile") == 0) return 0;
+    if (e != nullptr && std::strcmp(e, "wave") == 0) return 1;
+    return 2;
   }();
-  if (mt == 1 && !tile_form) {  // one wave per agent, 16 envs per workgroup (default)
+  if (mt == 1 && form != 0) {  // one or two waves per agent, 16 envs per workgroup
     a.lda = fused_ld(std::max(a.kxp + 64, 128));
+    if (form == 2 && A == 4) {  // two waves per agent: 8-wave workgroups
+      const size_t lds = ((size_t)4 * 16 * a.lda + 2 * (size_t)A * 16 * 16 + 16 * (size_t)A) * 4;
+      if (a.ld > 4 * a.lda || lds > kFusedLdsMax) return LBSIM_ENOTSUP;
+      return launch_fused(&qmix_agent_pair_kernel<64, 128>, B, 1, lds, s, a, 512);
+    }
     const size_t lds = ((size_t)4 * 16 * a.lda + (size_t)A * 16 * 16 + 16 * (size_t)A) * 4;
     if (a.ld > 4 * a.lda || lds > kFusedLdsMax) return LBSIM_ENOTSUP;
     return launch_fused(&qmix_agent_wave_kernel<64, 128>, B, 1, lds, s, a);

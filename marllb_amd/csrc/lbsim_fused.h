@@ -375,12 +375,14 @@ __device__ __forceinline__ void qmix_mixer(const QmixArgs& p, float* lds, const 
   stage_rows(lds, ld, 0, p.state, p.Ds, p.Ds, p.ksp, R, row0, p.B, nullptr);
   __syncthreads();
   const int he = p.he, E = p.E;
+  const bool mw = wave < 4;  // the mixer's GEMMs run on waves 0-3 (8-wave workgroups: the others
+                             // only meet the barriers)
   {
     const int nt0 = (3 * he + E) / 16;  // <= 16
     f4 acc[4][MT];
-    dense_acc<MT, 4>(acc, lds, ld, 0, p.m0, p.ksp / 16, nt0, p.mb0, wave, lane);
+    if (mw) dense_acc<MT, 4>(acc, lds, ld, 0, p.m0, p.ksp / 16, nt0, p.mb0, wave, lane);
     __syncthreads();
-    dense_store<MT, 4>(acc, lds, ld, 0, nt0, wave, lane, QmixMixAct{3 * he});
+    if (mw) dense_store<MT, 4>(acc, lds, ld, 0, nt0, wave, lane, QmixMixAct{3 * he});
   }
   __syncthreads();
   {
@@ -391,7 +393,7 @@ __device__ __forceinline__ void qmix_mixer(const QmixArgs& p, float* lds, const 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int t = wave + 4 * j;
-      if (t >= ntot) continue;
+      if (!mw || t >= ntot) continue;
       const float* w;
       const float* bias;
       int col0, tt;
@@ -411,7 +413,7 @@ __device__ __forceinline__ void qmix_mixer(const QmixArgs& p, float* lds, const 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int t = wave + 4 * j;
-      if (t >= ntot) continue;
+      if (!mw || t >= ntot) continue;
       const bool is_abs = t < n1 + n2;  // |W1|, |W2| (mixing_network.py:96,105)
       const int c = t * 16 + (lane & 15);
 #pragma unroll
@@ -518,8 +520,6 @@ __global__ void __launch_bounds__(256) qmix_policy_kernel(QmixArgs p) {
   }
   qmix_mixer<MT>(p, lds, chosen, row0, wave, lane);
 }
-
-// (wave_sync, lbsim_kernels.h: wave-local LDS ordering, no workgroup barrier)
 
 // The same step with one WAVE per agent (agents w, w + 4, ...) over a 16-env tile: each wave runs
 // its agent's whole network in its own LDS region [16][lda] with no workgroup barrier between
@@ -644,6 +644,148 @@ __global__ void __launch_bounds__(256) qmix_agent_wave_kernel(QmixArgs p) {
       }
     }
     wave_sync();
+  }
+  __syncthreads();
+  qmix_mixer<1>(p, lds, chosen, row0, wave, lane);
+}
+
+// The same step with TWO waves per agent (A = 4: eight waves, 16-env tiles): wave 2a + h owns half
+// of agent a's output tiles in every layer (GRU unit tiles u = h, h + 2, ...; fc1 / fc2 tiles
+// [h NT/2, (h+1) NT/2); fc3's k-blocks split in halves and summed), so 8192 envs give 4096 waves --
+// four per SIMD instead of two to hide the MFMA and L2 latency.  The pair shares the agent's LDS
+// region; every layer boundary is a workgroup barrier (all agents run the same layer sequence).
+template <int H, int F>
+__global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
+  extern __shared__ float lds[];
+  constexpr int R = 16, UT = H / 16, NT = F / 16;
+  static_assert(UT % 2 == 0 && NT % 8 == 0, "tiles split in halves of 4-tile passes");
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int a = wave >> 1, h = wave & 1;
+  const int64_t row0 = (int64_t)blockIdx.x * R;
+  const int lda = p.lda, kxp = p.kxp, A = p.A, NQ = p.n_act;
+  float* mine = lds + a * R * lda;
+  float* qv = lds + 4 * R * lda;    // [A][R][16]
+  float* chosen = qv + A * R * 16;  // [R][A]
+  float* part = chosen + R * A;     // [A][R][16] fc3 partials of the h = 1 waves
+  const int kbx = kxp / 16;
+  const int t2 = lane + 64 * h;     // the pair's 128 threads
+  for (int e = t2; e < R * kxp; e += 128) {  // obs rows of agent a, zero padded
+    const int r = e / kxp, c = e - r * kxp;
+    const int64_t b = row0 + r;
+    mine[r * lda + c] = (c < p.I && b < p.B) ? p.obs[(b * A + a) * p.I + c] : 0.0f;
+  }
+  for (int e = t2; e < R * H; e += 128) {  // hidden rows (zeros for reset envs)
+    const int r = e / H, c = e - r * H;
+    const int64_t b = row0 + r;
+    const bool live = b < p.B && !(p.reset && p.reset[b]);
+    mine[r * lda + kxp + c] = live ? p.hidden[(b * A + a) * H + c] : 0.0f;
+  }
+  __syncthreads();
+  const f4* wi = (const f4*)(p.w_ih + (size_t)a * 3 * H * kxp);
+  const f4* wh = (const f4*)(p.w_hh + (size_t)a * 3 * H * H);
+  const float* bi = p.b_ih + a * 3 * H;
+  const float* bh = p.b_hh + a * 3 * H;
+  f4 hn[UT / 2][1];
+#pragma unroll
+  for (int uu = 0; uu < UT / 2; ++uu) {
+    const int u = h + 2 * uu;
+    const int col = u * 16 + (lane & 15);
+    f4 g[4][1];
+    g[0][0] = splat4(bi[2 * H + col]);
+    g[1][0] = splat4(bi[col] + bh[col]);
+    g[2][0] = splat4(bi[H + col] + bh[H + col]);
+    g[3][0] = splat4(bh[2 * H + col]);
+    const f4* const wx[3] = {wi + (size_t)(2 * UT + u) * kbx * 64, wi + (size_t)u * kbx * 64,
+                             wi + (size_t)(UT + u) * kbx * 64};
+    const f4* const wy[3] = {wh + (size_t)u * UT * 64, wh + (size_t)(UT + u) * UT * 64,
+                             wh + (size_t)(2 * UT + u) * UT * 64};
+    mma_multi<1, 3>(*reinterpret_cast<f4(*)[3][1]>(&g[0]), mine, lda, 0, wx, kbx, lane);
+    mma_multi<1, 3>(*reinterpret_cast<f4(*)[3][1]>(&g[1]), mine, lda, kxp, wy, UT, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float hp = mine[(4 * (lane >> 4) + i) * lda + kxp + col];
+      const float r = sigmoid_f(g[1][0][i]);
+      const float z = sigmoid_f(g[2][0][i]);
+      const float n = tanhf(g[0][0][i] + r * g[3][0][i]);
+      hn[uu][0][i] = (1.0f - z) * n + z * hp;
+    }
+  }
+  __syncthreads();  // both halves have read the old hidden state
+#pragma unroll
+  for (int uu = 0; uu < UT / 2; ++uu)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 4 * (lane >> 4) + i, col = (h + 2 * uu) * 16 + (lane & 15);
+      mine[r * lda + kxp + col] = hn[uu][0][i];
+      if (row0 + r < p.B) p.hidden[((row0 + r) * A + a) * H + col] = hn[uu][0][i];
+    }
+  __syncthreads();
+  // fc1 (H -> F) then fc2 (F -> F), ReLU: this wave's NT / 2 tiles, four per mma_multi pass
+#pragma unroll
+  for (int layer = 0; layer < 2; ++layer) {
+    const int col0 = layer == 0 ? kxp : 0, nkb = layer == 0 ? H / 16 : F / 16;
+    const float* w = layer == 0 ? p.w1 + (size_t)a * F * H : p.w2 + (size_t)a * F * F;
+    const float* bias = (layer == 0 ? p.b1 : p.b2) + a * F;
+    f4 acc[NT / 2][1];
+#pragma unroll
+    for (int t0 = 0; t0 < NT / 2; t0 += 4) {
+      const f4* wp[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int t = h * (NT / 2) + t0 + j;
+        wp[j] = (const f4*)w + (size_t)t * nkb * 64;
+        acc[t0 + j][0] = splat4(bias[t * 16 + (lane & 15)]);
+      }
+      mma_multi<1, 4>(*reinterpret_cast<f4(*)[4][1]>(&acc[t0]), mine, lda, col0, wp, nkb, lane);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < NT / 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v = acc[t][0][i];
+        mine[(4 * (lane >> 4) + i) * lda + (h * (NT / 2) + t) * 16 + (lane & 15)] =
+            v > 0.0f ? v : 0.0f;
+      }
+    __syncthreads();
+  }
+  // fc3 -> Q-values (<= 16 actions: one tile), k-blocks [h NT/2, (h+1) NT/2); the halves meet in LDS
+  {
+    f4 q[1] = {splat4(h == 0 ? p.b3[a * 16 + (lane & 15)] : 0.0f)};
+    mma_tile<1>(q, mine, lda, h * (NT / 2) * 16,
+                (const f4*)(p.w3 + (size_t)a * 16 * F) + (size_t)h * (NT / 2) * 64, NT / 2, lane);
+    if (h == 1)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) part[(a * R + 4 * (lane >> 4) + i) * 16 + (lane & 15)] = q[0][i];
+    __syncthreads();
+    if (h == 0)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int o = (a * R + 4 * (lane >> 4) + i) * 16 + (lane & 15);
+        qv[o] = q[0][i] + part[o];
+      }
+  }
+  __syncthreads();
+  if (h == 0 && lane < R) {  // epsilon-greedy for (env lane, agent a), as qmix_policy_kernel
+    const int r = lane;
+    const int64_t b = row0 + r;
+    const float* q = qv + (a * R + r) * 16;
+    int g = 0;
+    for (int j = 1; j < NQ; ++j)
+      if (q[j] > q[g]) g = j;
+    const u32x4 d = philox4x32_10(u32x4{(uint32_t)b, p.step, (uint32_t)a, 4u << 24}, p.key0,
+                                  p.key1);
+    const float u = (float)(d.x >> 8) * 5.9604644775390625e-8f;
+    const int act = u < p.epsilon ? (int)(((uint64_t)d.y * (uint32_t)NQ) >> 32) : g;
+    chosen[r * A + a] = q[act];
+    if (b < p.B) {
+      p.actions[b * A + a] = act;
+      if (p.server_actions)
+        for (int j = 0; j < p.k; ++j) p.server_actions[(b * A + a) * p.k + j] = act;
+      if (p.q_out)
+        for (int j = 0; j < NQ; ++j) p.q_out[(b * A + a) * NQ + j] = q[j];
+      if (p.q_chosen) p.q_chosen[b * A + a] = q[act];
+    }
   }
   __syncthreads();
   qmix_mixer<1>(p, lds, chosen, row0, wave, lane);

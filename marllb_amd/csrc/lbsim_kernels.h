@@ -1069,15 +1069,6 @@ __device__ __forceinline__ double xor_lane(double v, int lane, int m) {
   return m == 1 ? xor_lane_f64<1>(v, lane) : m == 2 ? xor_lane_f64<2>(v, lane) : xor_lane_f64<4>(v, lane);
 }
 
-// Orders one wave's LDS accesses (the observe scratch is private to a wave): a compiler fence and
-// a wave barrier.  A wave's LDS instructions execute in issue order, so no s_barrier (which would
-// meet the other waves of a multi-wave workgroup) and no counter wait are needed.
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v, int lane) {
   uint32_t o;
   o = xor_lane_u32<1>(v, lane); v = o > v ? o : v;

@@ -11,6 +11,15 @@
 
 namespace lbk {
 
+// Orders one wave's LDS accesses (scratch private to a wave): a compiler fence and a wave
+// barrier.  A wave's LDS instructions execute in issue order, so no s_barrier (which would meet the
+// other waves of a multi-wave workgroup) and no counter wait are needed.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ---------------------------------------------------------------- Philox4x32-10 (Salmon et al.
 // SC'11, "Parallel random numbers: as easy as 1, 2, 3").  Counter-based: the draw for
 // (env, episode, stream, index) is a pure function, so no RNG state is stored per env.

@@ -162,12 +162,14 @@ def test_qmix_policy_kernel_matches_modules(g):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{"LBSIM_QMIX_KERNEL": "tile"},
+@pytest.mark.parametrize("env", [{"LBSIM_QMIX_KERNEL": "wave"},
+                                 {"LBSIM_QMIX_KERNEL": "tile"},
                                  {"LBSIM_FUSED_MT": "2", "LBSIM_QMIX_KERNEL": "tile"},
                                  {"LBSIM_FUSED_MT": "4", "LBSIM_QMIX_KERNEL": "tile"}])
 def test_other_tile_forms_match_modules(env):
-    """The layer-split QMIX kernel and the 32 / 64-env tiles (selected once per process by the
-    environment, so checked in a child process) pass the same parity tests."""
+    """The one-wave-per-agent and layer-split QMIX kernels and the 32 / 64-env tiles (selected once
+    per process by the environment, so checked in a child process) pass the same parity tests as
+    the default two-waves-per-agent kernel."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
