@@ -230,6 +230,24 @@ def test_simulator_bit_exact_vs_oracle(lib, oracle_mod, case, mapping):
     env.close()
 
 
+@pytest.mark.parametrize("lanes", ["8", "16"])
+def test_wider_groups_bit_exact(lanes):
+    """LBSIM_DYN_GROUP_LANES widens the server-per-lane groups past pow2 >= S (lanes that hold no
+    server only draw arrivals ahead): the simulator cases with S <= lanes stay bit-exact vs the
+    oracle.  The setting is read once per process, so the cases run in a child process."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ks = [f"test_simulator_bit_exact_vs_oracle[{c}-server]" for c in range(len(CONFIGS))
+          if CONFIGS[c]["S"] <= int(lanes)]
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p",
+                        "no:cacheprovider"] +
+                       [os.path.join(root, "tests", "test_gpu_parity.py") + "::" + k for k in ks],
+                       cwd=root, env={**os.environ, "LBSIM_DYN_GROUP_LANES": lanes},
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
 def test_sharding_invariance(lib):
     """Global env ids key the RNG: two shards reproduce the monolithic run exactly."""
     from marllb_amd.env import VecLoadBalanceEnv
