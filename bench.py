@@ -12,8 +12,10 @@ reward, done), episode bookkeeping and the masked auto-reset launch.
 
 Default N=1 workload: 65536 envs x 4 servers (north-star point; BASELINE configs[1] is the same
 random-policy rollout at 4096 envs and is a parity-test case).  Prints ONE JSON line (rank 0)
-with a `roofline` object for the dominant kernel (HIP-event timed inside the timed region) and a
-`cpu_baseline` (the C oracle on host cores, bounded sample of the same workload).
+with a `roofline` object for the dominant kernel (HIP-event timed inside the timed region), a
+`cpu_baseline` (the C oracle on host cores, bounded sample of the same workload) and, at N=1,
+`late_episode`: the same envs timed again at episode steps 1000 and 5000 (`value` stays the
+early-episode rate, the most expensive phase of an episode).
 """
 import argparse
 import ctypes
@@ -89,6 +91,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dyn-mapping", default="auto", choices=["auto", "env", "server"],
                     help="dynamics kernel mapping: one lane per env / per server (same results)")
+    ap.add_argument("--late-episode", default="1000,5000",
+                    help="rollout workload at N=1: after the headline measurement, keep stepping the "
+                         "same envs and also time --steps steps from these episode steps "
+                         "(comma list; '' to skip).  Reported beside `value`, never as it")
     return ap.parse_args()
 
 
@@ -172,6 +178,37 @@ def cpu_baseline(args, seconds: float):
                                     "host": "different host: survey container, Intel Xeon "
                                             "8 vCPU, reference Python run in place "
                                             "(SURVEY.md §6, BASELINE.md §2)"}}}
+
+
+def late_episode(args, env, handle, lib, one_step, rate, B, S, done_steps):
+    """The same rollout later in its episodes (max_steps 10000, the reference default): every
+    reservoir is full and most servers' reservoirs take no new sample in a step (Algorithm R
+    acceptance 128 / count), so observe reuses most feature rows.  The headline
+    `value` is the early-episode rate (the most expensive phase); this reports where the episode
+    spends most of its steps.  Untimed stepping to each start point, then --steps timed steps."""
+    import torch
+    res = []
+    step = done_steps
+    for target in sorted(int(x) for x in args.late_episode.split(",") if x.strip()):
+        while step < target:
+            one_step()
+            step += 1
+        torch.cuda.synchronize()
+        handle.check(lib.lbsim_profile_begin(handle.h, 4 * args.steps + 8))
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            one_step()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        ms = (ctypes.c_double * 4)()
+        cnt = (ctypes.c_int64 * 4)()
+        handle.check(lib.lbsim_profile_end(handle.h, ms, cnt))
+        step += args.steps
+        res.append({"episode_step": target, "value": B * args.steps / el, "unit": "env-steps/s",
+                    "ms_per_step": el / args.steps * 1e3,
+                    "kernel_avg_ms": {"dynamics": ms[0] / max(1, cnt[0]),
+                                      "observe": ms[1] / max(1, cnt[1])}})
+    return res
 
 
 def spawn_ranks(args) -> int:
@@ -369,6 +406,9 @@ def main():
                     "bound": "mfma", "avg_launch_ms": pms, "flops_per_launch": fl,
                     "achieved_TFLOPs": tf, "peak_TFLOPs": MFMA_F32_PEAK_TFLOPS,
                     "frac": tf / MFMA_F32_PEAK_TFLOPS}
+        if world == 1 and args.workload == "rollout" and args.late_episode:
+            out["late_episode"] = late_episode(args, env, handle, lib, one_step, rate, B, S,
+                                               args.warmup + args.steps)
         if world == 1 and not args.no_cpu_baseline and args.workload == "rollout":
             out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
         print(json.dumps(out), flush=True)
