@@ -13,8 +13,9 @@
 // iteration), then the group assigns the arrival:
 //   SED / LSQ choice: the reference's scan "start at the hashed server h, replace on a strictly
 //     lower score" equals: h (or the first eligible server when h is full) if its score is the
-//     minimum or NaN, else the lowest eligible server holding the minimum — one DPP min reduction
-//     inside the group's row and two ballots;
+//     minimum or NaN, else the lowest eligible server holding the minimum — with finite scores a
+//     (score, rank) minimum over two DPP min reductions inside the group's row; with NaN scores
+//     one DPP min reduction and ballots;
 //   SED2 / LSQ2: the two candidates' scores broadcast by OR-reducing a one-hot word.
 // Arrivals are drawn ahead, G at a time: every G iterations lane j of a group draws the group's
 // arrival cbase + j (Philox block, gap, work) into LDS, so the Philox block and its two logs cost
