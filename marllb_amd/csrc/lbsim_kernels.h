@@ -1261,46 +1261,39 @@ constexpr uint32_t kPackLimit = (1u << 25) - 1u;
 constexpr int kP90Lo = (K - 1) * 9 / 10;
 static_assert(kP90Lo == 114 && (kP90Lo & 15) != 15, "p90 pair inside one lane");
 
-// observe_chunk for the steady state of the simulator: every reservoir of the chunk (<= 4 servers)
-// full (n = K) and every sample below kPackLimit.  Lane (g, j), g = 2 u + r, owns reservoir r
-// (0 fct, 1 duration) of server s_base + u and holds its slots 8 e + j, e = 0..15 -- at n = K
-// exactly numpy's pairwise accumulator j (reservoir.py:143-155) -- in registers through every
-// phase: no LDS image, no per-element loops.  The two groups of a server (lanes 16 u .. 16 u + 15,
-// one DPP row) compute half of the decay weights each and swap halves by row_ror:8.  LDS holds only
-// the 2^-48 fixed-point weights by slot, gathered after the sort.  Same operations in the same
-// order as the general path, so the same bits.  Returns false (nothing written) when the chunk
-// does not qualify.
-template <bool INC>
-__device__ __forceinline__ bool observe_chunk_full(const DevState& st, const SimParams& p, size_t b,
-                                                   int s_base, int S, ObsScratch& sc,
+// observe_chunk with every value in registers, for simulator state whose chunk (<= 4 servers) has
+// n >= 8 samples in each reservoir and every sample below kPackLimit (FULL: n = K, the steady
+// state; else n in [8, K), the first steps of an episode).  Lane (g, j), g = 2 u + r, owns
+// reservoir r (0 fct, 1 duration) of server s_base + u and holds its slots 8 e + j, e = 0..15 --
+// numpy's pairwise accumulator j (reservoir.py:143-155) over the slots below m8 = n - n % 8; the
+// tail slots [m8, n) are added in order after the accumulators are combined.  The two groups of a
+// server (lanes 16 u .. 16 u + 15, one DPP row) compute half of the decay weights each and swap
+// halves by row_ror:8.  LDS holds the 2^-48 fixed-point weights by slot (gathered after the sort;
+// 0 for empty slots) and, when n < K, the tail values and the sorted keys for the p90 pair.  Same
+// operations in the same order as the general path, so the same bits.
+template <bool INC, bool FULL>
+__device__ __forceinline__ void observe_chunk_regs(const DevState& st, const SimParams& p, size_t b,
+                                                   int s_base, int S, int n_in, ObsScratch& sc,
                                                    float* obs_out, int lane) {
   const size_t srow = b * (size_t)p.S + (size_t)s_base;
   const int g = lane >> 3, j = lane & 7, u = g >> 1, r = g & 1;
   const bool act = u < S;
   const size_t sb = srow + (size_t)(act ? u : 0);
-  if (__any(act && st.res_count[sb] < (uint32_t)K)) return false;
+  const int n = FULL ? K : n_in;  // this group's sample count
+  const int m8 = FULL ? K : n - (n & 7);
   // values of reservoir r (the 12-B record is {fct, duration, ts}); timestamps of the half of the
   // slots whose weights this group computes, 8 (q + 8 r) + j -- the pair's other group reads the
   // other half, and the newest timestamp is a max over the 16 lanes of the pair
   const uint32_t* rec = reinterpret_cast<const uint32_t*>(st.res + sb * K + (size_t)j);
   uint32_t key[16], th[8];
-  {
-    // qualification pass; its loads are dropped and re-issued below (L1/L2 hits) so that no
-    // value stays live across the branch into the general path (which would spill at 96 VGPRs)
-    uint32_t vmax = 0;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const uint32_t v = rec[24 * e + r];
-      vmax = v > vmax ? v : vmax;
-    }
-    if (__any(act && vmax >= kPackLimit)) return false;
-    __asm__ volatile("" ::: "memory");
-  }
 #pragma unroll
   for (int e = 0; e < 16; ++e) key[e] = rec[24 * e + r];
   const uint32_t* rts = rec + 2 + 192 * r;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) th[q] = rts[24 * q];
+  for (int q = 0; q < 8; ++q) {
+    th[q] = rts[24 * q];
+    if constexpr (!FULL) th[q] = 8 * (q + 8 * r) + j < n ? th[q] : 0u;  // empty slots: stale words
+  }
   uint32_t tmax = 0;
 #pragma unroll
   for (int q = 0; q < 8; ++q) tmax = th[q] > tmax ? th[q] : tmax;
@@ -1318,8 +1311,10 @@ __device__ __forceinline__ bool observe_chunk_full(const DevState& st, const Sim
   uint64_t* wfix = reinterpret_cast<uint64_t*>(&sc.vals[0][0]) + u * K;  // [4][K] u64
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
+    const int slot = 8 * (q + 8 * r) + j;
     wh[q] = lb_exp2f((float)(tmax - th[q]) * p.decay_c);
-    if (act) wfix[8 * (q + 8 * r) + j] = (uint64_t)(wh[q] * 281474976710656.0f);
+    if constexpr (!FULL) wh[q] = slot < n ? wh[q] : 0.0f;
+    if (act) wfix[slot] = (uint64_t)(wh[q] * 281474976710656.0f);
   }
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
@@ -1328,23 +1323,24 @@ __device__ __forceinline__ bool observe_chunk_full(const DevState& st, const Sim
     w[q + 8] = r ? wh[q] : pw;
   }
 
-  // numpy-order sums (pairwise8 / pairwise8x2 at n = K): accumulator j over e, xor-combine
+  // numpy-order sums (pairwise8 / pairwise8x2): accumulator j over e (terms past m8 are +0: every
+  // term is >= 0, so adding +0 changes no bit), xor-combine, then the tail
   float vf[16];
 #pragma unroll
   for (int e = 0; e < 16; ++e) vf[e] = sample_value<true>(key[e]);
+  auto in_acc = [&](int e) { return FULL || 8 * e + j < m8; };
   float acc = vf[0];
 #pragma unroll
-  for (int e = 1; e < 16; ++e) acc += vf[e];
+  for (int e = 1; e < 16; ++e) acc += in_acc(e) ? vf[e] : 0.0f;
   acc = acc + xor_f32_z<1>(acc, lane);
   acc = acc + xor_f32_z<2>(acc, lane);
   acc = acc + xor_f32_z<4>(acc, lane);
-  const float mean = acc / (float)K;
   double svw = (double)vf[0] * (double)w[0], sw = (double)w[0];
 #pragma unroll
   for (int e = 1; e < 16; ++e) {
     const double wi = (double)w[e];
-    svw += (double)vf[e] * wi;
-    sw += wi;
+    svw += in_acc(e) ? (double)vf[e] * wi : 0.0;
+    sw += in_acc(e) ? wi : 0.0;
   }
   svw = svw + xor_f64_z<1>(svw, lane);
   sw = sw + xor_f64_z<1>(sw, lane);
@@ -1352,6 +1348,27 @@ __device__ __forceinline__ bool observe_chunk_full(const DevState& st, const Sim
   sw = sw + xor_f64_z<2>(sw, lane);
   svw = svw + xor_f64_z<4>(svw, lane);
   sw = sw + xor_f64_z<4>(sw, lane);
+  float* tail_v = reinterpret_cast<float*>(&sc.wts[0][0]) + g * 16;  // [8 groups][8] tail values
+  float* tail_w = reinterpret_cast<float*>(&sc.perm[0][0]) + g * 16;  // [8 groups][8] tail weights
+  int ntail = 0;
+  if constexpr (!FULL) {  // slots [m8, n) are lanes 0 .. n - m8 - 1 at e = m8 / 8: through LDS
+    ntail = n - m8;
+    const int et = m8 >> 3;
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+      if (e == et) {
+        tail_v[j] = vf[e];
+        tail_w[j] = w[e];
+      }
+    wave_sync();
+    for (int k = 0; k < ntail; ++k) {
+      const float tv = tail_v[k], tw = tail_w[k];
+      acc += tv;
+      svw += (double)tv * (double)tw;
+      sw += (double)tw;
+    }
+  }
+  const float mean = acc / (float)n;
   float ss;
   {
     float dv = vf[0] - mean;
@@ -1359,18 +1376,27 @@ __device__ __forceinline__ bool observe_chunk_full(const DevState& st, const Sim
 #pragma unroll
     for (int e = 1; e < 16; ++e) {
       dv = vf[e] - mean;
-      ss += dv * dv;
+      ss += in_acc(e) ? dv * dv : 0.0f;
     }
   }
   ss = ss + xor_f32_z<1>(ss, lane);
   ss = ss + xor_f32_z<2>(ss, lane);
   ss = ss + xor_f32_z<4>(ss, lane);
-  const float sd = sqrtf(ss / (float)K);
+  if constexpr (!FULL) {
+    for (int k = 0; k < ntail; ++k) {
+      const float dv = tail_v[k] - mean;
+      ss += dv * dv;
+    }
+  }
+  const float sd = sqrtf(ss / (float)n);
   const float md = (float)(svw / sw);
 
-  // order statistics: one key-only sort of (us << 7 | slot)
+  // order statistics: one key-only sort of (us << 7 | slot), empty slots last
 #pragma unroll
-  for (int e = 0; e < 16; ++e) key[e] = (key[e] << 7) | (uint32_t)(8 * e + j);
+  for (int e = 0; e < 16; ++e) {
+    key[e] = (key[e] << 7) | (uint32_t)(8 * e + j);
+    if constexpr (!FULL) key[e] = 8 * e + j < n ? key[e] : 0xFFFFFFFFu;
+  }
   bitonic128_keys_g8(key, j);
   wave_sync();  // wfix complete
   uint64_t incl[16];
@@ -1394,7 +1420,8 @@ __device__ __forceinline__ bool observe_chunk_full(const DevState& st, const Sim
   const uint64_t thr = ((((uint64_t)thi << 32) | tlo) * 9u + 9u) / 10u;
   const uint64_t thr_lane = thr > excl ? thr - excl : 0u;
   // the first e with incl[e] >= thr_lane holds this lane's smallest such key (keys ascend with
-  // e): a min instead of a register-indexed read; past the last position: position 127
+  // e): a min instead of a register-indexed read; past the last position: position 127.  The
+  // crossing is always at a filled position (empty slots add no weight).
   uint32_t cand = 0xFFFFFFFFu;
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
@@ -1407,17 +1434,30 @@ __device__ __forceinline__ bool observe_chunk_full(const DevState& st, const Sim
   const int tstar = gm ? __builtin_ctz(gm) : 7;
   cand = crosses ? cand : key[15];
   const float p90d = sample_value<true>(shfl_u32(cand, (lane & ~7) | tstar));
-  // p90: positions kP90Lo, kP90Lo + 1 of lane 7 (reservoir.py:144, numpy 2 'linear' in float32)
+  // p90 (reservoir.py:144, numpy 2 'linear' in float32): virtual index (n - 1) * 0.9f; at n = K
+  // sorted positions kP90Lo, kP90Lo + 1 of lane 7, else read back from LDS
   float p90;
   {
-    const float hidx = (float)(K - 1) * 0.9f;
+    const float hidx = (float)(n - 1) * 0.9f;
     const float fl = floorf(hidx);
     const float gg = hidx - fl;
-    const float va = sample_value<true>(key[kP90Lo & 15]);
-    const float vb = sample_value<true>(key[(kP90Lo & 15) + 1]);
+    float va, vb;
+    if constexpr (FULL) {
+      va = sample_value<true>(key[kP90Lo & 15]);
+      vb = sample_value<true>(key[(kP90Lo & 15) + 1]);
+    } else {
+      wave_sync();  // every gather from wfix done: reuse sc.vals for the sorted keys
+      uint32_t* srt = &sc.vals[g][0];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) srt[16 * j + e] = key[e];
+      wave_sync();
+      const int lo = (int)fl;
+      va = sample_value<true>(srt[lo]);
+      vb = sample_value<true>(srt[lo + 1 < n ? lo + 1 : lo]);
+    }
     const float diff = vb - va;
     p90 = (gg >= 0.5f) ? (vb - diff * (1.0f - gg)) : (va + diff * gg);
-    p90 = __uint_as_float(shfl_u32(__float_as_uint(p90), (lane & ~7) | 7));
+    if constexpr (FULL) p90 = __uint_as_float(shfl_u32(__float_as_uint(p90), (lane & ~7) | 7));
   }
   // row of server u: lane j < 5 of group r writes feature j of reservoir r; lane 5 of the fct
   // group writes n_flow_on
@@ -1432,6 +1472,41 @@ __device__ __forceinline__ bool observe_chunk_full(const DevState& st, const Sim
     }
   }
   wave_sync();
+}
+
+// Chooses observe_chunk_regs for a chunk of simulator state: every reservoir with n >= 8 samples
+// and every sample below kPackLimit (else false: the general path; reservoirs with n < 8 sum
+// sequentially in numpy, samples >= 2^25 - 1 us need the two-pass sort).  FULL (all n = K, the
+// steady state) is a wave-uniform choice.
+template <bool INC>
+__device__ __forceinline__ bool observe_chunk_full(const DevState& st, const SimParams& p, size_t b,
+                                                   int s_base, int S, ObsScratch& sc,
+                                                   float* obs_out, int lane) {
+  const size_t srow = b * (size_t)p.S + (size_t)s_base;
+  const int g = lane >> 3, j = lane & 7, u = g >> 1, r = g & 1;
+  const bool act = u < S;
+  const size_t sb = srow + (size_t)(act ? u : 0);
+  const uint32_t rc = st.res_count[sb];
+  const int n = rc < (uint32_t)K ? (int)rc : K;
+  if (__any(act && n < 8)) return false;
+  const bool full = !__any(act && n < K);
+  {
+    // qualification pass; its loads are dropped and re-issued (L1/L2 hits) so that no value stays
+    // live across the branch into the general path (which would spill at 96 VGPRs).  Empty slots
+    // (stale words of an earlier episode) are not masked: a stale sample >= 2^25 - 1 us only sends
+    // a partly filled chunk to the general path, which is exact for every input.
+    const uint32_t* rec = reinterpret_cast<const uint32_t*>(st.res + sb * K + (size_t)j);
+    uint32_t vmax = 0;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const uint32_t v = rec[24 * e + r];
+      vmax = v > vmax ? v : vmax;
+    }
+    if (__any(act && vmax >= kPackLimit)) return false;
+    __asm__ volatile("" ::: "memory");
+  }
+  if (full) observe_chunk_regs<INC, true>(st, p, b, s_base, S, K, sc, obs_out, lane);
+  else observe_chunk_regs<INC, false>(st, p, b, s_base, S, n, sc, obs_out, lane);
   return true;
 }
 

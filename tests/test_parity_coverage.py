@@ -5,8 +5,9 @@ kernels -- checked here on the CPU with the oracle, which follows the same state
   * arrivals dropped because every queue is full;
   * observe's unchanged-reservoir skip: steps in which dynamics wrote no slot of any server of
     an env (observe reuses the cached features) next to steps that wrote many;
-  * observe's register-resident path (every reservoir of a 4-server chunk full, every sample below
-    2^25 - 1 us) next to its general path (a chunk partly filled, or full with a large sample).
+  * observe's register-resident path (every reservoir of a 4-server chunk holding >= 8 samples,
+    every slot below 2^25 - 1 us), both full (n = 128) and partly filled, next to its general path
+    (a reservoir with fewer than 8 samples, or a large sample in the chunk).
 """
 import numpy as np
 import pytest
@@ -34,7 +35,8 @@ def run_case(oracle_mod, case, steps=12):
     rng = np.random.default_rng(case)
     max_q = 0
     written = []  # slots written per (env, server) by each step's dynamics
-    paths = np.zeros(3, np.int64)  # recomputed chunks: full fast path / full with a big sample / partial
+    paths = np.zeros(4, np.int64)  # recomputed chunks: register path full / register path partly
+    #                                  filled / general path with a big sample / general with n < 8
     for _ in range(steps):
         ora.step(_actions(rng, B, S, c["kw"]))  # the GPU test's action stream
         st = statelayout.parse(ora.state_bytes(), B, S, cfg.queue_capacity, bool(cfg.normalize_obs))
@@ -43,13 +45,17 @@ def run_case(oracle_mod, case, steps=12):
         written.append(per_server.sum(1))  # slots written per env (all its servers)
         nc = (S + 3) // 4
         pad = nc * 4 - S
-        full = np.pad(st["res_count"].reshape(B, S) >= 128, ((0, 0), (0, pad)), constant_values=True)
+        cnt = st["res_count"].reshape(B, S)
+        full = np.pad(cnt >= 128, ((0, 0), (0, pad)), constant_values=True)
+        ge8 = np.pad(cnt >= 8, ((0, 0), (0, pad)), constant_values=True)
+        # the kernel's qualification reads all 128 slots (stale words of empty slots included)
         big = np.maximum(st["res_fct"], st["res_dur"]).reshape(B, S, 128).max(2) >= PACK_LIMIT
         big = np.pad(big, ((0, 0), (0, pad)))
         chg = np.pad(per_server > 0, ((0, 0), (0, pad)))
-        full, big, chg = (x.reshape(B, nc, 4) for x in (full, big, chg))
-        cf, cb, cc = full.all(2), big.any(2), chg.any(2)
-        paths += [(cc & cf & ~cb).sum(), (cc & cf & cb).sum(), (cc & ~cf).sum()]
+        full, ge8, big, chg = (x.reshape(B, nc, 4) for x in (full, ge8, big, chg))
+        cf, c8, cb, cc = full.all(2), ge8.all(2), big.any(2), chg.any(2)
+        paths += [(cc & cf & ~cb).sum(), (cc & c8 & ~cf & ~cb).sum(), (cc & c8 & cb).sum(),
+                  (cc & ~c8).sum()]
     run_case.written = np.concatenate(written)
     run_case.paths = paths
     return st, max_q, S
@@ -58,7 +64,7 @@ def run_case(oracle_mod, case, steps=12):
 def test_parity_cases_cover_rare_paths(oracle_mod):
     two_pass = overflow = dropped = False
     written = []
-    paths = np.zeros(3, np.int64)
+    paths = np.zeros(4, np.int64)
     for case in range(len(CONFIGS)):
         st, max_q, S = run_case(oracle_mod, case)
         two_pass |= bool(max(st["res_fct"].max(), st["res_dur"].max()) >= PACK_LIMIT)
@@ -67,7 +73,8 @@ def test_parity_cases_cover_rare_paths(oracle_mod):
         written.append(run_case.written)
         paths += run_case.paths
     w = np.concatenate(written)
-    assert (paths > 20).all(), f"observe paths (full / full + big sample / partial): {paths}"
+    assert (paths > 20).all(), f"observe paths (register full / register partial / general with a " \
+                               f"big sample / general with n < 8): {paths}"
     assert (w == 0).sum() > 50, "too few env-steps leave every reservoir unchanged (the skip)"
     assert (w == 1).any() and (w >= 64).sum() > 100
     assert two_pass, "no parity case produces a sample >= 2^25 - 1 us"
