@@ -107,7 +107,8 @@ __device__ __forceinline__ uint64_t group_bits(uint64_t m, int gbase) {
 struct SrvLane {
   int32_t cnt, head_tc, head, lh, tail, last, assigned;
   uint32_t rcnt;
-  uint32_t chg[4];  // reservoir slots written this launch (DevState::chg)
+  uint32_t* chgw;   // LDS [4][64]: word w of this lane's 128-bit mask of the reservoir slots
+                    // written this launch (DevState::chg), set by one ds_or per insert
   float score, scale;
   double den, rcp;
   bool act;  // s < S
@@ -165,11 +166,7 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
   const int lane = gbase + s;
   auto wslot = [&](int i) -> int2* { return win + i * 64 + lane; };
   auto mark = [&](int slot) {  // the slot's bit in the lane's 128-bit written-slot mask
-    const uint32_t bit = 1u << (slot & 31), w = (uint32_t)slot >> 5;
-    V.chg[0] |= w == 0 ? bit : 0u;
-    V.chg[1] |= w == 1 ? bit : 0u;
-    V.chg[2] |= w == 2 ? bit : 0u;
-    V.chg[3] |= w == 3 ? bit : 0u;
+    atomicOr(V.chgw + ((uint32_t)slot >> 5) * 64u, 1u << (slot & 31));
   };
   // Draw-ahead: every G iterations (a wave-uniform schedule: all active groups loop in step) lane
   // j of a group draws arrival cbase + j (cbase = the group's next undrawn arrival) -- its Philox
@@ -345,11 +342,7 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
   }
   auto wslot = [&](int i) -> int2* { return win + i * 64 + lane; };
   auto mark = [&](int slot) {  // the slot's bit in the lane's 128-bit written-slot mask
-    const uint32_t bit = 1u << (slot & 31), w = (uint32_t)slot >> 5;
-    V.chg[0] |= w == 0 ? bit : 0u;
-    V.chg[1] |= w == 1 ? bit : 0u;
-    V.chg[2] |= w == 2 ? bit : 0u;
-    V.chg[3] |= w == 3 ? bit : 0u;
+    atomicOr(V.chgw + ((uint32_t)slot >> 5) * 64u, 1u << (slot & 31));
   };
 
   // ---- 1. this lane's carried-in flows that complete in this step: samples in FIFO order
@@ -435,6 +428,7 @@ __global__ void __launch_bounds__(64)
   __shared__ int2 win[WL * 64];
   __shared__ int32_t atab[alias ? 2 * 64 : 1];
   __shared__ int4 acache[64];  // draw-ahead arrival slots, [group][G]
+  __shared__ uint32_t chgw[4 * 64];  // written-slot masks, [word][lane]
   const int lane = (int)threadIdx.x;
   const int s = lane & (G - 1);
   const int gbase = lane & ~(G - 1);
@@ -456,7 +450,8 @@ __global__ void __launch_bounds__(64)
   V.assigned = 0;
   V.lh = 0;
 #pragma unroll
-  for (int w = 0; w < 4; ++w) V.chg[w] = 0u;
+  for (int w = 0; w < 4; ++w) chgw[w * 64 + lane] = 0u;
+  V.chgw = chgw + lane;
   const uint32_t sb = b * (uint32_t)S + (uint32_t)s;
   float wall[G];
   float w_own = 1.0f;
@@ -536,7 +531,7 @@ __global__ void __launch_bounds__(64)
     st.last_tc[sb] = V.last;
     st.res_count[sb] = V.rcnt;
     *reinterpret_cast<uint4*>(st.chg + (size_t)sb * 4) =
-        make_uint4(V.chg[0], V.chg[1], V.chg[2], V.chg[3]);
+        make_uint4(chgw[lane], chgw[64 + lane], chgw[128 + lane], chgw[192 + lane]);
     if (MODE != kModeReset && assign_out != nullptr) assign_out[sb] = V.assigned;
   }
   if (s == 0) {
