@@ -13,9 +13,9 @@ reward, done), episode bookkeeping and the masked auto-reset launch.
 Default N=1 workload: 65536 envs x 4 servers (north-star point; BASELINE configs[1] is the same
 random-policy rollout at 4096 envs and is a parity-test case).  Prints ONE JSON line (rank 0)
 with a `roofline` object for the dominant kernel (HIP-event timed inside the timed region), a
-`cpu_baseline` (the C oracle on host cores, bounded sample of the same workload) and, at N=1,
-`late_episode`: the same envs timed again at episode steps 1000 and 5000 (`value` stays the
-early-episode rate, the most expensive phase of an episode).
+`cpu_baseline` (the C oracle on host cores, bounded sample of the same workload) and, with
+`--late-episode 1000,5000` at N=1, `late_episode`: the same envs timed again at those episode steps
+(`value` stays the early-episode rate, the most expensive phase of an episode).
 """
 import argparse
 import ctypes
@@ -91,10 +91,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dyn-mapping", default="auto", choices=["auto", "env", "server"],
                     help="dynamics kernel mapping: one lane per env / per server (same results)")
-    ap.add_argument("--late-episode", default="1000,5000",
+    ap.add_argument("--late-episode", default="",
                     help="rollout workload at N=1: after the headline measurement, keep stepping the "
-                         "same envs and also time --steps steps from these episode steps "
-                         "(comma list; '' to skip).  Reported beside `value`, never as it")
+                         "same envs and also time --steps steps from these episode steps (comma "
+                         "list, e.g. 1000,5000; off by default so a profile of the default command "
+                         "covers exactly the headline steps).  Reported beside `value`, never as it")
     return ap.parse_args()
 
 
