@@ -175,6 +175,10 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
   // the two logs cost one pass per G iterations instead of one per iteration.
   uint32_t cbase = 0u;
   uint32_t it = 0u;
+  // TRACE: the trace row of arrival kbase, advanced by the arrivals consumed between refills (one
+  // 64-bit modulo per step instead of one per drawn arrival)
+  uint32_t kbase = E.arr_idx + 1u, rbase = 0u;
+  if constexpr (TRACE) rbase = trace_row(p, E.gid, E.episode, kbase);
   for (;;) {
     if ((it & (uint32_t)(G - 1)) == 0u) {
       cbase = E.arr_idx + 1u;
@@ -183,7 +187,12 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
       int32_t gap;
       float wk;
       if constexpr (TRACE) {
-        const uint32_t r = trace_row(p, E.gid, E.episode, k);
+        const uint32_t rows = p.trace_rows;
+        rbase += cbase - kbase;  // <= G arrivals since the last refill
+        kbase = cbase;
+        while (rbase >= rows) rbase -= rows;
+        uint32_t r = rbase + (uint32_t)s;
+        while (r >= rows) r -= rows;
         gap = (int32_t)st.trace_gap[r];
         wk = st.trace_work[r];
       } else {
