@@ -1834,6 +1834,27 @@ __device__ __forceinline__ double reward_values(int n, X x, int metric) {
   }
 }
 
+// reward_values' jain_fairness (rewards.py:21-67) for n <= 4 active values, straight-line: numpy's
+// pairwise sum of n < 8 terms is the sequential sum from 0.0, and a term past n adds +0.0 to a
+// non-negative partial sum (every load is >= 0), which changes no bit; 1 / n from a table of the
+// correctly rounded quotients.
+__device__ __forceinline__ double jain_upto4(int n, const float* x) {
+  if (n == 0) return 0.0;
+  const double eps = 1e-10;
+  double sv = 0.0, sq = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const double v = i < n ? (double)x[i] : 0.0;
+    sv += v;
+    sq += v * v;
+  }
+  if (sv < eps) return 1.0;
+  if (sq < eps) return 1.0;
+  const double j = (sv * sv) / ((double)n * sq);
+  const double lo = n == 1 ? 1.0 : n == 2 ? 0.5 : n == 3 ? 1.0 / 3.0 : 0.25;
+  return j < lo ? lo : (j > 1.0 ? 1.0 : j);
+}
+
 // Active servers of an (S, 11) row as a bit mask, one thread.
 __device__ __forceinline__ uint64_t active_mask_seq(const float* obs, int S) {
   uint64_t m = 0;
@@ -1908,9 +1929,14 @@ __global__ void __launch_bounds__(64 * kObsWavesPerEnv<MAXS>, 5)
     if (act && fok) s_act[__popcll(act_mask & ((1ull << lane) - 1ull))] = s_obs[lane * NF + p.reward_field];
     wave_sync();
     if (mode == kModeStep && lane == 0) {
-      const double r = fok ? reward_values(__popcll(act_mask), [&](int i) { return (double)s_act[i]; },
-                                           p.reward_metric)
-                           : 0.0;
+      const int na = __popcll(act_mask);
+      double r = 0.0;
+      if (fok) {
+        if (MAXS <= kObsChunk && p.reward_metric == 0)
+          r = jain_upto4(na, s_act);
+        else
+          r = reward_values(na, [&](int i) { return (double)s_act[i]; }, p.reward_metric);
+      }
       out.reward[b] = (float)r;
       const int32_t es = st.ep_step[b] + 1;
       const double er = st.ep_return[b] + r;
