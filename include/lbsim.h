@@ -311,6 +311,24 @@ int lbsim_set_trace(lbsim_t* h, const uint32_t* gap_us, const float* work, int64
 int lbsim_alias_tables(const float* weights, int64_t n, int S, float* odd_out, int32_t* alias_out,
                        int32_t* active_out, void* stream);
 
+/* Stateless: n Vose alias tables of S weights each (device pointers), the O(n) build of
+ * problem-07's realtime VPP plugin (realtime-mode/problem-07-realtime-deployment/vpp-plugin/
+ * alias_table.h:82-158, alias_table_build, rebuilt by lb_rl_node.c:92-111 from the weights the
+ * controller writes): weights[n, S] f32 -> prob_out[n, S] f32, alias_out[n, S] u32, in the
+ * float32 arithmetic of the C (a row summing to <= 0 gets the identity table). */
+int lbsim_vose_tables(const float* weights, int64_t n, int S, float* prob_out,
+                      uint32_t* alias_out, void* stream);
+
+/* Stateless: k draws of alias_table_sample (alias_table.h:195-209, the per-packet pick of
+ * lb_rl_node.c:246-288) from each of n tables (prob[n, S], alias[n, S] as lbsim_vose_tables
+ * writes them) with the table's xorshift32 state (alias_table.h:163-172; state_io[n] u32, the
+ * C's random_state, advanced in place).  idx_out[n, k] i32 (may be NULL) gets the picks;
+ * hist_out[n, S] u64 (may be NULL) the per-server counts of this call
+ * (alias_table_test_distribution, :221-237).  k <= INT32_MAX. */
+int lbsim_vose_sample(const float* prob, const uint32_t* alias, int64_t n, int S,
+                      uint32_t* state_io, int64_t k, int32_t* idx_out, uint64_t* hist_out,
+                      void* stream);
+
 /*
  * Kernel timing: between lbsim_profile_begin and lbsim_profile_end every kernel launch of this
  * handle is bracketed by a pair of hipEvents recorded on the launch stream (at most max_launches

@@ -142,6 +142,9 @@ _SIGNATURES = {
                                        ctypes.c_int, _P, _P]),
     "lbsim_set_trace": (ctypes.c_int, [_P, _P, _P, ctypes.c_int64, _P]),
     "lbsim_alias_tables": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int, _P, _P, _P, _P]),
+    "lbsim_vose_tables": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int, _P, _P, _P]),
+    "lbsim_vose_sample": (ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.c_int, _P, ctypes.c_int64,
+                                         _P, _P, _P]),
     "lbsim_reservoir_features": (ctypes.c_int, [_P, _P, _P, ctypes.c_int64, ctypes.c_float, _P,
                                                 _P]),
     "lbsim_profile_begin": (ctypes.c_int, [_P, ctypes.c_int]),

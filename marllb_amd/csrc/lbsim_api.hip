@@ -813,6 +813,27 @@ int lbsim_alias_tables(const float* weights, int64_t n, int S, float* odd_out, i
   return hipGetLastError() == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
 }
 
+int lbsim_vose_tables(const float* weights, int64_t n, int S, float* prob_out,
+                      uint32_t* alias_out, void* stream) {
+  if (n < 0 || S < 1 || S > LBSIM_MAX_SERVERS) return LBSIM_EINVAL;
+  if (n == 0) return LBSIM_OK;
+  if (!weights || !prob_out || !alias_out) return LBSIM_EINVAL;
+  hipLaunchKernelGGL(vose_tables_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
+                     (hipStream_t)stream, weights, n, S, prob_out, alias_out);
+  return hipGetLastError() == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
+}
+
+int lbsim_vose_sample(const float* prob, const uint32_t* alias, int64_t n, int S,
+                      uint32_t* state_io, int64_t k, int32_t* idx_out, uint64_t* hist_out,
+                      void* stream) {
+  if (n < 0 || S < 1 || S > LBSIM_MAX_SERVERS || k < 0 || k > INT32_MAX) return LBSIM_EINVAL;
+  if (n == 0) return LBSIM_OK;
+  if (!prob || !alias || !state_io) return LBSIM_EINVAL;
+  hipLaunchKernelGGL(vose_sample_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
+                     (hipStream_t)stream, prob, alias, n, S, state_io, k, idx_out, hist_out);
+  return hipGetLastError() == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
+}
+
 int lbsim_reservoir_features(const float* values, const uint32_t* ts_ms, const uint32_t* counts,
                              int64_t n, float decay_factor, float* feats_out, void* stream) {
   if (values == nullptr || ts_ms == nullptr || counts == nullptr || feats_out == nullptr || n < 0)

@@ -57,6 +57,9 @@ def load() -> ctypes.CDLL:
         "oracle_normalize": (None, [_P, ctypes.c_int, _P, _P, _P, _P]),
         "oracle_set_trace": (ctypes.c_int, [_P, _P, _P, ctypes.c_long]),
         "oracle_gen_alias": (None, [_P, ctypes.c_int, _P, _P]),
+        "oracle_vose_build": (None, [_P, ctypes.c_int, _P, _P]),
+        "oracle_vose_sample": (ctypes.c_uint32, [_P, _P, ctypes.c_int, ctypes.c_uint32,
+                                                 ctypes.c_int64, _P, _P]),
         "oracle_algr_slot": (ctypes.c_long, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                              ctypes.c_uint32, _P]),
         "oracle_algr_slot_r32": (ctypes.c_long, [ctypes.c_uint32, ctypes.c_uint32]),
@@ -81,6 +84,28 @@ def gen_alias(weights):
     alias = np.zeros(len(w), np.int32)
     load().oracle_gen_alias(ptr(w), len(w), ptr(odd), ptr(alias))
     return odd, alias
+
+
+def vose_build(weights):
+    """oracle_vose_build: (prob float32[n], alias uint32[n]) of problem-07's alias_table_build
+    (vpp-plugin/alias_table.h:82-158)."""
+    w = np.ascontiguousarray(weights, np.float32)
+    prob = np.zeros(len(w), np.float32)
+    alias = np.zeros(len(w), np.uint32)
+    load().oracle_vose_build(ptr(w), len(w), ptr(prob), ptr(alias))
+    return prob, alias
+
+
+def vose_sample(prob, alias, state, k):
+    """oracle_vose_sample: k alias_table_sample picks (alias_table.h:163-209) from xorshift32
+    `state` -> (picks int32[k], histogram uint64[n], final state)."""
+    p = np.ascontiguousarray(prob, np.float32)
+    a = np.ascontiguousarray(alias, np.uint32)
+    idx = np.zeros(k, np.int32)
+    hist = np.zeros(len(p), np.uint64)
+    st = load().oracle_vose_sample(ptr(p), ptr(a), len(p), int(state) & 0xFFFFFFFF, k,
+                                   ptr(idx), ptr(hist))
+    return idx, hist, st
 
 
 def philox(ctr, key) -> np.ndarray:

@@ -448,6 +448,62 @@ void oracle_gen_alias(const float* w, int n, double* odd_out, int32_t* alias_out
 #undef NEXT_BIG
 }
 
+/* Vose alias table of problem-07's VPP plugin
+ * (realtime-mode/problem-07-realtime-deployment/vpp-plugin/alias_table.h:82-158), in float32 as
+ * the C: sequential f32 sum (:90-93); sum <= 0 (NaN is not) -> the identity table (:95-102);
+ * prob_scaled[i] = (f32)n * w[i] / sum (:106-108); small (< 1) / large stacks filled in index
+ * order (:116-122) and popped from the top (:125-139); the large's remainder
+ * (prob_l + prob_s) - 1.0 is an f32 sum, a double subtraction and a store to f32 (:132) -- the
+ * correctly rounded f32 subtraction, since double carries more than 2 x 24 + 2 bits; leftovers
+ * get (1, self) (:142-152).  n <= LBSIM_MAX_SERVERS. */
+void oracle_vose_build(const float* w, int n, float* prob, uint32_t* alias) {
+  float sum = 0.0f;
+  for (int i = 0; i < n; ++i) sum += w[i];
+  if (sum <= 0.0f) {
+    for (int i = 0; i < n; ++i) { prob[i] = 1.0f; alias[i] = (uint32_t)i; }
+    return;
+  }
+  float ps[LBSIM_MAX_SERVERS];
+  uint32_t small[LBSIM_MAX_SERVERS], large[LBSIM_MAX_SERVERS];
+  int ns = 0, nl = 0;
+  for (int i = 0; i < n; ++i) ps[i] = (float)(uint32_t)n * w[i] / sum;
+  for (int i = 0; i < n; ++i) {
+    if (ps[i] < 1.0f) small[ns++] = (uint32_t)i;
+    else large[nl++] = (uint32_t)i;
+  }
+  while (ns > 0 && nl > 0) {
+    const uint32_t s = small[--ns], l = large[--nl];
+    prob[s] = ps[s];
+    alias[s] = l;
+    ps[l] = (float)((double)(ps[l] + ps[s]) - 1.0);
+    if (ps[l] < 1.0f) small[ns++] = l;
+    else large[nl++] = l;
+  }
+  while (ns > 0) { const uint32_t s = small[--ns]; prob[s] = 1.0f; alias[s] = s; }
+  while (nl > 0) { const uint32_t l = large[--nl]; prob[l] = 1.0f; alias[l] = l; }
+}
+
+/* alias_table_sample (alias_table.h:195-209) k times from the table's xorshift32 state
+ * (:163-172: x ^= x << 13; x ^= x >> 17; x ^= x << 5): i = x1 % n, r = (f32)x2 / (f32)0xFFFFFFFF
+ * (:178-182), the pick is i if r < prob[i] else alias[i].  idx_out[k] (may be NULL) and the
+ * histogram hist[n] += picks (alias_table_test_distribution, :221-237; not zeroed here).
+ * Returns the final state. */
+uint32_t oracle_vose_sample(const float* prob, const uint32_t* alias, int n, uint32_t state,
+                            int64_t k, int32_t* idx_out, uint64_t* hist) {
+  for (int64_t j = 0; j < k; ++j) {
+    uint32_t x = state;
+    x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+    const uint32_t i = x % (uint32_t)n;
+    x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+    state = x;
+    const float r = (float)x / (float)0xFFFFFFFFu;
+    const uint32_t pick = r < prob[i] ? i : alias[i];
+    if (idx_out) idx_out[j] = (int32_t)pick;
+    if (hist) hist[pick] += 1;
+  }
+  return state;
+}
+
 static int ring_head(const oracle_t* o, size_t sb) { return (int)(o->hc[sb] & 0xFFFFu); }
 static int ring_count(const oracle_t* o, size_t sb) { return (int)(o->hc[sb] >> 16); }
 static void ring_set(oracle_t* o, size_t sb, int head, int cnt) {

@@ -111,6 +111,60 @@ def test_alias_tables_kernel_matches_reference(lib, oracle_mod, golden_dir):
         assert (act.cpu().numpy()[r, len(keep):] == -1).all()
 
 
+def test_vose_kernels_match_oracle(lib, oracle_mod):
+    """problem-07's Vose alias tables (vpp-plugin/alias_table.h:82-158) built on the GPU equal
+    oracle_vose_build bit for bit (prob as float32 bits, alias indices), and alias_table_sample
+    (:163-209) driven from the same xorshift32 states gives the same picks, histograms and final
+    states.  Rows: ragged S 1..64, zero / all-zero / negative-sum / wide-range weights.
+    (Parity vs the C itself is unpinned: alias_table.h needs vppinfra to compile.)"""
+    from tests.test_oracle_golden import vose_rows
+    rows = vose_rows(11)
+    by_s = {}
+    for w in rows:
+        by_s.setdefault(len(w), []).append(w)
+    K = 300
+    for S, ws in sorted(by_s.items()):
+        w = np.stack(ws).astype(np.float32)
+        n = len(w)
+        prob = torch.empty((n, S), dtype=torch.float32, device="cuda:0")
+        ali = torch.empty((n, S), dtype=torch.int32, device="cuda:0")
+        assert lib.load().lbsim_vose_tables(dev(w).data_ptr(), n, S, prob.data_ptr(),
+                                            ali.data_ptr(), None) == 0
+        states0 = (np.arange(n, dtype=np.uint64) * 2654435761 + S + 1).astype(np.uint32)
+        st = dev(states0.view(np.int32))
+        idx = torch.empty((n, K), dtype=torch.int32, device="cuda:0")
+        hist = torch.empty((n, S), dtype=torch.int64, device="cuda:0")
+        assert lib.load().lbsim_vose_sample(prob.data_ptr(), ali.data_ptr(), n, S, st.data_ptr(),
+                                            K, idx.data_ptr(), hist.data_ptr(), None) == 0
+        torch.cuda.synchronize()
+        gp, ga = prob.cpu().numpy(), ali.cpu().numpy().view(np.uint32)
+        gi, gh = idx.cpu().numpy(), hist.cpu().numpy()
+        gs = st.cpu().numpy().view(np.uint32)
+        for r in range(n):
+            p, a = oracle_mod.vose_build(w[r])
+            np.testing.assert_array_equal(gp[r].view(np.uint32), p.view(np.uint32))
+            np.testing.assert_array_equal(ga[r], a)
+            oi, oh, os_ = oracle_mod.vose_sample(p, a, int(states0[r]), K)
+            np.testing.assert_array_equal(gi[r], oi)
+            np.testing.assert_array_equal(gh[r], oh.astype(np.int64))
+            assert int(gs[r]) == os_
+    # large batch, histogram only: frequencies follow the weights
+    n, S, K = 4096, 8, 20000
+    w = np.tile(np.array([1, 2, 0, 4, 1, 1, 0.5, 0.5], np.float32), (n, 1))
+    prob = torch.empty((n, S), dtype=torch.float32, device="cuda:0")
+    ali = torch.empty((n, S), dtype=torch.int32, device="cuda:0")
+    assert lib.load().lbsim_vose_tables(dev(w).data_ptr(), n, S, prob.data_ptr(), ali.data_ptr(),
+                                        None) == 0
+    st = dev((np.arange(n, dtype=np.uint32) * 7 + 1).view(np.int32))
+    hist = torch.empty((n, S), dtype=torch.int64, device="cuda:0")
+    assert lib.load().lbsim_vose_sample(prob.data_ptr(), ali.data_ptr(), n, S, st.data_ptr(), K,
+                                        None, hist.data_ptr(), None) == 0
+    freq = hist.sum(0).double().cpu().numpy() / (n * K)
+    np.testing.assert_allclose(freq, w[0] / w[0].sum(), atol=2e-4)
+    assert lib.load().lbsim_vose_sample(prob.data_ptr(), ali.data_ptr(), n, 0, st.data_ptr(), K,
+                                        None, None, None) < 0
+
+
 # ------------------------------------------------------------------ the simulator
 CONFIGS = [
     dict(B=257, S=4, kw={}),

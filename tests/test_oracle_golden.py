@@ -180,3 +180,55 @@ def test_alias_pick_frequencies(oracle_mod):
     pick = np.where(rn - bucket.astype(np.float32) > odd[bucket], alias[bucket], bucket)
     freq = np.bincount(pick, minlength=len(w)) / len(u)
     np.testing.assert_allclose(freq, w / w.sum(), atol=3e-3)
+
+
+def vose_rows(seed=5):
+    """Weight rows for the Vose tests: ragged S (1..64), zeros, ties, one dominant weight,
+    all-zero and negative-sum rows (the identity table), huge dynamic range."""
+    rng = np.random.default_rng(seed)
+    rows = [np.array([1, 2, 3, 2], np.float32), np.ones(4, np.float32), np.zeros(6, np.float32),
+            np.array([5.0], np.float32), np.array([0, 0, 7, 0], np.float32),
+            np.array([-1.0, 0.5, 0.25], np.float32), np.array([1e-6, 1e6, 1.0, 3.0], np.float32),
+            np.array([0.1] * 10 + [10.0], np.float32)]
+    for S in (2, 3, 4, 8, 16, 20, 33, 64):
+        for _ in range(12):
+            w = rng.choice([0.1, 1.0, 1.5, 2.0, 10.0], S).astype(np.float32)
+            if rng.random() < 0.5:
+                w = rng.uniform(0, 10, S).astype(np.float32)
+            w[rng.random(S) < 0.2] = 0.0
+            rows.append(w)
+    return rows
+
+
+def test_vose_known_answers(oracle_mod):
+    """Hand-traced alias_table_build (problem-07 vpp-plugin/alias_table.h:82-158) and the
+    xorshift32 of alias_table_random (:163-172)."""
+    # w = [1,2,3,2]: prob_scaled [0.5,1,1.5,1]; small [0], large [1,2,3]; (0 <- 3) leaves 3 at
+    # 0.5 -> small; (3 <- 2) leaves 2 at 1.0 -> large; leftovers 2, 1 are (1, self)
+    prob, alias = oracle_mod.vose_build([1, 2, 3, 2])
+    assert prob.tolist() == [0.5, 1.0, 1.0, 0.5] and alias.tolist() == [3, 1, 2, 2]
+    prob, alias = oracle_mod.vose_build([0, 0, 0])  # sum <= 0: identity (:95-102)
+    assert prob.tolist() == [1.0] * 3 and alias.tolist() == [0, 1, 2]
+    # xorshift32 from state 1: 270369, then 67634689 (13/17/5 triple)
+    idx, hist, st = oracle_mod.vose_sample(np.ones(4, np.float32), np.arange(4), 1, 1)
+    assert st == 67634689 and idx.tolist() == [270369 % 4] and hist.tolist() == [0, 1, 0, 0]
+
+
+def test_vose_tables_represent_weights(oracle_mod):
+    """Every Vose table's implied distribution (prob[i] + sum over j aliased to i of
+    1 - prob[j], over n) equals w / sum(w) within float32 rounding; the sampler's frequencies
+    follow it."""
+    for w in vose_rows():
+        prob, alias = oracle_mod.vose_build(w)
+        n = len(w)
+        assert ((prob >= 0) & (prob <= 1.0 + 1e-6)).all() and (alias < n).all()
+        implied = prob.astype(np.float64).copy()
+        np.add.at(implied, alias, 1.0 - prob.astype(np.float64))
+        implied /= n
+        s = float(np.sum(w, dtype=np.float32))
+        want = w / s if s > 0 else np.full(n, 1.0 / n)
+        np.testing.assert_allclose(implied, want, atol=2e-6 * max(1, n))
+    w = np.array([1, 2, 3, 2, 0, 8], np.float32)
+    prob, alias = oracle_mod.vose_build(w)
+    _, hist, _ = oracle_mod.vose_sample(prob, alias, 12345, 400000)
+    np.testing.assert_allclose(hist / 400000, w / w.sum(), atol=3e-3)
