@@ -91,6 +91,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dyn-mapping", default="auto", choices=["auto", "env", "server"],
                     help="dynamics kernel mapping: one lane per env / per server (same results)")
+    ap.add_argument("--step-streams", type=int, default=1,
+                    help="lbsim step_streams: the batch as N env ranges on internal HIP streams "
+                         "(same results; overlaps one range's dynamics with another's observe)")
     ap.add_argument("--late-episode", default="",
                     help="rollout workload at N=1: after the headline measurement, keep stepping the "
                          "same envs and also time --steps steps from these episode steps (comma "
@@ -195,7 +198,7 @@ def late_episode(args, env, handle, lib, one_step, rate, B, S, done_steps):
             one_step()
             step += 1
         torch.cuda.synchronize()
-        handle.check(lib.lbsim_profile_begin(handle.h, 4 * args.steps + 8))
+        handle.check(lib.lbsim_profile_begin(handle.h, (4 * args.steps + 8) * max(1, args.step_streams)))
         t0 = time.perf_counter()
         for _ in range(args.steps):
             one_step()
@@ -281,7 +284,8 @@ def main():
         from marllb_amd import trace
         tr = trace.builtin(args.trace)
     common = dict(device=dev, seed=args.seed, env_id_offset=shard.env_id_offset, autoreset=True,
-                  assign_policy=args.policy, trace=tr, dyn_mapping=args.dyn_mapping)
+                  assign_policy=args.policy, trace=tr, dyn_mapping=args.dyn_mapping,
+                  step_streams=args.step_streams)
     torch.manual_seed(args.seed)  # network init (random weights of the reference architecture)
     if args.workload == "rollout":
         env = VecLoadBalanceEnv(B, S, max_steps=10000, **common)
@@ -323,7 +327,7 @@ def main():
     from marllb_amd import policies
     if args.workload != "rollout":  # HIP events around each fused policy launch
         policies.profile_events = []
-    handle.check(lib.lbsim_profile_begin(handle.h, 4 * args.steps + 8))
+    handle.check(lib.lbsim_profile_begin(handle.h, (4 * args.steps + 8) * max(1, args.step_streams)))
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_step()
@@ -347,18 +351,21 @@ def main():
         rate = tr.rate if tr is not None else ARRIVAL_RATE
         abytes = algorithmic_bytes(S, rate * STEP_INTERVAL)
         abytes[dyn] = abytes.pop("dynamics_kernel")
+        # with step_streams > 1 each launch covers one env range (whole 64-env blocks)
+        parts = min(max(args.step_streams, 1), max(1, (B + 63) // 64))
+        launch_envs = B / parts
         per_kernel = {}
         for k in names:
-            ab_k = abytes[k] * B
+            ab_k = abytes[k] * launch_envs
             ach = ab_k / (avg[k] * 1e-3) / 1e9
             per_kernel[k] = {"avg_launch_ms": avg[k], "algorithmic_bytes_per_launch": ab_k,
                              "achieved_GBps": ach, "frac": ach / HBM_PEAK_GBS}
         dom = max(avg, key=avg.get)
-        ab = abytes[dom] * B
+        ab = abytes[dom] * launch_envs
         achieved = ab / (avg[dom] * 1e-3) / 1e9
         traffic = None
         tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(tfile):
+        if parts == 1 and os.path.exists(tfile):  # PMC passes were per whole-batch launch
             t = json.load(open(tfile))
             if t.get("batch") == B and t.get("servers") == S and dom in t.get("bytes_per_launch", {}):
                 traffic = t["bytes_per_launch"][dom]
@@ -378,7 +385,8 @@ def main():
                        "assign_policy": args.policy,
                        "envs_per_gpu": B, "servers": S, "global_batch": world * B,
                        "step_interval_s": 0.25, "autoreset": True,
-                       "parallelism": f"env-shard x{world}", "dyn_mapping": args.dyn_mapping},
+                       "parallelism": f"env-shard x{world}", "dyn_mapping": args.dyn_mapping,
+                       "step_streams": parts},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "algorithmic_bytes_per_launch": ab,
