@@ -91,9 +91,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dyn-mapping", default="auto", choices=["auto", "env", "server"],
                     help="dynamics kernel mapping: one lane per env / per server (same results)")
-    ap.add_argument("--step-streams", type=int, default=1,
-                    help="lbsim step_streams: the batch as N env ranges on internal HIP streams "
-                         "(same results; overlaps one range's dynamics with another's observe)")
+    ap.add_argument("--async-groups", type=int, default=0,
+                    help="rollout workload at N=1: after the headline, also time the same rollout "
+                         "as this many env groups (B / groups envs each, global ids kept), each "
+                         "stepped on its own HIP stream with no join between groups per step "
+                         "(EnvPool-style async groups).  Off by default; reported beside `value`, "
+                         "never as it")
     ap.add_argument("--late-episode", default="",
                     help="rollout workload at N=1: after the headline measurement, keep stepping the "
                          "same envs and also time --steps steps from these episode steps (comma "
@@ -184,6 +187,51 @@ def cpu_baseline(args, seconds: float):
                                             "(SURVEY.md §6, BASELINE.md §2)"}}}
 
 
+def async_groups(args, dev, shard, B, S, common, groups):
+    """The headline rollout as `groups` env groups of B / groups envs (global ids kept, so the
+    same envs), each stepped on its own HIP stream with its own random-action generator and no
+    join between groups inside a step: a group's next dynamics launch can start while another
+    group's observe is running, filling the SIMDs that the latency-bound dynamics kernel's tail
+    leaves idle (one step = every group advances one env step; warmup and timing as the headline;
+    profiles/r02_round2c/stream_split_*.jsonl).  A different calling pattern from one batched
+    step(), so it is reported beside `value`, never as it."""
+    import torch
+    from marllb_amd.env import VecLoadBalanceEnv
+    b = B // groups
+    streams = [torch.cuda.Stream(dev) for _ in range(groups)]
+    envs, gens = [], []
+    for i in range(groups):
+        kw = dict(common)
+        kw["env_id_offset"] = shard.env_id_offset + i * b
+        with torch.cuda.stream(streams[i]):
+            e = VecLoadBalanceEnv(b, S, max_steps=10000, **kw)
+            e.reset()
+            g = torch.Generator(device=dev)
+            g.manual_seed(args.seed + 1000 + i)
+        envs.append(e)
+        gens.append(g)
+
+    def step_all():
+        for i in range(groups):
+            with torch.cuda.stream(streams[i]):
+                a = torch.randint(0, 3, (b, S), device=dev, dtype=torch.int64, generator=gens[i])
+                envs[i].step(a)
+
+    for _ in range(args.warmup):
+        step_all()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step_all()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    for e in envs:
+        e.close()
+    return {"groups": groups, "envs_per_group": b, "value": groups * b * args.steps / el,
+            "unit": "env-steps/s", "ms_per_step": el / args.steps * 1e3,
+            "streams": "one HIP stream per group, no cross-group join per step"}
+
+
 def late_episode(args, env, handle, lib, one_step, rate, B, S, done_steps):
     """The same rollout later in its episodes (max_steps 10000, the reference default): every
     reservoir is full and most servers' reservoirs take no new sample in a step (Algorithm R
@@ -198,7 +246,7 @@ def late_episode(args, env, handle, lib, one_step, rate, B, S, done_steps):
             one_step()
             step += 1
         torch.cuda.synchronize()
-        handle.check(lib.lbsim_profile_begin(handle.h, (4 * args.steps + 8) * max(1, args.step_streams)))
+        handle.check(lib.lbsim_profile_begin(handle.h, 4 * args.steps + 8))
         t0 = time.perf_counter()
         for _ in range(args.steps):
             one_step()
@@ -284,8 +332,7 @@ def main():
         from marllb_amd import trace
         tr = trace.builtin(args.trace)
     common = dict(device=dev, seed=args.seed, env_id_offset=shard.env_id_offset, autoreset=True,
-                  assign_policy=args.policy, trace=tr, dyn_mapping=args.dyn_mapping,
-                  step_streams=args.step_streams)
+                  assign_policy=args.policy, trace=tr, dyn_mapping=args.dyn_mapping)
     torch.manual_seed(args.seed)  # network init (random weights of the reference architecture)
     if args.workload == "rollout":
         env = VecLoadBalanceEnv(B, S, max_steps=10000, **common)
@@ -327,7 +374,7 @@ def main():
     from marllb_amd import policies
     if args.workload != "rollout":  # HIP events around each fused policy launch
         policies.profile_events = []
-    handle.check(lib.lbsim_profile_begin(handle.h, (4 * args.steps + 8) * max(1, args.step_streams)))
+    handle.check(lib.lbsim_profile_begin(handle.h, 4 * args.steps + 8))
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_step()
@@ -351,21 +398,18 @@ def main():
         rate = tr.rate if tr is not None else ARRIVAL_RATE
         abytes = algorithmic_bytes(S, rate * STEP_INTERVAL)
         abytes[dyn] = abytes.pop("dynamics_kernel")
-        # with step_streams > 1 each launch covers one env range (whole 64-env blocks)
-        parts = min(max(args.step_streams, 1), max(1, (B + 63) // 64))
-        launch_envs = B / parts
         per_kernel = {}
         for k in names:
-            ab_k = abytes[k] * launch_envs
+            ab_k = abytes[k] * B
             ach = ab_k / (avg[k] * 1e-3) / 1e9
             per_kernel[k] = {"avg_launch_ms": avg[k], "algorithmic_bytes_per_launch": ab_k,
                              "achieved_GBps": ach, "frac": ach / HBM_PEAK_GBS}
         dom = max(avg, key=avg.get)
-        ab = abytes[dom] * launch_envs
+        ab = abytes[dom] * B
         achieved = ab / (avg[dom] * 1e-3) / 1e9
         traffic = None
         tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if parts == 1 and os.path.exists(tfile):  # PMC passes were per whole-batch launch
+        if os.path.exists(tfile):
             t = json.load(open(tfile))
             if t.get("batch") == B and t.get("servers") == S and dom in t.get("bytes_per_launch", {}):
                 traffic = t["bytes_per_launch"][dom]
@@ -385,8 +429,7 @@ def main():
                        "assign_policy": args.policy,
                        "envs_per_gpu": B, "servers": S, "global_batch": world * B,
                        "step_interval_s": 0.25, "autoreset": True,
-                       "parallelism": f"env-shard x{world}", "dyn_mapping": args.dyn_mapping,
-                       "step_streams": parts},
+                       "parallelism": f"env-shard x{world}", "dyn_mapping": args.dyn_mapping},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "algorithmic_bytes_per_launch": ab,
@@ -418,6 +461,8 @@ def main():
         if world == 1 and args.workload == "rollout" and args.late_episode:
             out["late_episode"] = late_episode(args, env, handle, lib, one_step, rate, B, S,
                                                args.warmup + args.steps)
+        if world == 1 and args.workload == "rollout" and args.async_groups > 1:
+            out["async_groups"] = async_groups(args, dev, shard, B, S, common, args.async_groups)
         if world == 1 and not args.no_cpu_baseline and args.workload == "rollout":
             out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
         print(json.dumps(out), flush=True)

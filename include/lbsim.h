@@ -116,12 +116,7 @@ typedef struct lbsim_config {
   int32_t queue_capacity;    /* Q: max flows in flight per server (1..64), default 32       */
   int32_t warmup_steps;      /* simulated steps run inside reset() with weights 1.0         */
   int32_t dyn_mapping;       /* lbsim_dyn_mapping: how envs map onto lanes (results identical) */
-  int32_t step_streams;      /* 0 / 1: lbsim_step(_ex) launches on the caller's stream; 2..4:  */
-                             /* the batch runs as that many env ranges on internal streams      */
-                             /* forked from and joined back to the caller's stream (one range's */
-                             /* latency-bound dynamics overlaps another's observe; results      */
-                             /* identical -- envs are independent)                              */
-  int32_t reserved[6];
+  int32_t reserved[7];
 } lbsim_config_t;
 
 typedef struct lbsim lbsim_t; /* opaque handle */

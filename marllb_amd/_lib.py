@@ -53,8 +53,7 @@ class LbsimConfig(ctypes.Structure):
         ("queue_capacity", ctypes.c_int32),
         ("warmup_steps", ctypes.c_int32),
         ("dyn_mapping", ctypes.c_int32),
-        ("step_streams", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 6),
+        ("reserved", ctypes.c_int32 * 7),
     ]
 
 

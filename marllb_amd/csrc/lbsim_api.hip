@@ -29,8 +29,6 @@ struct Profiler {
   size_t used = 0;
 };
 
-constexpr int kMaxStepStreams = 4;
-
 struct lbsim {
   lbsim_config_t cfg;
   Profiler prof;
@@ -41,12 +39,6 @@ struct lbsim {
   SimParams prm;
   std::vector<void*> allocs;
   void* trace_buf = nullptr;  // gap_us[rows] then work[rows]
-  // step_streams > 1: env ranges [pb[i], pb[i + 1]) stepped on pst[i]; pev[i] joins range i back
-  // to the caller's stream, pev[kMaxStepStreams] forks
-  int parts = 1;
-  int pb[kMaxStepStreams + 1] = {};
-  hipStream_t pst[kMaxStepStreams] = {};
-  hipEvent_t pev[kMaxStepStreams + 1] = {};
   bool initialised;  // a full reset has been issued
   std::string err;
 };
@@ -127,8 +119,6 @@ int validate(const lbsim_config_t* c, char* msg, size_t n) {
   if (c->queue_capacity < 1 || c->queue_capacity > 64)
     return bad("queue_capacity must be in [1, 64]");
   if (c->warmup_steps < 0 || c->warmup_steps > 100000) return bad("warmup_steps out of range");
-  if (c->step_streams < 0 || c->step_streams > kMaxStepStreams)
-    return bad("step_streams must be in [0, %d] (got %d)", kMaxStepStreams, c->step_streams);
   if (c->dyn_mapping < LBSIM_DYN_AUTO || c->dyn_mapping > LBSIM_DYN_SERVER_PER_LANE)
     return bad("unknown dyn_mapping %d", c->dyn_mapping);
   if (c->dyn_mapping == LBSIM_DYN_ENV_PER_LANE && c->num_servers > 16)
@@ -226,23 +216,6 @@ struct ProfScope {
       (void)hipEventRecord(h->prof.ev[h->prof.used + 1], s);
       h->prof.used += 2;
     }
-  }
-};
-
-// Restricts the launches in its scope to envs [b0, b1) of the handle: grids cover b1 - b0 envs,
-// kernels add prm.b0 to their env index and stop at prm.B = b1.
-struct EnvRange {
-  lbsim_t* h;
-  int B0, pB, pb0;
-  EnvRange(lbsim_t* h_, int b0, int b1) : h(h_), B0(h_->B), pB(h_->prm.B), pb0(h_->prm.b0) {
-    h->B = b1 - b0;
-    h->prm.B = b1;
-    h->prm.b0 = b0;
-  }
-  ~EnvRange() {
-    h->B = B0;
-    h->prm.B = pB;
-    h->prm.b0 = pb0;
   }
 };
 
@@ -497,27 +470,6 @@ int lbsim_create(const lbsim_config_t* cfg, int device, lbsim_t** out) {
     hipLaunchKernelGGL(init_norm_std, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, nullptr,
                        h->st.norm_std, n);
   }
-  // step_streams: env ranges of whole 64-env blocks (at most B ranges), one internal stream each
-  const int parts = std::min(std::max(cfg->step_streams, 1), std::max(1, (h->B + 63) / 64));
-  h->parts = parts;
-  for (int i = 0; i <= parts; ++i) {
-    const int64_t blocks = (h->B + 63) / 64;
-    h->pb[i] = i == parts ? h->B : (int)std::min<int64_t>(h->B, blocks * i / parts * 64);
-  }
-  if (parts > 1) {
-    for (int i = 0; i < parts; ++i)
-      if (hipStreamCreateWithFlags(&h->pst[i], hipStreamNonBlocking) != hipSuccess) {
-        h->pst[i] = nullptr;
-        lbsim_destroy(h);
-        return fail(nullptr, LBSIM_EDEVICE, "hipStreamCreate failed");
-      }
-    for (int i = 0; i <= kMaxStepStreams; ++i)
-      if (hipEventCreateWithFlags(&h->pev[i], hipEventDisableTiming) != hipSuccess) {
-        h->pev[i] = nullptr;
-        lbsim_destroy(h);
-        return fail(nullptr, LBSIM_EDEVICE, "hipEventCreate failed");
-      }
-  }
   if (hipDeviceSynchronize() != hipSuccess) {
     lbsim_destroy(h);
     return fail(nullptr, LBSIM_EDEVICE, "device init failed");
@@ -533,10 +485,6 @@ int lbsim_destroy(lbsim_t* h) {
     for (void* p : h->allocs) (void)hipFree(p);
     if (h->trace_buf) (void)hipFree(h->trace_buf);
     for (hipEvent_t e : h->prof.ev) (void)hipEventDestroy(e);
-    for (hipStream_t s : h->pst)
-      if (s) (void)hipStreamDestroy(s);
-    for (hipEvent_t e : h->pev)
-      if (e) (void)hipEventDestroy(e);
   }
   delete h;
   return LBSIM_OK;
@@ -602,34 +550,11 @@ int lbsim_step_ex(lbsim_t* h, const void* action, int action_dtype,
   }
   DeviceGuard g(h->device);
   const hipStream_t s = (hipStream_t)stream;
+  int rc = launch_dynamics(h, action, action_dtype, out->assign_count, nullptr, kModeStep, s);
+  if (rc != LBSIM_OK) return rc;
   const ObsOutputs o{out->obs, out->reward, out->done, out->raw_obs, out->episode_length,
                      out->episode_return};
-  if (h->parts <= 1) {
-    int rc = launch_dynamics(h, action, action_dtype, out->assign_count, nullptr, kModeStep, s);
-    if (rc != LBSIM_OK) return rc;
-    return launch_observe(h, o, nullptr, kModeStep, s);
-  }
-  // fork: every range stream waits for the caller's stream (the actions), steps its env range
-  // (dynamics then observe; the kernels index the handle-wide buffers by global env), and the
-  // caller's stream waits for every range (join)
-  if (hipEventRecord(h->pev[kMaxStepStreams], s) != hipSuccess)
-    return fail(h, LBSIM_EDEVICE, "fork event failed");
-  int rc = LBSIM_OK;
-  for (int i = 0; i < h->parts && rc == LBSIM_OK; ++i) {
-    if (hipStreamWaitEvent(h->pst[i], h->pev[kMaxStepStreams], 0) != hipSuccess) {
-      rc = fail(h, LBSIM_EDEVICE, "stream wait failed");
-      break;
-    }
-    EnvRange r(h, h->pb[i], h->pb[i + 1]);
-    rc = launch_dynamics(h, action, action_dtype, out->assign_count, nullptr, kModeStep, h->pst[i]);
-    if (rc == LBSIM_OK) rc = launch_observe(h, o, nullptr, kModeStep, h->pst[i]);
-  }
-  // join every range launched so far, also on failure, so the caller's stream never runs ahead
-  for (int i = 0; i < h->parts; ++i) {
-    (void)hipEventRecord(h->pev[i], h->pst[i]);
-    (void)hipStreamWaitEvent(s, h->pev[i], 0);
-  }
-  return rc;
+  return launch_observe(h, o, nullptr, kModeStep, s);
 }
 
 int lbsim_episode_stats(lbsim_t* h, int32_t* length_out, double* return_out, void* stream) {

@@ -441,7 +441,7 @@ __global__ void __launch_bounds__(64)
   const int lane = (int)threadIdx.x;
   const int s = lane & (G - 1);
   const int gbase = lane & ~(G - 1);
-  const uint32_t b = (uint32_t)p.b0 + blockIdx.x * (uint32_t)(64 / G) + (uint32_t)(lane / G);
+  const uint32_t b = blockIdx.x * (uint32_t)(64 / G) + (uint32_t)(lane / G);
   if (b >= (uint32_t)p.B) return;  // whole groups leave together
   const int S = p.S, Q = p.Q;
   if (MODE == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;

@@ -94,7 +94,6 @@ struct SimParams {
   int32_t normalize;
   int32_t trace;          // 1: arrivals replay the trace (LBSIM_ARRIVAL_TRACE)
   uint32_t trace_rows;
-  int32_t b0;  // first env of this launch (env range [b0, B); lbsim_step with step_streams > 1)
 };
 
 constexpr uint32_t kTraceEnvStride = 7919u;        // SURVEY §8d C3 per-env offset
@@ -935,7 +934,7 @@ __global__ void __launch_bounds__(64 * kDynWaves<MAXS>)
     dynamics_kernel(DevState st, SimParams p, const void* action, int action_dtype,
                     int32_t* assign_out, const uint8_t* reset_mask) {
   constexpr int mode = MODE;
-  const uint32_t b = (uint32_t)p.b0 + blockIdx.x * (64u * kDynWaves<MAXS>) + threadIdx.x;
+  const uint32_t b = blockIdx.x * (64u * kDynWaves<MAXS>) + threadIdx.x;
   const int wv = (int)(threadIdx.x >> 6);
   __shared__ int2 qwin[kDynWaves<MAXS>][(MAXS * Win<MAXS>::WL + 1) * 64];  // + scratch slots
   __shared__ int32_t fields[kDynWaves<MAXS>][F_NUM * MAXS * 64];
@@ -1904,7 +1903,7 @@ template <int MAXS, int MODE>
 __global__ void __launch_bounds__(64 * kObsWavesPerEnv<MAXS>, 5)
     observe_kernel(DevState st, SimParams p, ObsOutputs out, const uint8_t* reset_mask) {
   constexpr int mode = MODE;
-  const size_t b = (size_t)p.b0 + blockIdx.x;
+  const size_t b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nthr = blockDim.x;
   if (mode == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
   extern __shared__ double obs_dyn[];

@@ -104,7 +104,7 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
                 server_rates: Optional[List[float]] = None, load: float = 0.8,
                 queue_capacity: int = 32, warmup_steps: int = 8, decay_factor: float = 0.9,
                 assign_policy: str = "sed", trace=None,
-                dyn_mapping: str = "auto", step_streams: int = 1) -> _lib.LbsimConfig:
+                dyn_mapping: str = "auto") -> _lib.LbsimConfig:
     """Build and validate an lbsim_config_t from reference-style kwargs.
 
     server_rates defaults to identical servers at utilisation `load`: mu = rate / (load * S).
@@ -112,9 +112,6 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
     replaces arrival_rate.  The arrays themselves go to the handle (Handle.set_trace).
     dyn_mapping: "auto" | "env" (one lane per env) | "server" (one lane per server): how the
     dynamics kernel lays envs onto lanes; results are identical, only speed differs.
-    step_streams: 1 steps the batch on the caller's stream; 2..4 step that many env ranges on
-    internal HIP streams forked from and joined back to it (one range's latency-bound dynamics
-    overlaps another's VALU-bound observe); results are identical.
     """
     if reward_metric not in _lib.METRICS:  # rewards.py:321-323
         raise ValueError(f"Unsupported metric: {reward_metric}. Supported: {_lib.METRICS}")
@@ -160,7 +157,6 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
     if dyn_mapping not in _lib.DYN_MAPPINGS:
         raise ValueError(f"Unknown dyn_mapping: {dyn_mapping}. Supported: {_lib.DYN_MAPPINGS}")
     cfg.dyn_mapping = _lib.DYN_MAPPINGS.index(dyn_mapping)
-    cfg.step_streams = int(step_streams)
     _lib.validate(cfg)
     return cfg
 
