@@ -1339,7 +1339,9 @@ __device__ __forceinline__ void observe_chunk_regs(const DevState& st, const Sim
 #pragma unroll
   for (int e = 1; e < 16; ++e) {
     const double wi = (double)w[e];
-    svw += in_acc(e) ? (double)vf[e] * wi : 0.0;
+    // a product of two floats is exact in double, so fma(v, w, svw) rounds exactly as numpy's
+    // product-then-add: one f64 op instead of two
+    svw = in_acc(e) ? fma((double)vf[e], wi, svw) : svw;
     sw += in_acc(e) ? wi : 0.0;
   }
   svw = svw + xor_f64_z<1>(svw, lane);
@@ -1364,7 +1366,7 @@ __device__ __forceinline__ void observe_chunk_regs(const DevState& st, const Sim
     for (int k = 0; k < ntail; ++k) {
       const float tv = tail_v[k], tw = tail_w[k];
       acc += tv;
-      svw += (double)tv * (double)tw;
+      svw = fma((double)tv, (double)tw, svw);
       sw += (double)tw;
     }
   }
