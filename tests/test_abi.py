@@ -70,3 +70,19 @@ def test_null_arguments_are_rejected():
     assert lib.lbsim_step(None, None, 0, None, None, None, None, None) == _lib.EINVAL
     assert lib.lbsim_reward(None, None, 0, None, None) == _lib.EINVAL
     assert lib.lbsim_destroy(None) == _lib.OK
+
+
+def test_integration_ctypes_stub_matches_config_size():
+    """The lbsim_config_t mirror shown to maintainers in INTEGRATION.md §2 has the library's size
+    (the stub would otherwise hand the library a short struct)."""
+    import ctypes
+    import os
+    import re
+    from marllb_amd import _lib
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    txt = open(os.path.join(root, "INTEGRATION.md")).read()
+    m = re.search(r"^class Cfg\(ctypes\.Structure\):.*?\]\n", txt, re.S | re.M)
+    assert m, "INTEGRATION.md lost its lbsim_config_t stub"
+    ns = {"ctypes": ctypes}
+    exec(m.group(0), ns)
+    assert ctypes.sizeof(ns["Cfg"]) == _lib.load().lbsim_config_size() == ctypes.sizeof(_lib.LbsimConfig)
