@@ -331,8 +331,9 @@ int lbsim_vose_sample(const float* prob, const uint32_t* alias, int64_t n, int S
 
 /*
  * Kernel timing: between lbsim_profile_begin and lbsim_profile_end every kernel launch of this
- * handle is bracketed by a pair of hipEvents recorded on the launch stream (at most max_launches
- * launches are timed).  lbsim_profile_end synchronises, and returns per kernel class
+ * handle is bracketed by hipEvents recorded on the launch stream (at most max_launches launches
+ * are timed; inside lbsim_step the event that closes the dynamics launch also opens the observe
+ * launch, so a step records three events, not four).  lbsim_profile_end synchronises, and returns per kernel class
  * {0: dynamics step, 1: observe step, 2: dynamics reset, 3: observe reset} the summed event time
  * in ms (ms_out[4]) and the number of timed launches (count_out[4]).  Used by bench.py.
  */

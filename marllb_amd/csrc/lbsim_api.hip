@@ -24,9 +24,15 @@ using namespace lbk;
 
 struct Profiler {
   bool on = false;
-  std::vector<hipEvent_t> ev;  // 2 per timed launch
+  std::vector<hipEvent_t> ev;  // at most 2 per timed launch
   std::vector<int> cls;        // kernel class per timed launch
-  size_t used = 0;
+  std::vector<int> beg, end;   // event indices bracketing each timed launch
+  size_t used = 0;             // events recorded
+  size_t cap = 0;              // events this profile may record (2 per requested launch)
+  // lbsim_step: the event that ends the dynamics launch also starts the observe launch (one
+  // event between the two kernels instead of two)
+  bool chain = false;
+  int chain_ev = -1;
 };
 
 struct lbsim {
@@ -206,16 +212,24 @@ struct ProfScope {
   bool rec = false;
   ProfScope(lbsim_t* h_, hipStream_t s_, int cls) : h(h_), s(s_) {
     Profiler& p = h->prof;
-    if (p.on && p.used + 2 <= p.ev.size()) {
-      rec = hipEventRecord(p.ev[p.used], s) == hipSuccess;
-      if (rec) p.cls.push_back(cls);
+    if (!p.on) return;
+    if (p.chain_ev >= 0 && p.used + 1 <= p.cap) {
+      p.beg.push_back(p.chain_ev);  // the previous launch's end event, on the same stream
+      rec = true;
+    } else if (p.used + 2 <= p.cap && hipEventRecord(p.ev[p.used], s) == hipSuccess) {
+      p.beg.push_back((int)p.used++);
+      rec = true;
     }
+    p.chain_ev = -1;
+    if (rec) p.cls.push_back(cls);
   }
   ~ProfScope() {
-    if (rec) {
-      (void)hipEventRecord(h->prof.ev[h->prof.used + 1], s);
-      h->prof.used += 2;
-    }
+    if (!rec) return;
+    Profiler& p = h->prof;
+    (void)hipEventRecord(p.ev[p.used], s);
+    p.end.push_back((int)p.used);
+    p.chain_ev = p.chain ? (int)p.used : -1;
+    ++p.used;
   }
 };
 
@@ -550,8 +564,13 @@ int lbsim_step_ex(lbsim_t* h, const void* action, int action_dtype,
   }
   DeviceGuard g(h->device);
   const hipStream_t s = (hipStream_t)stream;
+  h->prof.chain = true;  // dynamics then observe back to back on s: one event between them
   int rc = launch_dynamics(h, action, action_dtype, out->assign_count, nullptr, kModeStep, s);
-  if (rc != LBSIM_OK) return rc;
+  h->prof.chain = false;
+  if (rc != LBSIM_OK) {
+    h->prof.chain_ev = -1;
+    return rc;
+  }
   const ObsOutputs o{out->obs, out->reward, out->done, out->raw_obs, out->episode_length,
                      out->episode_return};
   return launch_observe(h, o, nullptr, kModeStep, s);
@@ -857,7 +876,12 @@ int lbsim_profile_begin(lbsim_t* h, int max_launches) {
     p.ev.push_back(e);
   }
   p.used = 0;
+  p.cap = need;
   p.cls.clear();
+  p.beg.clear();
+  p.end.clear();
+  p.chain = false;
+  p.chain_ev = -1;
   p.on = true;
   return LBSIM_OK;
 }
@@ -872,7 +896,7 @@ int lbsim_profile_end(lbsim_t* h, double* ms_out, int64_t* count_out) {
     return fail(h, LBSIM_EDEVICE, "hipEventSynchronize failed");
   for (size_t i = 0; i < p.cls.size(); ++i) {
     float t = 0.0f;
-    if (hipEventElapsedTime(&t, p.ev[2 * i], p.ev[2 * i + 1]) != hipSuccess)
+    if (hipEventElapsedTime(&t, p.ev[p.beg[i]], p.ev[p.end[i]]) != hipSuccess)
       return fail(h, LBSIM_EDEVICE, "hipEventElapsedTime failed");
     ms[p.cls[i]] += t;
     cnt[p.cls[i]] += 1;
@@ -880,6 +904,9 @@ int lbsim_profile_end(lbsim_t* h, double* ms_out, int64_t* count_out) {
   p.on = false;
   p.used = 0;
   p.cls.clear();
+  p.beg.clear();
+  p.end.clear();
+  p.chain_ev = -1;
   for (int i = 0; i < 4; ++i) {
     if (ms_out) ms_out[i] = ms[i];
     if (count_out) count_out[i] = cnt[i];

@@ -324,3 +324,36 @@ def test_reset_mask_validation():
     with pytest.raises(IndexError):
         strict.step(torch.full((8, 4), 3, dtype=torch.int64))
     strict.step(torch.full((8, 4), -3, dtype=torch.int64))  # python indexing: -n is valid
+
+
+def test_profiler_counts_and_times_every_launch():
+    """lbsim_profile_begin/end (bench.py's live kernel timing): every step's dynamics and observe
+    launches are timed (the step's middle event shared by both), resets are their own classes, and
+    the per-class sums are positive and below the wall time of the region."""
+    import ctypes
+    import time
+    from marllb_amd import _lib
+    from marllb_amd.env import VecLoadBalanceEnv
+    env = VecLoadBalanceEnv(4096, 4, device="cuda:0", seed=3)
+    env.reset()
+    lib, h = _lib.load(), env.handle
+    h.check(lib.lbsim_profile_begin(h.h, 64))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(7):
+        env.step(torch.randint(0, 3, (4096, 4), device="cuda:0"))
+    env.reset()
+    torch.cuda.synchronize()
+    wall_ms = (time.perf_counter() - t0) * 1e3
+    ms = (ctypes.c_double * 4)()
+    cnt = (ctypes.c_int64 * 4)()
+    h.check(lib.lbsim_profile_end(h.h, ms, cnt))
+    assert list(cnt) == [7, 7, 1, 1]
+    assert all(m > 0 for m in ms) and sum(ms) < wall_ms
+    # capacity: with room for 3 launches only the first ones are timed, nothing overflows
+    h.check(lib.lbsim_profile_begin(h.h, 2))
+    for _ in range(3):
+        env.step(torch.randint(0, 3, (4096, 4), device="cuda:0"))
+    h.check(lib.lbsim_profile_end(h.h, ms, cnt))
+    assert cnt[0] + cnt[1] <= 3 and cnt[0] >= 1
+    env.close()
