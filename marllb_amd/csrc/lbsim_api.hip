@@ -323,6 +323,11 @@ void launch_dynamics_t(lbsim_t* h, const void* action, int dtype, int32_t* assig
     else if (fg == 32) launch_dyn_group_policy<32, MODE>(h, action, dtype, assign, mask, stream);
     else launch_dyn_group_policy<64, MODE>(h, action, dtype, assign, mask, stream);
   } else if (g && h->S <= 2) launch_dyn_group_policy<2, MODE>(h, action, dtype, assign, mask, stream);
+  // small batches (configs[1]: 4096 x 4): 8 lanes per env -- twice the waves for SIMDs that would
+  // sit idle, the draw-ahead spread over 8 lanes: 4096 x 4 0.0908 -> 0.0894 ms, 8192 x 4 0.0962 ->
+  // 0.0947 (profiles/r02_round2b/ab_group_lanes_small.txt); slower from 16384 envs on
+  else if (g && h->S <= 4 && h->B <= 8192)
+    launch_dyn_group_policy<8, MODE>(h, action, dtype, assign, mask, stream);
   else if (h->S <= 4) launch_dyn_policy<4, MODE>(h, g, action, dtype, assign, mask, stream);
   else if (h->S <= 8) launch_dyn_policy<8, MODE>(h, g, action, dtype, assign, mask, stream);
   else if (h->S <= 16) launch_dyn_policy<16, MODE>(h, g, action, dtype, assign, mask, stream);

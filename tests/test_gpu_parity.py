@@ -206,6 +206,8 @@ CONFIGS = [
     # with the two-pass sort, after steps on its register-resident path)
     dict(B=32, S=4, kw={"arrival_rate": 12.0, "server_rates": [1.2, 1.4, 1.6, 1.8],
                         "step_interval": 10.0, "queue_capacity": 64}),
+    # above the small-batch threshold (B > 8192, S <= 4): the 4-lane groups of the headline shape
+    dict(B=8256, S=4, kw={}),
 ]
 
 
