@@ -145,21 +145,38 @@ def cpu_baseline(args, seconds: float):
     # box the affinity mask lists the whole machine, 256, but cpu.max grants 16; 256 threads on
     # 16 CPUs of quota run 4x slower than 16 threads: throttling, not the host's capability)
     threads = affinity if quota is None else max(1, min(affinity, int(quota + 0.999)))
-    nb = max(2048, 64 * threads)
-    cfg = make_config(nb, args.servers, seed=args.seed, env_id_offset=0)
-    ora = oracle.OracleEnv(cfg, threads=threads)
-    ora.reset()
     rng = np.random.default_rng(1)
-    acts = [rng.integers(0, 3, (nb, args.servers)).astype(np.int64) for _ in range(8)]
-    ora.step(acts[0])  # warm caches / thread pool
-    n, t0 = 0, time.perf_counter()
-    while True:
-        ora.step(acts[n % len(acts)])
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds and n >= 3:
-            break
-    ora.close()
+
+    def timed(nb, S, secs, trace=None):
+        """Oracle env-steps/s over nb envs (global ids 0..nb-1) x S servers for ~secs."""
+        kw = {"trace": trace} if trace is not None else {}
+        cfg = make_config(nb, S, seed=args.seed, env_id_offset=0, **kw)
+        ora = oracle.OracleEnv(cfg, threads=threads, trace=trace)
+        ora.reset()
+        acts = [rng.integers(0, 3, (nb, S)).astype(np.int64) for _ in range(8)]
+        ora.step(acts[0])  # warm caches / thread pool
+        n, t0 = 0, time.perf_counter()
+        while True:
+            ora.step(acts[n % len(acts)])
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= secs and n >= 3:
+                break
+        ora.close()
+        return nb * n / el, n, el
+
+    nb = max(2048, 64 * threads)
+    rate, n, el = timed(nb, args.servers, seconds)
+    # BASELINE.md §3's two CPU points: configs[1] 4096 x 4 (every env) and configs[2] 65536 x 8
+    # trace replay (a sample of its envs), each ~seconds/2
+    from marllb_amd import trace as lbtrace
+    points = []
+    for name, nb_p, S_p, tr in (("configs[1] 4096 x 4, random policy, all 4096 envs", 4096, 4, None),
+                                ("configs[2] 65536 x 8, rate_500 trace replay, envs 0-4095 of "
+                                 "65536 sampled", 4096, 8, lbtrace.builtin())):
+        r_p, n_p, el_p = timed(nb_p, S_p, seconds / 2, tr)
+        points.append({"config": name, "value": r_p, "unit": "env-steps/s", "cores": threads,
+                       "kind": "port", "steps": n_p, "seconds": el_p})
     # the reference's CPU plumbing step (configs[0], 1 x S, step_interval 0), one core
     pe = LoadBalanceEnv(num_servers=args.servers, step_interval=0.0, seed=0,
                         reference_plumbing=True)
@@ -170,7 +187,8 @@ def cpu_baseline(args, seconds: float):
         pe.step(pa[m % 64])
         m += 1
     pel = time.perf_counter() - t1
-    return {"value": nb * n / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
+    return {"value": rate, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "baseline_points": points,
             "cpu_model": model, "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
             "sample": f"{nb} of the {args.batch} envs (global ids 0-{nb - 1}), S={args.servers}, "
                       f"{n} random-policy steps, {el:.1f} s, oracle/lbsim_oracle.c "
@@ -386,7 +404,9 @@ def main():
     cnt = (ctypes.c_int64 * 4)()
     handle.check(lib.lbsim_profile_end(handle.h, ms, cnt))
     pol_events, policies.profile_events = policies.profile_events, None
-    elapsed = lbdist.max_over_ranks(t1 - t0, dev if backend == "nccl" else None)
+    cdev = dev if backend == "nccl" else None
+    elapsed = lbdist.max_over_ranks(t1 - t0, cdev)
+    per_rank = lbdist.gather_over_ranks(t1 - t0, cdev)
 
     if rank == 0:
         value = lbdist.throughput(shard, args.steps, elapsed)
@@ -418,6 +438,10 @@ def main():
             "n_gpus": dist.get_world_size() if world > 1 else 1,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            # every rank's timed-region wall time (value uses the max): imbalance shows here
+            "ranks": {"world_size": world, "backend": backend if world > 1 else None,
+                      "elapsed_s": per_rank, "elapsed_min_s": min(per_rank),
+                      "elapsed_max_s": elapsed},
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32/int32 (f64 reward)",
             "data": ("synthetic: Philox4x32-10 Poisson arrivals lambda=400/s, Exp(1) work, "
                      "mu=lambda/(0.8 S) per server, random discrete policy") if tr is None else

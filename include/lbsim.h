@@ -78,12 +78,14 @@ enum lbsim_assign_policy {
  * trace set with lbsim_set_trace (data/trace/poisson_for_loop/rate_N.csv). */
 enum lbsim_arrival_source { LBSIM_ARRIVAL_POISSON = 0, LBSIM_ARRIVAL_TRACE = 1 };
 
-/* Dynamics-kernel mapping; every choice produces the same bits.  AUTO picks SERVER_PER_LANE when
- * one lane per env would leave most of the GPU's SIMDs idle (small batches). */
+/* Dynamics-kernel mapping; every choice produces the same bits.  AUTO = SERVER_PER_LANE (faster
+ * than one lane per env at every measured shape). */
 enum lbsim_dyn_mapping {
   LBSIM_DYN_AUTO = 0,
-  LBSIM_DYN_ENV_PER_LANE = 1,    /* one lane = one env (large batches)                      */
-  LBSIM_DYN_SERVER_PER_LANE = 2  /* pow2(S) lanes = one env, one lane per server            */
+  LBSIM_DYN_ENV_PER_LANE = 1,    /* one lane = one env                                        */
+  LBSIM_DYN_SERVER_PER_LANE = 2  /* a group of G lanes = one env, one lane per server: G =     */
+                                 /* pow2 >= S, except S <= 4 on small batches (B*4/64 <= half */
+                                 /* the device's SIMDs), which get G = 8 (twice the waves)     */
 };
 
 /*
@@ -328,6 +330,23 @@ int lbsim_vose_tables(const float* weights, int64_t n, int S, float* prob_out,
 int lbsim_vose_sample(const float* prob, const uint32_t* alias, int64_t n, int S,
                       uint32_t* state_io, int64_t k, int32_t* idx_out, uint64_t* hist_out,
                       void* stream);
+
+/* ---- the VPP LB plugin's shared-memory view (src/vpp/lb/shm.h:14-91, marllb_amd/vpp_shm.py) ----
+ * lbsim_vpp_export: envs [env_begin, env_begin + n_envs) of the handle as the data plane's raw
+ * per-AS reservoirs (reservoir_as_t, shm.h:35-37; written by lbhash.h:116-135):
+ *   tv_out [n_envs, S, 2, 128, 2] f32 = per server {fct[128], flow_duration[128]} of (t, v)
+ *   pairs, t = the sample's completion time and v = the sample, both in seconds (slots past
+ *   min(count, 128) are (0, 0), VPP's zeroed shm); n_flow_on_out [n_envs, S] i32 (as_stat_t
+ *   n_flow_on, may be NULL); ts_out [n_envs] f32 frame time = simulated seconds since reset
+ *   (msg_out_t ts, may be NULL).
+ * lbsim_vpp_features: Shm_Manager.process_reservoir (src/lb/shm_proxy.py:518-543) of n raw
+ *   reservoirs tv[n, 128, 2] (t, v) f32, reservoir r at frame time ts[r / res_per_ts] ->
+ *   feats_out[n, 5] f64 {avg, 90, std, avg_decay, 90_decay} over all 128 bins, the decayed value
+ *   v * decay^(ts - t) (numpy order; everything but the f64 pow bit-identical). */
+int lbsim_vpp_export(lbsim_t* h, int64_t env_begin, int64_t n_envs, float* tv_out,
+                     int32_t* n_flow_on_out, float* ts_out, void* stream);
+int lbsim_vpp_features(const float* tv, const float* ts, int64_t res_per_ts, int64_t n,
+                       double decay, double* feats_out, void* stream);
 
 /*
  * Kernel timing: between lbsim_profile_begin and lbsim_profile_end every kernel launch of this

@@ -147,6 +147,9 @@ _SIGNATURES = {
                                          _P, _P, _P]),
     "lbsim_reservoir_features": (ctypes.c_int, [_P, _P, _P, ctypes.c_int64, ctypes.c_float, _P,
                                                 _P]),
+    "lbsim_vpp_export": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int64, _P, _P, _P, _P]),
+    "lbsim_vpp_features": (ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.c_int64, ctypes.c_double,
+                                          _P, _P]),
     "lbsim_profile_begin": (ctypes.c_int, [_P, ctypes.c_int]),
     "lbsim_profile_end": (ctypes.c_int, [_P, _P, _P]),
     "lbsim_state_size": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_size_t)]),

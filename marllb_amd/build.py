@@ -1,24 +1,34 @@
 """Build liblbsim.so in-tree for gfx950 (hipcc).  `python -m marllb_amd.build [--force]`.
 
-One translation unit (csrc/lbsim_api.hip includes the kernels).  -ffp-contract=off is part of
-the numerical contract: no FMA contraction, so integer state and every
-observation column are bit-reproducible against oracle/.
+Several translation units (csrc/*.hip, see csrc/lbsim_internal.h) compiled in parallel to objects
+under build/, then linked into marllb_amd/liblbsim.so.  -ffp-contract=off is part of the
+numerical contract: no FMA contraction, so integer state and every observation
+column are bit-reproducible against oracle/.
 """
 from __future__ import annotations
 
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = os.path.join(HERE, "csrc", "lbsim_api.hip")
-DEPS = [os.path.join(HERE, "csrc", f) for f in sorted(os.listdir(os.path.join(HERE, "csrc")))]
+CSRC = os.path.join(HERE, "csrc")
+OBJDIR = os.path.join(ROOT, "build", "lbsim")
+DEPS = [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC))]
 DEPS.append(os.path.join(ROOT, "include", "lbsim.h"))
 OUT = os.path.join(HERE, "liblbsim.so")
 ARCH = os.environ.get("LBSIM_OFFLOAD_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-Wall",
-         f"--offload-arch={ARCH}"]
+FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-Wall", f"--offload-arch={ARCH}"]
+# (source, extra defines, object name)
+UNITS = [
+    ("lbsim_api.hip", [], "api.o"),
+    ("lbsim_dyn.hip", ["-DLBSIM_DYN_MODE=0"], "dyn_step.o"),
+    ("lbsim_dyn.hip", ["-DLBSIM_DYN_MODE=1"], "dyn_reset.o"),
+    ("lbsim_obs.hip", [], "obs.o"),
+    ("lbsim_pol.hip", [], "pol.o"),
+]
 
 
 def hipcc() -> str:
@@ -35,12 +45,27 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(d) <= t for d in DEPS)
 
 
-def build_library(force: bool = False, verbose: bool = False) -> str:
+def _compile(unit, verbose: bool) -> str:
+    src, defs, obj = unit
+    out = os.path.join(OBJDIR, obj)
+    cmd = [hipcc(), *FLAGS, *defs, "-c", "-o", out + ".tmp", os.path.join(CSRC, src)]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+    return out
+
+
+def build_library(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
     if not force and up_to_date():
         return OUT
-    cmd = [hipcc(), *FLAGS, "-o", OUT + ".tmp", SRC]
+    os.makedirs(OBJDIR, exist_ok=True)
+    jobs = jobs or min(len(UNITS), os.cpu_count() or 1, 16)
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(lambda u: _compile(u, verbose), UNITS))
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs]
     if verbose:
-        print(" ".join(cmd))
+        print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(OUT + ".tmp", OUT)
     return OUT

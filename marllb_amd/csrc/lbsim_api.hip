@@ -15,10 +15,11 @@
 #include <vector>
 
 #include "../../include/lbsim.h"
-#include "lbsim_kernels.h"
-#include "lbsim_dyn_group.h"
+#include "lbsim_internal.h"
 #include "lbsim_fused.h"
 #include "lbsim_nets.h"
+#include "lbsim_stateless.h"
+#include "lbsim_vpp.h"
 
 using namespace lbk;
 
@@ -233,143 +234,23 @@ struct ProfScope {
   }
 };
 
-template <int MAXS, int MODE, int POLICY>
-void launch_dyn(lbsim_t* h, const void* action, int dtype, int32_t* assign, const uint8_t* mask,
-                hipStream_t stream) {
-  constexpr unsigned epb = 64u * kDynWaves<MAXS>;  // envs per workgroup (one per CU, kDynWaves)
-  const dim3 block(epb), grid((unsigned)((h->B + epb - 1) / epb));
-  if (h->prm.trace)
-    hipLaunchKernelGGL((dynamics_kernel<MAXS, MODE, POLICY, true>), grid, block, 0, stream, h->st,
-                       h->prm, action, dtype, assign, mask);
-  else
-    hipLaunchKernelGGL((dynamics_kernel<MAXS, MODE, POLICY, false>), grid, block, 0, stream,
-                       h->st, h->prm, action, dtype, assign, mask);
-}
-
-// server per lane: G = MAXS lanes per env, 64 / G envs per wave
-template <int MAXS, int MODE, int POLICY>
-void launch_dyn_group(lbsim_t* h, const void* action, int dtype, int32_t* assign,
-                      const uint8_t* mask, hipStream_t stream) {
-  constexpr int epw = 64 / MAXS;
-  const dim3 block(64), grid((unsigned)((h->B + epw - 1) / epw));
-  if (h->prm.trace)
-    hipLaunchKernelGGL((dynamics_group_kernel<MAXS, MODE, POLICY, true>), grid, block, 0, stream,
-                       h->st, h->prm, action, dtype, assign, mask);
-  else
-    hipLaunchKernelGGL((dynamics_group_kernel<MAXS, MODE, POLICY, false>), grid, block, 0, stream,
-                       h->st, h->prm, action, dtype, assign, mask);
-}
-
-template <int MAXS, int MODE, int POLICY>
-void launch_dyn_map(lbsim_t* h, bool group, const void* action, int dtype, int32_t* assign,
-                    const uint8_t* mask, hipStream_t stream) {
-  if (group) launch_dyn_group<MAXS, MODE, POLICY>(h, action, dtype, assign, mask, stream);
-  else launch_dyn<MAXS, MODE, POLICY>(h, action, dtype, assign, mask, stream);
-}
-
-template <int MAXS, int MODE>
-void launch_dyn_policy(lbsim_t* h, bool g, const void* action, int dtype, int32_t* assign,
-                       const uint8_t* mask, hipStream_t stream) {
-  switch (h->prm.policy) {
-    case LBSIM_POLICY_SED: launch_dyn_map<MAXS, MODE, 0>(h, g, action, dtype, assign, mask, stream); break;
-    case LBSIM_POLICY_SED2: launch_dyn_map<MAXS, MODE, 1>(h, g, action, dtype, assign, mask, stream); break;
-    case LBSIM_POLICY_LSQ: launch_dyn_map<MAXS, MODE, 2>(h, g, action, dtype, assign, mask, stream); break;
-    case LBSIM_POLICY_LSQ2: launch_dyn_map<MAXS, MODE, 3>(h, g, action, dtype, assign, mask, stream); break;
-    default: launch_dyn_map<MAXS, MODE, 4>(h, g, action, dtype, assign, mask, stream); break;
-  }
-}
-
-// Mapping choice (LBSIM_DYN_AUTO): one lane per server.  With arrivals drawn G at a
-// time (lbsim_dyn_group.h) it is faster than one lane per env at every measured shape
-// (profiles/r02_round2/mapping_sweep.jsonl): 65536 x 4 0.182 vs 0.214 ms, 131072 x 4 0.316 vs
-// 0.402, 65536 x 8 0.267 vs 0.320, configs[2] trace replay 0.317 vs 0.381, 16384 x 4 0.117 vs
-// 0.198.  The env-per-lane kernel stays selectable (LBSIM_DYN_ENV_PER_LANE).
-bool server_per_lane(const lbsim_t* h) {
-  return h->cfg.dyn_mapping != LBSIM_DYN_ENV_PER_LANE;
-}
-
-// S > 16: server-per-lane only (32 or 64 lanes per env; the env-per-lane kernel keeps its
-// per-server state in registers / LDS rows sized for at most 16 servers).
-template <int G, int MODE>
-void launch_dyn_group_policy(lbsim_t* h, const void* action, int dtype, int32_t* assign,
-                             const uint8_t* mask, hipStream_t stream) {
-  switch (h->prm.policy) {
-    case LBSIM_POLICY_SED: launch_dyn_group<G, MODE, 0>(h, action, dtype, assign, mask, stream); break;
-    case LBSIM_POLICY_SED2: launch_dyn_group<G, MODE, 1>(h, action, dtype, assign, mask, stream); break;
-    case LBSIM_POLICY_LSQ: launch_dyn_group<G, MODE, 2>(h, action, dtype, assign, mask, stream); break;
-    case LBSIM_POLICY_LSQ2: launch_dyn_group<G, MODE, 3>(h, action, dtype, assign, mask, stream); break;
-    default: launch_dyn_group<G, MODE, 4>(h, action, dtype, assign, mask, stream); break;
-  }
-}
-
-// Lanes per env of the server-per-lane mapping: LBSIM_DYN_GROUP_LANES = 8 | 16 | 32 | 64 widens
-// the group past pow2 >= S (experiments; the extra lanes draw arrivals ahead, hold no server).
-int forced_group_lanes() {
-  static const int g = [] {
-    const char* s = std::getenv("LBSIM_DYN_GROUP_LANES");
-    return s ? std::atoi(s) : 0;
-  }();
-  return g;
-}
-
-template <int MODE>
-void launch_dynamics_t(lbsim_t* h, const void* action, int dtype, int32_t* assign,
-                       const uint8_t* mask, hipStream_t stream) {
-  const bool g = server_per_lane(h);
-  const int fg = g ? forced_group_lanes() : 0;
-  if (fg >= h->S && (fg == 8 || fg == 16 || fg == 32 || fg == 64)) {
-    if (fg == 8) launch_dyn_group_policy<8, MODE>(h, action, dtype, assign, mask, stream);
-    else if (fg == 16) launch_dyn_group_policy<16, MODE>(h, action, dtype, assign, mask, stream);
-    else if (fg == 32) launch_dyn_group_policy<32, MODE>(h, action, dtype, assign, mask, stream);
-    else launch_dyn_group_policy<64, MODE>(h, action, dtype, assign, mask, stream);
-  } else if (g && h->S <= 2) launch_dyn_group_policy<2, MODE>(h, action, dtype, assign, mask, stream);
-  // small batches (configs[1]: 4096 x 4): 8 lanes per env -- twice the waves for SIMDs that would
-  // sit idle, the draw-ahead spread over 8 lanes: 4096 x 4 0.0908 -> 0.0894 ms, 8192 x 4 0.0962 ->
-  // 0.0947 (profiles/r02_round2b/ab_group_lanes_small.txt); slower from 16384 envs on
-  else if (g && h->S <= 4 && h->B <= 8192)
-    launch_dyn_group_policy<8, MODE>(h, action, dtype, assign, mask, stream);
-  else if (h->S <= 4) launch_dyn_policy<4, MODE>(h, g, action, dtype, assign, mask, stream);
-  else if (h->S <= 8) launch_dyn_policy<8, MODE>(h, g, action, dtype, assign, mask, stream);
-  else if (h->S <= 16) launch_dyn_policy<16, MODE>(h, g, action, dtype, assign, mask, stream);
-  else if (h->S <= 32) launch_dyn_group_policy<32, MODE>(h, action, dtype, assign, mask, stream);
-  else launch_dyn_group_policy<64, MODE>(h, action, dtype, assign, mask, stream);
+LaunchCtx ctx(const lbsim_t* h) {
+  return LaunchCtx{h->st, h->prm, h->B, h->S, h->simds, h->cfg.dyn_mapping};
 }
 
 int launch_dynamics(lbsim_t* h, const void* action, int dtype, int32_t* assign,
                     const uint8_t* mask, int mode, hipStream_t stream) {
   ProfScope ps(h, stream, mode == kModeStep ? 0 : 2);
-  if (mode == kModeStep) launch_dynamics_t<kModeStep>(h, action, dtype, assign, mask, stream);
-  else launch_dynamics_t<kModeReset>(h, action, dtype, assign, mask, stream);
+  if (mode == kModeStep) launch_dynamics_step(ctx(h), action, dtype, assign, mask, stream);
+  else launch_dynamics_reset(ctx(h), action, dtype, assign, mask, stream);
   return launch_check(h, "dynamics_kernel");
-}
-
-template <int MODE>
-void launch_observe_t(lbsim_t* h, const ObsOutputs& o, const uint8_t* mask, hipStream_t stream) {
-  // one wave per 4-server chunk, each with its own ObsScratch in dynamic LDS
-  const int nw = (h->S + kObsChunk - 1) / kObsChunk;
-  const dim3 grid((unsigned)h->B), block((unsigned)(64 * nw));
-  const size_t lds = (size_t)nw * sizeof(ObsScratch);
-  if (lds > 65536) {  // S > 32: 9-16 chunk waves
-    static const bool ok = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&observe_kernel<64, MODE>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, 16 * (int)sizeof(ObsScratch)) == hipSuccess;
-    (void)ok;
-  }
-  if (h->S <= 4)
-    hipLaunchKernelGGL((observe_kernel<4, MODE>), grid, block, lds, stream, h->st, h->prm, o, mask);
-  else if (h->S <= 8)
-    hipLaunchKernelGGL((observe_kernel<8, MODE>), grid, block, lds, stream, h->st, h->prm, o, mask);
-  else if (h->S <= 16)
-    hipLaunchKernelGGL((observe_kernel<16, MODE>), grid, block, lds, stream, h->st, h->prm, o, mask);
-  else
-    hipLaunchKernelGGL((observe_kernel<64, MODE>), grid, block, lds, stream, h->st, h->prm, o, mask);
 }
 
 int launch_observe(lbsim_t* h, const ObsOutputs& o, const uint8_t* mask, int mode,
                    hipStream_t stream) {
   ProfScope ps(h, stream, mode == kModeStep ? 1 : 3);
-  if (mode == kModeStep) launch_observe_t<kModeStep>(h, o, mask, stream);
-  else launch_observe_t<kModeReset>(h, o, mask, stream);
+  if (mode == kModeStep) launch_observe_step(ctx(h), o, mask, stream);
+  else launch_observe_reset(ctx(h), o, mask, stream);
   return launch_check(h, "observe_kernel");
 }
 
@@ -390,18 +271,6 @@ int fused_mt(int64_t) {
     return s ? std::atoi(s) : 0;
   }();
   return (forced == 2 || forced == 4) ? forced : 1;
-}
-
-template <typename Args>
-int launch_fused(void (*kern)(Args), int64_t B, int mt, size_t lds, hipStream_t s, Args a,
-                 unsigned threads = 256) {
-  const void* f = reinterpret_cast<const void*>(kern);
-  if (lds > 65536 &&
-      hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return LBSIM_EDEVICE;
-  void* args[] = {&a};
-  const dim3 grid((unsigned)((B + 16 * mt - 1) / (16 * mt))), block(threads);
-  return hipLaunchKernel(f, grid, block, args, lds, s) == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
 }
 
 }  // namespace
@@ -728,9 +597,7 @@ int lbsim_sac_actor_step(const lbsim_sac_actor_t* n, const float* state, float* 
   while (mt > 1 && lds_of(mt) > kFusedLdsMax) mt >>= 1;
   const size_t lds = lds_of(mt);
   const hipStream_t s = (hipStream_t)stream;
-  if (mt == 4) return launch_fused(&sac_actor_kernel<4, 128, 256>, B, 4, lds, s, a);
-  if (mt == 2) return launch_fused(&sac_actor_kernel<2, 128, 256>, B, 2, lds, s, a);
-  return launch_fused(&sac_actor_kernel<1, 128, 256>, B, 1, lds, s, a);
+  return launch_sac_actor(a, B, mt, lds, s);
 }
 
 int lbsim_qmix_policy_step(const lbsim_qmix_policy_t* n, const float* obs, float* hidden,
@@ -816,15 +683,13 @@ int lbsim_qmix_policy_step(const lbsim_qmix_policy_t* n, const float* obs, float
     if (form == 2 && A == 4) {  // two waves per agent: 8-wave workgroups
       const size_t lds = ((size_t)4 * 16 * a.lda + 2 * (size_t)A * 16 * 16 + 16 * (size_t)A) * 4;
       if (a.ld > 4 * a.lda || lds > kFusedLdsMax) return LBSIM_ENOTSUP;
-      return launch_fused(&qmix_agent_pair_kernel<64, 128>, B, 1, lds, s, a, 512);
+      return launch_qmix_policy(a, B, 2, 1, lds, s);
     }
     const size_t lds = ((size_t)4 * 16 * a.lda + (size_t)A * 16 * 16 + 16 * (size_t)A) * 4;
     if (a.ld > 4 * a.lda || lds > kFusedLdsMax) return LBSIM_ENOTSUP;
-    return launch_fused(&qmix_agent_wave_kernel<64, 128>, B, 1, lds, s, a);
+    return launch_qmix_policy(a, B, 1, 1, lds, s);
   }
-  if (mt == 4) return launch_fused(&qmix_policy_kernel<4, 64, 128>, B, 4, lds_of(4), s, a);
-  if (mt == 2) return launch_fused(&qmix_policy_kernel<2, 64, 128>, B, 2, lds_of(2), s, a);
-  return launch_fused(&qmix_policy_kernel<1, 64, 128>, B, 1, lds_of(1), s, a);
+  return launch_qmix_policy(a, B, 0, mt, lds_of(mt), s);
 }
 
 int lbsim_alias_tables(const float* weights, int64_t n, int S, float* odd_out, int32_t* alias_out,
@@ -867,6 +732,32 @@ int lbsim_reservoir_features(const float* values, const uint32_t* ts_ms, const u
   const float c = (float)(std::log2((double)decay_factor) / 1000.0);
   hipLaunchKernelGGL(features_kernel, dim3((unsigned)((n + 3) / 4)), dim3(64), 0,
                      (hipStream_t)stream, values, ts_ms, counts, n, c, feats_out);
+  return hipGetLastError() == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
+}
+
+int lbsim_vpp_export(lbsim_t* h, int64_t env_begin, int64_t n_envs, float* tv_out,
+                     int32_t* n_flow_on_out, float* ts_out, void* stream) {
+  if (h == nullptr) return LBSIM_EINVAL;
+  if (env_begin < 0 || n_envs < 0 || env_begin + n_envs > h->B)
+    return fail(h, LBSIM_EINVAL, "envs [%lld, %lld) outside [0, %d)", (long long)env_begin,
+                (long long)(env_begin + n_envs), h->B);
+  if (!h->initialised) return fail(h, LBSIM_EINVAL, "call lbsim_reset before lbsim_vpp_export");
+  if (n_envs == 0) return LBSIM_OK;
+  if (tv_out == nullptr) return fail(h, LBSIM_EINVAL, "tv_out is NULL");
+  DeviceGuard g(h->device);
+  hipLaunchKernelGGL(vpp_export_kernel, dim3((unsigned)(n_envs * h->S)), dim3(64), 0,
+                     (hipStream_t)stream, h->st, h->prm, env_begin, n_envs,
+                     reinterpret_cast<float2*>(tv_out), n_flow_on_out, ts_out);
+  return launch_check(h, "vpp_export_kernel");
+}
+
+int lbsim_vpp_features(const float* tv, const float* ts, int64_t res_per_ts, int64_t n,
+                       double decay, double* feats_out, void* stream) {
+  if (n < 0 || res_per_ts < 1 || !(decay > 0.0) || !(decay < 1.0)) return LBSIM_EINVAL;
+  if (n == 0) return LBSIM_OK;
+  if (!tv || !ts || !feats_out || n > 0x7FFFFFFF) return LBSIM_EINVAL;
+  hipLaunchKernelGGL(vpp_features_kernel, dim3((unsigned)n), dim3(64), 0, (hipStream_t)stream,
+                     reinterpret_cast<const float2*>(tv), ts, res_per_ts, n, decay, feats_out);
   return hipGetLastError() == hipSuccess ? LBSIM_OK : LBSIM_EDEVICE;
 }
 

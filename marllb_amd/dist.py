@@ -44,6 +44,20 @@ def max_over_ranks(x: float, device=None) -> float:
     return float(t.item())
 
 
+def gather_over_ranks(x: float, device=None) -> list:
+    """Every rank's value of a per-rank scalar, in rank order (the bench reports the per-rank
+    elapsed times beside their max, so an imbalanced rank shows in the line)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [float(x)]
+    n = dist.get_world_size()
+    t = torch.zeros(n, dtype=torch.float64, device=device)
+    t[dist.get_rank()] = float(x)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)  # one small collective, no all_gather list plumbing
+    return [float(v) for v in t.tolist()]
+
+
 def throughput(shard: Shard, steps: int, elapsed_max: float) -> float:
     """Whole-job env-steps/s: every rank's envs x steps over the slowest rank's time."""
     return shard.global_envs * steps / elapsed_max

@@ -225,8 +225,20 @@ class VecLoadBalanceEnv:
 
     def __init__(self, num_envs: int, num_servers: int = 4, *, device=None,
                  autoreset: bool = True, keep_terminal_obs: bool = False,
-                 strict_actions: bool = False, **kwargs):
+                 strict_actions: bool = False, feature_mode: str = "problem01", **kwargs):
         torch = _torch()
+        # feature_mode "upstream": columns 1-10 follow the live agent's process_reservoir
+        # (src/lb/shm_proxy.py:518-543: value-decayed mean / p90 over all 128 raw bins, f64) on the
+        # simulator's reservoirs seen the VPP way (lbsim_vpp_export + lbsim_vpp_features), and the
+        # reward is computed on those rows (lbsim_reward); default: problem-01's features
+        if feature_mode not in ("problem01", "upstream"):
+            raise ValueError(f"Unknown feature_mode: {feature_mode}")
+        if feature_mode == "upstream" and kwargs.get("normalize_obs"):
+            raise ValueError("feature_mode='upstream' does not combine with normalize_obs")
+        self.feature_mode = feature_mode
+        self._up_buf = None
+        self._up_decay = float(kwargs.get("decay_factor", 0.9))  # RES_DECAY, a Python float
+        self._up_ret = None  # episode returns of the upstream reward
         self.device_index = _device_index(device)
         self.device = torch.device("cuda", self.device_index)
         self.cfg = make_config(num_envs, num_servers, **kwargs)
@@ -287,6 +299,31 @@ class VecLoadBalanceEnv:
                              f"got {m.numel()}")
         return m.reshape(-1).to(self.device).to(torch.uint8).contiguous()
 
+    def _upstream(self, obs, reward=None, rows=None):
+        """Overwrite obs[:, :, 1:] (and reward) with the upstream features of the current state;
+        rows (bool [B]): only those envs."""
+        torch = _torch()
+        B, S = self.num_envs, self.num_servers
+        if self._up_buf is None:
+            self._up_buf = (torch.empty((B, S, 2, 128, 2), dtype=torch.float32, device=self.device),
+                            torch.empty(B, dtype=torch.float32, device=self.device),
+                            torch.empty((B * S * 2, 5), dtype=torch.float64, device=self.device))
+        tv, ts, feats = self._up_buf
+        lib, h, st = self.handle.lib, self.handle.h, self._stream()
+        self.handle.check(lib.lbsim_vpp_export(h, 0, B, tv.data_ptr(), None, ts.data_ptr(), st))
+        _lib.check(lib.lbsim_vpp_features(tv.data_ptr(), ts.data_ptr(), 2 * S, 2 * B * S,
+                                          self._up_decay,
+                                          feats.data_ptr(), st))
+        f = feats.view(B, S, 10).to(torch.float32)
+        if rows is None:
+            obs[:, :, 1:] = f
+        else:
+            obs[:, :, 1:] = torch.where(rows.view(B, 1, 1), f, obs[:, :, 1:])
+        if reward is not None:
+            _lib.check(lib.lbsim_reward(ctypes.byref(self.cfg), obs.data_ptr(), B,
+                                        reward.data_ptr(), st))
+        return obs
+
     # -- API
     def reset(self, mask=None):
         """Reset all envs (mask None) or those with mask[b] true; returns obs for all envs.
@@ -301,6 +338,9 @@ class VecLoadBalanceEnv:
                                                           self._stream()))
             self._reset_done = True
             self._step_bound = 0
+            if self.feature_mode == "upstream":
+                self._upstream(obs)
+                self._up_ret = None
             self._last_obs = obs
             return obs
         if not self._reset_done:
@@ -309,6 +349,10 @@ class VecLoadBalanceEnv:
         obs = self._last_obs.clone()
         self.handle.check(self.handle.lib.lbsim_reset(self.handle.h, m.data_ptr(),
                                                       obs.data_ptr(), self._stream()))
+        if self.feature_mode == "upstream":
+            self._upstream(obs, rows=m.bool())
+            if self._up_ret is not None:
+                self._up_ret.masked_fill_(m.bool(), 0.0)
         self._last_obs = obs
         return obs
 
@@ -337,6 +381,16 @@ class VecLoadBalanceEnv:
         out.episode_return = ep_ret.data_ptr()
         self.handle.check(self.handle.lib.lbsim_step_ex(self.handle.h, a.data_ptr(), dt,
                                                         ctypes.byref(out), self._stream()))
+        if self.feature_mode == "upstream":
+            self._upstream(obs, reward)
+            if raw is not None:
+                raw.copy_(obs)
+            if self._up_ret is None:
+                self._up_ret = torch.zeros(B, dtype=torch.float64, device=self.device)
+            self._up_ret += reward.to(torch.float64)
+            ep_ret = self._up_ret.clone()
+            if self.autoreset:  # done envs start a new episode inside this step
+                self._up_ret.masked_fill_(done, 0.0)
         info: Dict[str, Any] = {"episode_length": ep_len, "episode_return": ep_ret}
         if assign is not None:
             info["assign_counts"] = assign
@@ -349,6 +403,8 @@ class VecLoadBalanceEnv:
             # envs with done == 0 are untouched by the masked reset (no host sync needed)
             self.handle.check(self.handle.lib.lbsim_reset(self.handle.h, done.data_ptr(),
                                                           obs.data_ptr(), self._stream()))
+            if self.feature_mode == "upstream":
+                self._upstream(obs, rows=done)
         self._last_obs = obs
         return obs, reward, done, info
 
@@ -515,8 +571,6 @@ class LoadBalanceEnv:
             self._last_raw = obs
             return self._plumb.normalize(obs) if self.normalize_obs else obs
         if self.use_shm and self.shm is not None:  # env.py:197-205
-            # the simulator is reset too, so a later step without a new frame can fall back to it
-            self._vec.reset()
             try:
                 obs_dict = self.shm.read_observation()
             except Exception as e:
@@ -524,6 +578,9 @@ class LoadBalanceEnv:
                 print(f"Warning: Failed to read from SHM: {e}")
             if obs_dict is not None:
                 self.last_observation = obs_dict
+                # the simulator starts a fresh episode lazily, at the first step that falls back
+                # to it (_sim_step), so it is reset once per episode either way
+                self._vec._reset_done = False
                 return self._shm_obs(obs_dict)
             print("Warning: Failed to read from SHM: no observation published")
         return self._sim_reset()

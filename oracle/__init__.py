@@ -63,6 +63,8 @@ def load() -> ctypes.CDLL:
         "oracle_algr_slot": (ctypes.c_long, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                              ctypes.c_uint32, _P]),
         "oracle_algr_slot_r32": (ctypes.c_long, [ctypes.c_uint32, ctypes.c_uint32]),
+        "oracle_vpp_features": (None, [_P, _P, ctypes.c_long, ctypes.c_long, ctypes.c_double,
+                                       _P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -75,6 +77,16 @@ def load() -> ctypes.CDLL:
 def ptr(a: np.ndarray) -> int:
     assert a.flags["C_CONTIGUOUS"]
     return a.ctypes.data
+
+
+def vpp_features(tv, ts, res_per_ts: int = 128, decay: float = 0.9) -> np.ndarray:
+    """oracle_vpp_features: process_reservoir (src/lb/shm_proxy.py:518-543) of raw VPP reservoirs
+    tv [n, 128, 2] (t, v) f32 at frame times ts [n / res_per_ts] f32 -> [n, 5] f64."""
+    tv = np.ascontiguousarray(tv, np.float32).reshape(-1, 128, 2)
+    ts = np.ascontiguousarray(np.atleast_1d(ts), np.float32)
+    out = np.zeros((len(tv), 5), np.float64)
+    load().oracle_vpp_features(ptr(tv), ptr(ts), res_per_ts, len(tv), decay, ptr(out))
+    return out
 
 
 def gen_alias(weights):

@@ -873,3 +873,47 @@ long oracle_algr_slot(uint32_t count, uint32_t gid, uint32_t episode, uint32_t s
   const uint64_t j = (uint64_t)(prod >> 64);
   return j < (uint64_t)K ? (long)j : -1;
 }
+
+/* ------------------------------------------------------------------ VPP shm (upstream) features */
+/* Shm_Manager.process_reservoir (src/lb/shm_proxy.py:518-543) of n raw VPP reservoirs: tv[r][128]
+ * (t, v) f32 pairs (reservoir_as_t, src/vpp/lb/shm.h:35-37), frame time ts[r / res_per_ts] (the
+ * msg_out_t f32, a Python float).  Over all 128 bins in float64, numpy's order:
+ *   mean = pairwise(v) / 128; p90 = 'linear' percentile (virtual index 127 * 0.9, _lerp);
+ *   std = sqrt(pairwise((v - mean)^2) / 128); vd = v * pow(decay, ts - t); mean(vd), p90(vd). */
+static int cmp_f64(const void* a, const void* b) {
+  const double x = *(const double*)a, y = *(const double*)b;
+  return (x > y) - (x < y);
+}
+
+static double np_p90_128(double* s) {
+  qsort(s, 128, sizeof(double), cmp_f64);
+  const double vi = 127.0 * 0.9, gamma = vi - 114.0;
+  const double a = s[114], d = s[115] - a;
+  return a + d * gamma; /* gamma < 0.5: _lerp's add branch */
+}
+
+void oracle_vpp_features(const float* tv, const float* ts, long res_per_ts, long n, double decay,
+                         double* out) {
+  for (long r = 0; r < n; ++r) {
+    const float* p = tv + r * 256;
+    const double now = (double)ts[r / res_per_ts];
+    double v[128], vd[128], x2[128], s[128];
+    for (int i = 0; i < 128; ++i) {
+      v[i] = (double)p[2 * i + 1];
+      vd[i] = v[i] * pow(decay, now - (double)p[2 * i]);
+    }
+    const double mean = pw64(v, 128) / 128.0;
+    for (int i = 0; i < 128; ++i) {
+      const double x = v[i] - mean;
+      x2[i] = x * x;
+    }
+    double* o = out + r * 5;
+    o[0] = mean;
+    memcpy(s, v, sizeof(s));
+    o[1] = np_p90_128(s);
+    o[2] = sqrt(pw64(x2, 128) / 128.0);
+    o[3] = pw64(vd, 128) / 128.0;
+    memcpy(s, vd, sizeof(s));
+    o[4] = np_p90_128(s);
+  }
+}

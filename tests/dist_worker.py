@@ -71,13 +71,14 @@ def main():
     dist.gather_object(payload, gathered, dst=0)
     # the bench's timing reduction: slowest rank wins; whole-job rate over all ranks' envs
     slowest = lbdist.max_over_ranks(float(shard.rank + 1))
+    per_rank = lbdist.gather_over_ranks(float(shard.rank + 1))
     rate = lbdist.throughput(shard, args.steps, slowest)
     if shard.rank == 0:
         gathered.sort(key=lambda p: p[0])
         np.savez(args.out, offsets=np.array([p[0] for p in gathered]),
                  obs=np.concatenate([p[1] for p in gathered], axis=1),
                  rew=np.concatenate([p[2] for p in gathered], axis=1),
-                 slowest=slowest, rate=rate)
+                 slowest=slowest, rate=rate, per_rank=np.array(per_rank))
     dist.destroy_process_group()
 
 

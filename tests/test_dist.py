@@ -69,12 +69,14 @@ def test_shard_arithmetic():
     assert list(sh.global_ids())[:2] == [196608, 196609]
     assert lbdist.throughput(sh, 10, 2.0) == 8 * 65536 * 10 / 2.0
     assert lbdist.max_over_ranks(1.5) == 1.5  # no process group: identity
+    assert lbdist.gather_over_ranks(1.5) == [1.5]
 
 
 def test_two_rank_oracle_shards_equal_single_process(tmp_path, oracle_mod):
     res = run_ranks("oracle", 2, str(tmp_path / "r.npz"))
     assert list(res["offsets"]) == [0, B]
     assert float(res["slowest"]) == 2.0 and float(res["rate"]) == 2 * B * T / 2.0
+    assert list(res["per_rank"]) == [1.0, 2.0]  # gather_over_ranks: rank order
     obs, rew = single_process_reference(oracle_mod, 2)
     np.testing.assert_array_equal(res["obs"], obs)
     np.testing.assert_array_equal(res["rew"], rew)
@@ -104,3 +106,7 @@ def test_bench_self_launches_ranks():
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 4096 and out["value"] > 0
+    ranks = out["ranks"]
+    assert ranks["world_size"] == 2 and len(ranks["elapsed_s"]) == 2
+    assert ranks["elapsed_min_s"] <= ranks["elapsed_max_s"]
+    assert abs(ranks["elapsed_max_s"] - out["ms_per_step"] * 3 / 1e3) < 1e-9

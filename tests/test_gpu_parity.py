@@ -286,11 +286,13 @@ def test_simulator_bit_exact_vs_oracle(lib, oracle_mod, case, mapping):
     env.close()
 
 
-@pytest.mark.parametrize("lanes", ["8", "16"])
+@pytest.mark.parametrize("lanes", ["4", "8", "16"])
 def test_wider_groups_bit_exact(lanes):
-    """LBSIM_DYN_GROUP_LANES widens the server-per-lane groups past pow2 >= S (lanes that hold no
-    server only draw arrivals ahead): the simulator cases with S <= lanes stay bit-exact vs the
-    oracle.  The setting is read once per process, so the cases run in a child process."""
+    """LBSIM_DYN_GROUP_LANES forces the server-per-lane group width (lanes past S hold no server and
+    only draw arrivals ahead): the simulator cases with S <= lanes stay bit-exact vs the oracle.
+    lanes = 4 runs the headline 65536 x 4 kernel (4-lane groups) on every S <= 4 case -- every
+    policy, trace arrivals, NaN fallbacks -- which the default small-batch dispatch sends to 8-lane
+    groups.  The setting is read once per process, so the cases run in a child process."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
