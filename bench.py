@@ -34,19 +34,41 @@ STEP_INTERVAL = 0.25   # simulated seconds per step
 K = 128
 
 
-def algorithmic_bytes(S: int, flows_per_step: float):
+def algorithmic_bytes(S: int, slots_per_env: float, inflight_per_env: float):
     """Bytes each kernel must move per env-step with the state layout of DESIGN.md §4.
 
-    observe : read the 3 reservoir arrays (fct, dur, ts: 128 x 4 B each) + hc + res_count per
-              server, ep_step/ep_return read+write, obs 44 B/server, reward 4, done 1, ep outputs 12.
+    observe : read the 128 slot records (fct, dur, ts: 12 B each) + hc + res_count per server,
+              ep_step/ep_return read+write, obs 44 B/server, reward 4, done 1, ep outputs 12.
     dynamics: env header (8 x 4 B) and per-server hc/last_tc/res_count read+write, action 8 B and
-              assign count 4 B per server, and every flow's 8-B ring entry written once and read
-              once (flows_per_step = lambda * dt).  Reservoir inserts (data dependent, ~12 B per
-              accepted sample) are not counted: a lower bound.
+              assign count 4 B per server, the reservoir slots actually written (12 B each,
+              slots_per_env = lbsim_step_stats' popcount of the written-slot masks, measured on
+              the timed steps), and the flows carried into the next step (8-B ring entry written
+              at the end of the step and read at the start of the next: inflight_per_env).
+    fused   : one launch does both, so both (the observe reads of freshly written records are
+              algorithmic traffic even when L2 serves them).
     """
-    obs = S * (3 * K * 4 + 8 + 44) + 12 + 12 + 4 + 1 + 12
-    dyn = 2 * 32 + S * (2 * 12 + 8 + 4) + 16 * flows_per_step
-    return {"observe_kernel": obs, "dynamics_kernel": dyn}
+    obs = S * (K * 12 + 8 + 44) + 12 + 12 + 4 + 1 + 12
+    dyn = 2 * 32 + S * (2 * 12 + 8 + 4) + 12 * slots_per_env + 16 * inflight_per_env
+    return {"observe_kernel": obs, "dynamics_kernel": dyn, "fused_step_kernel": obs + dyn}
+
+
+def step_accounting(handle, lib, one_step, steps: int, replay=None):
+    """Reservoir slots written and flows in flight per step (lbsim_step_stats after each step).
+    replay = (state bytes, restore-generator callable): rewind to the timed region's start and
+    re-run exactly its steps; else `steps` more steps of the same trajectory."""
+    import torch
+    if replay is not None:
+        handle.load_state(replay[0])
+        replay[1]()
+    st = (ctypes.c_int64 * 2)()
+    slots = flows = 0
+    for _ in range(steps):
+        one_step()
+        torch.cuda.synchronize()
+        handle.check(lib.lbsim_step_stats(handle.h, st))
+        slots += st[0]
+        flows += st[1]
+    return slots / steps, flows / steps
 
 
 MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32, dense
@@ -270,14 +292,15 @@ def late_episode(args, env, handle, lib, one_step, rate, B, S, done_steps):
             one_step()
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
-        ms = (ctypes.c_double * 4)()
-        cnt = (ctypes.c_int64 * 4)()
-        handle.check(lib.lbsim_profile_end(handle.h, ms, cnt))
+        NC = 5
+        ms = (ctypes.c_double * NC)()
+        cnt = (ctypes.c_int64 * NC)()
+        handle.check(lib.lbsim_profile_end_ex(handle.h, ms, cnt, NC))
         step += args.steps
+        names = {0: "dynamics", 1: "observe", 4: "fused_step"}
         res.append({"episode_step": target, "value": B * args.steps / el, "unit": "env-steps/s",
                     "ms_per_step": el / args.steps * 1e3,
-                    "kernel_avg_ms": {"dynamics": ms[0] / max(1, cnt[0]),
-                                      "observe": ms[1] / max(1, cnt[1])}})
+                    "kernel_avg_ms": {names[i]: ms[i] / cnt[i] for i in names if cnt[i] > 0}})
     return res
 
 
@@ -390,6 +413,10 @@ def main():
         dist.barrier()
     lib = _lib.load()
     from marllb_amd import policies
+    replay = None
+    if args.workload == "rollout" and rank == 0:  # exact accounting replay of the timed steps
+        gstate = gen.get_state()
+        replay = (handle.state_bytes(), lambda: gen.set_state(gstate))
     if args.workload != "rollout":  # HIP events around each fused policy launch
         policies.profile_events = []
     handle.check(lib.lbsim_profile_begin(handle.h, 4 * args.steps + 8))
@@ -400,9 +427,10 @@ def main():
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
-    ms = (ctypes.c_double * 4)()
-    cnt = (ctypes.c_int64 * 4)()
-    handle.check(lib.lbsim_profile_end(handle.h, ms, cnt))
+    NC = _lib.PROFILE_CLASSES
+    ms = (ctypes.c_double * NC)()
+    cnt = (ctypes.c_int64 * NC)()
+    handle.check(lib.lbsim_profile_end_ex(handle.h, ms, cnt, NC))
     pol_events, policies.profile_events = policies.profile_events, None
     cdev = dev if backend == "nccl" else None
     elapsed = lbdist.max_over_ranks(t1 - t0, cdev)
@@ -410,16 +438,18 @@ def main():
 
     if rank == 0:
         value = lbdist.throughput(shard, args.steps, elapsed)
-        # the dynamics launch runs dynamics_group_kernel (one lane per server, the default) or
-        # dynamics_kernel (one lane per env, --dyn-mapping env); lbsim_profile times either
+        # a step is one fused_step_kernel launch (default) or dynamics_group_kernel (one lane per
+        # server) / dynamics_kernel (one lane per env, --dyn-mapping env) then observe_kernel;
+        # lbsim_profile times each class
         dyn = "dynamics_kernel" if args.dyn_mapping == "env" else "dynamics_group_kernel"
-        names = [dyn, "observe_kernel"]
-        avg = {names[i]: ms[i] / max(1, cnt[i]) for i in range(2)}
+        names = {0: dyn, 1: "observe_kernel", 4: "fused_step_kernel"}
+        avg = {names[i]: ms[i] / cnt[i] for i in names if cnt[i] > 0}
         rate = tr.rate if tr is not None else ARRIVAL_RATE
-        abytes = algorithmic_bytes(S, rate * STEP_INTERVAL)
+        slots, inflight = step_accounting(handle, lib, one_step, args.steps, replay)
+        abytes = algorithmic_bytes(S, slots / B, inflight / B)
         abytes[dyn] = abytes.pop("dynamics_kernel")
         per_kernel = {}
-        for k in names:
+        for k in avg:
             ab_k = abytes[k] * B
             ach = ab_k / (avg[k] * 1e-3) / 1e9
             per_kernel[k] = {"avg_launch_ms": avg[k], "algorithmic_bytes_per_launch": ab_k,
@@ -458,7 +488,12 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "algorithmic_bytes_per_launch": ab,
                          "avg_launch_ms": avg[dom],
-                         "kernel_avg_ms": avg, "kernels": per_kernel},
+                         "kernel_avg_ms": avg, "kernels": per_kernel,
+                         "accounting": {"reservoir_slots_written_per_env_step": slots / B,
+                                        "flows_in_flight_per_env": inflight / B,
+                                        "basis": "lbsim_step_stats after each step of an exact "
+                                                 "replay of the timed steps" if replay else
+                                                 "lbsim_step_stats over as many further steps"}},
         }
         if args.workload != "rollout":
             out["config"]["workload"] = {

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define LBSIM_ABI_VERSION 2
+#define LBSIM_ABI_VERSION 3
 #define LBSIM_MAX_SERVERS 64   /* S <= 64: BASELINE configs[4] read literally is 4 agents x 16 */
                                /* servers = 64 (S > 16: server-per-lane dynamics only)       */
 #define LBSIM_RESERVOIR_K 128  /* reservoir.py:31 capacity=128, reservoir.h:24               */
@@ -88,6 +88,12 @@ enum lbsim_dyn_mapping {
                                  /* the device's SIMDs), which get G = 8 (twice the waves)     */
 };
 
+/* How lbsim_step runs; every choice produces the same bits.  FUSED: one launch per step whose
+ * workgroups simulate their envs and then observe them; SPLIT: a dynamics launch
+ * and an observe launch.  AUTO = FUSED where it exists (server-per-lane groups of <= 16 lanes),
+ * else SPLIT.  The environment variable LBSIM_STEP_KERNEL=split|fused overrides AUTO. */
+enum lbsim_step_kernel { LBSIM_STEP_AUTO = 0, LBSIM_STEP_SPLIT = 1, LBSIM_STEP_FUSED = 2 };
+
 /*
  * POD configuration.  Mirrors the LoadBalanceEnv kwargs (env.py:71-87) plus the simulator knobs
  * the reference leaves implicit.  Fill with lbsim_config_default() and override.
@@ -118,7 +124,8 @@ typedef struct lbsim_config {
   int32_t queue_capacity;    /* Q: max flows in flight per server (1..64), default 32       */
   int32_t warmup_steps;      /* simulated steps run inside reset() with weights 1.0         */
   int32_t dyn_mapping;       /* lbsim_dyn_mapping: how envs map onto lanes (results identical) */
-  int32_t reserved[7];
+  int32_t step_kernel;       /* lbsim_step_kernel: one fused launch or two (results identical) */
+  int32_t reserved[6];
 } lbsim_config_t;
 
 typedef struct lbsim lbsim_t; /* opaque handle */
@@ -174,11 +181,23 @@ typedef struct lbsim_step_outputs {
   float* raw_obs;          /* [B, S, 11] f32 un-normalised obs (reward/active_servers basis)  */
   int32_t* episode_length; /* [B] i32 step count of the episode after this step (info['step'])*/
   double* episode_return;  /* [B] f64 return of the episode after this step                   */
+  /* problem-05 MultiAgentLoadBalanceEnv facade (multi_agent_env.py:152-188, 240-258), written by
+   * the same launch; num_agents * servers_per_agent must equal S when either is requested */
+  float* agent_obs;        /* [B, A, 4k + 7S] f32: agent a = flat[4ak, 4(a+1)k) ++ flat[4S:] of */
+                           /* the returned (S, 11) rows                                        */
+  float* state;            /* [B, 4S + 10] f32 get_state(): zeros, episode step / max_steps, A */
+  int32_t num_agents;      /* A                                                               */
+  int32_t servers_per_agent; /* k                                                             */
 } lbsim_step_outputs_t;
 
 /* lbsim_step with every output optional except obs, reward and done. */
 int lbsim_step_ex(lbsim_t* h, const void* action, int action_dtype,
                   const lbsim_step_outputs_t* out, void* stream);
+
+/* lbsim_reset with the step outputs that make sense after a reset: out->obs (required),
+ * out->raw_obs, out->agent_obs and out->state (rows of reset envs only). */
+int lbsim_reset_ex(lbsim_t* h, const uint8_t* env_mask, const lbsim_step_outputs_t* out,
+                   void* stream);
 
 /* sizeof(lbsim_config_t) / sizeof(lbsim_step_outputs_t) for binding-side layout checks. */
 size_t lbsim_config_size(void);
@@ -186,6 +205,12 @@ size_t lbsim_step_outputs_size(void);
 
 /* Per-env episode length (i32 [B]) and return (f64 [B]) into device buffers (info['episode']). */
 int lbsim_episode_stats(lbsim_t* h, int32_t* length_out, double* return_out, void* stream);
+
+/* Accounting of the last step (bench.py's algorithmic bytes; synchronises the device): HOST
+ * stats_out[0] = reservoir slots the last dynamics launch wrote (popcount of the written-slot
+ * masks: each a 12-B record store), stats_out[1] = flows in flight after it (sum of the queue
+ * counts: ring entries carried into the next step). */
+int lbsim_step_stats(lbsim_t* h, int64_t* stats_out);
 
 /* Stateless reward of given raw observations obs[n, S, 11] -> reward_out[n] (f32), using
  * cfg->reward_metric / reward_field and the active rule any(obs[s] > 0) (env.py:410-417,
@@ -354,10 +379,14 @@ int lbsim_vpp_features(const float* tv, const float* ts, int64_t res_per_ts, int
  * are timed; inside lbsim_step the event that closes the dynamics launch also opens the observe
  * launch, so a step records three events, not four).  lbsim_profile_end synchronises, and returns per kernel class
  * {0: dynamics step, 1: observe step, 2: dynamics reset, 3: observe reset} the summed event time
- * in ms (ms_out[4]) and the number of timed launches (count_out[4]).  Used by bench.py.
+ * in ms (ms_out[4]) and the number of timed launches (count_out[4]).  lbsim_profile_end_ex
+ * returns the first n_classes (<= LBSIM_PROFILE_CLASSES) classes, class 4 being the fused step
+ * kernel.  Used by bench.py.
  */
+#define LBSIM_PROFILE_CLASSES 5
 int lbsim_profile_begin(lbsim_t* h, int max_launches);
 int lbsim_profile_end(lbsim_t* h, double* ms_out, int64_t* count_out);
+int lbsim_profile_end_ex(lbsim_t* h, double* ms_out, int64_t* count_out, int n_classes);
 
 /* Snapshot: total bytes of the device state, and copies to/from a HOST buffer of that size.
  * Layout: DESIGN.md §4 (used by the parity tests to compare every state word with oracle/). */

@@ -22,6 +22,8 @@ OK, EINVAL, ENOMEM, EDEVICE, ESHAPE, ENOTSUP = 0, -1, -2, -3, -4, -5
 ACTION_DISCRETE, ACTION_CONTINUOUS = 0, 1
 ARRIVAL_POISSON, ARRIVAL_TRACE = 0, 1
 DYN_MAPPINGS = ("auto", "env", "server")  # lbsim_dyn_mapping
+STEP_KERNELS = ("auto", "split", "fused")  # lbsim_step_kernel
+PROFILE_CLASSES = 5  # dynamics step, observe step, dynamics reset, observe reset, fused step
 DTYPE_I32, DTYPE_I64, DTYPE_F32 = 0, 1, 2
 METRICS = ["jain", "variance", "std", "cv", "max", "min", "product", "range", "gini"]
 POLICIES = ["sed", "sed2", "lsq", "lsq2", "alias"]
@@ -53,7 +55,8 @@ class LbsimConfig(ctypes.Structure):
         ("queue_capacity", ctypes.c_int32),
         ("warmup_steps", ctypes.c_int32),
         ("dyn_mapping", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 7),
+        ("step_kernel", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 6),
     ]
 
 
@@ -68,6 +71,10 @@ class StepOutputs(ctypes.Structure):
         ("raw_obs", ctypes.c_void_p),
         ("episode_length", ctypes.c_void_p),
         ("episode_return", ctypes.c_void_p),
+        ("agent_obs", ctypes.c_void_p),
+        ("state", ctypes.c_void_p),
+        ("num_agents", ctypes.c_int32),
+        ("servers_per_agent", ctypes.c_int32),
     ]
 
 
@@ -119,9 +126,11 @@ _SIGNATURES = {
     "lbsim_reset": (ctypes.c_int, [_P, _P, _P, _P]),
     "lbsim_step": (ctypes.c_int, [_P, _P, ctypes.c_int, _P, _P, _P, _P, _P]),
     "lbsim_step_ex": (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.POINTER(StepOutputs), _P]),
+    "lbsim_reset_ex": (ctypes.c_int, [_P, _P, ctypes.POINTER(StepOutputs), _P]),
     "lbsim_config_size": (ctypes.c_size_t, []),
     "lbsim_step_outputs_size": (ctypes.c_size_t, []),
     "lbsim_episode_stats": (ctypes.c_int, [_P, _P, _P, _P]),
+    "lbsim_step_stats": (ctypes.c_int, [_P, _P]),
     "lbsim_reward": (ctypes.c_int, [ctypes.POINTER(LbsimConfig), _P, ctypes.c_int64, _P, _P]),
     "lbsim_gru_gates": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int64, ctypes.c_int, _P]),
     "lbsim_sac_head": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int, ctypes.c_float,
@@ -152,6 +161,7 @@ _SIGNATURES = {
                                           _P, _P]),
     "lbsim_profile_begin": (ctypes.c_int, [_P, ctypes.c_int]),
     "lbsim_profile_end": (ctypes.c_int, [_P, _P, _P]),
+    "lbsim_profile_end_ex": (ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
     "lbsim_state_size": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_size_t)]),
     "lbsim_get_state": (ctypes.c_int, [_P, _P, ctypes.c_size_t]),
     "lbsim_set_state": (ctypes.c_int, [_P, _P, ctypes.c_size_t]),

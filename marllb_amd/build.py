@@ -28,6 +28,7 @@ UNITS = [
     ("lbsim_dyn.hip", ["-DLBSIM_DYN_MODE=1"], "dyn_reset.o"),
     ("lbsim_obs.hip", [], "obs.o"),
     ("lbsim_pol.hip", [], "pol.o"),
+    ("lbsim_step.hip", [], "step.o"),
 ]
 
 

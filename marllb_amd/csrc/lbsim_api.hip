@@ -46,6 +46,7 @@ struct lbsim {
   SimParams prm;
   std::vector<void*> allocs;
   void* trace_buf = nullptr;  // gap_us[rows] then work[rows]
+  unsigned long long* stats_buf = nullptr;  // lbsim_step_stats sums (2 x u64)
   bool initialised;  // a full reset has been issued
   std::string err;
 };
@@ -128,6 +129,8 @@ int validate(const lbsim_config_t* c, char* msg, size_t n) {
   if (c->warmup_steps < 0 || c->warmup_steps > 100000) return bad("warmup_steps out of range");
   if (c->dyn_mapping < LBSIM_DYN_AUTO || c->dyn_mapping > LBSIM_DYN_SERVER_PER_LANE)
     return bad("unknown dyn_mapping %d", c->dyn_mapping);
+  if (c->step_kernel < LBSIM_STEP_AUTO || c->step_kernel > LBSIM_STEP_FUSED)
+    return bad("unknown step_kernel %d", c->step_kernel);
   if (c->dyn_mapping == LBSIM_DYN_ENV_PER_LANE && c->num_servers > 16)
     return bad("the env-per-lane dynamics mapping takes at most 16 servers (got %d)",
                c->num_servers);
@@ -192,6 +195,28 @@ __global__ void init_norm_std(double* p, size_t n) {
   if (i < n) p[i] = 1.0;  // env.py:153 obs_std = ones
 }
 
+// lbsim_step_stats: popcount of the written-slot masks and the sum of the queue counts, one
+// device-wide sum each (wave shuffles, then one vector atomic per wave).
+__global__ void __launch_bounds__(256)
+    step_stats_kernel(const uint32_t* chg, const uint32_t* hc, int64_t n_srv,
+                      unsigned long long* out) {
+  unsigned long long slots = 0, flows = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_srv;
+       i += (int64_t)gridDim.x * 256) {
+    const uint4 m = reinterpret_cast<const uint4*>(chg)[i];
+    slots += __popc(m.x) + __popc(m.y) + __popc(m.z) + __popc(m.w);
+    flows += hc[i] >> 16;
+  }
+  for (int d = 32; d > 0; d >>= 1) {
+    slots += __shfl_xor(slots, d, 64);
+    flows += __shfl_xor(flows, d, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(out, slots);
+    atomicAdd(out + 1, flows);
+  }
+}
+
 __global__ void copy_episode_stats(const int32_t* steps, const double* ret, int32_t* lo,
                                    double* ro, int B) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -244,6 +269,44 @@ int launch_dynamics(lbsim_t* h, const void* action, int dtype, int32_t* assign,
   if (mode == kModeStep) launch_dynamics_step(ctx(h), action, dtype, assign, mask, stream);
   else launch_dynamics_reset(ctx(h), action, dtype, assign, mask, stream);
   return launch_check(h, "dynamics_kernel");
+}
+
+bool facade_bad(const lbsim_t* h, const lbsim_step_outputs_t* out) {
+  if (out->agent_obs == nullptr && out->state == nullptr) return false;
+  return out->num_agents < 1 || out->servers_per_agent < 1 ||
+         (int64_t)out->num_agents * out->servers_per_agent != h->S;
+}
+
+ObsOutputs obs_outputs(const lbsim_step_outputs_t* out, bool reset) {
+  ObsOutputs o{};
+  o.obs = out->obs;
+  o.raw_obs = out->raw_obs;
+  if (!reset) {
+    o.reward = out->reward;
+    o.done = out->done;
+    o.ep_len = out->episode_length;
+    o.ep_ret = out->episode_return;
+  }
+  o.agent_obs = out->agent_obs;
+  o.state = out->state;
+  o.num_agents = out->num_agents;
+  o.servers_per_agent = out->servers_per_agent;
+  return o;
+}
+
+// The fused step for this handle: its config (LBSIM_STEP_KERNEL=split|fused overrides AUTO) and
+// a group width that has a fused form.
+bool use_fused_step(const lbsim_t* h) {
+  static const int env = [] {
+    const char* e = std::getenv("LBSIM_STEP_KERNEL");
+    if (e != nullptr && std::strcmp(e, "split") == 0) return LBSIM_STEP_SPLIT;
+    if (e != nullptr && std::strcmp(e, "fused") == 0) return LBSIM_STEP_FUSED;
+    return LBSIM_STEP_AUTO;
+  }();
+  const int k = h->cfg.step_kernel != LBSIM_STEP_AUTO ? h->cfg.step_kernel : env;
+  if (k == LBSIM_STEP_SPLIT) return false;
+  const int g = dyn_group_lanes(ctx(h));
+  return g >= 2 && g <= 16;
 }
 
 int launch_observe(lbsim_t* h, const ObsOutputs& o, const uint8_t* mask, int mode,
@@ -372,6 +435,7 @@ int lbsim_destroy(lbsim_t* h) {
     DeviceGuard g(h->device);
     for (void* p : h->allocs) (void)hipFree(p);
     if (h->trace_buf) (void)hipFree(h->trace_buf);
+    if (h->stats_buf) (void)hipFree(h->stats_buf);
     for (hipEvent_t e : h->prof.ev) (void)hipEventDestroy(e);
   }
   delete h;
@@ -394,15 +458,25 @@ int lbsim_seed(lbsim_t* h, uint64_t seed) {
 }
 
 int lbsim_reset(lbsim_t* h, const uint8_t* env_mask, float* obs_out, void* stream) {
+  lbsim_step_outputs_t o;
+  memset(&o, 0, sizeof(o));
+  o.obs = obs_out;
+  return lbsim_reset_ex(h, env_mask, &o, stream);
+}
+
+int lbsim_reset_ex(lbsim_t* h, const uint8_t* env_mask, const lbsim_step_outputs_t* out,
+                   void* stream) {
   if (h == nullptr) return LBSIM_EINVAL;
-  if (obs_out == nullptr) return fail(h, LBSIM_EINVAL, "obs_out is NULL");
+  if (out == nullptr || out->obs == nullptr) return fail(h, LBSIM_EINVAL, "obs_out is NULL");
+  if (facade_bad(h, out)) return fail(h, LBSIM_EINVAL, "agent_obs / state need num_agents * "
+                                                       "servers_per_agent == num_servers");
   if (h->prm.trace && h->prm.trace_rows == 0)
     return fail(h, LBSIM_EINVAL, "arrival_source TRACE: call lbsim_set_trace before lbsim_reset");
   DeviceGuard g(h->device);
   const hipStream_t s = (hipStream_t)stream;
   int rc = launch_dynamics(h, nullptr, 0, nullptr, env_mask, kModeReset, s);
   if (rc != LBSIM_OK) return rc;
-  const ObsOutputs o{obs_out, nullptr, nullptr, nullptr, nullptr, nullptr};
+  const ObsOutputs o = obs_outputs(out, true);
   rc = launch_observe(h, o, env_mask, kModeReset, s);
   if (rc != LBSIM_OK) return rc;
   if (env_mask == nullptr) h->initialised = true;
@@ -436,8 +510,18 @@ int lbsim_step_ex(lbsim_t* h, const void* action, int action_dtype,
   } else if (action_dtype != LBSIM_DTYPE_F32) {
     return fail(h, LBSIM_EINVAL, "continuous actions must be float32");
   }
+  if (facade_bad(h, out)) return fail(h, LBSIM_EINVAL, "agent_obs / state need num_agents * "
+                                                       "servers_per_agent == num_servers");
   DeviceGuard g(h->device);
   const hipStream_t s = (hipStream_t)stream;
+  const ObsOutputs o = obs_outputs(out, false);
+  if (use_fused_step(h)) {
+    ProfScope ps(h, s, 4);
+    const LaunchCtx L = ctx(h);
+    if (!launch_fused_step(L, dyn_group_lanes(L), action, action_dtype, out->assign_count, o, s))
+      return fail(h, LBSIM_EINVAL, "no fused step for this group width");
+    return launch_check(h, "fused_step_kernel");
+  }
   h->prof.chain = true;  // dynamics then observe back to back on s: one event between them
   int rc = launch_dynamics(h, action, action_dtype, out->assign_count, nullptr, kModeStep, s);
   h->prof.chain = false;
@@ -445,9 +529,28 @@ int lbsim_step_ex(lbsim_t* h, const void* action, int action_dtype,
     h->prof.chain_ev = -1;
     return rc;
   }
-  const ObsOutputs o{out->obs, out->reward, out->done, out->raw_obs, out->episode_length,
-                     out->episode_return};
   return launch_observe(h, o, nullptr, kModeStep, s);
+}
+
+int lbsim_step_stats(lbsim_t* h, int64_t* stats_out) {
+  if (h == nullptr || stats_out == nullptr) return LBSIM_EINVAL;
+  DeviceGuard g(h->device);
+  if (h->stats_buf == nullptr && hipMalloc(&h->stats_buf, 16) != hipSuccess) {
+    h->stats_buf = nullptr;
+    return fail(h, LBSIM_ENOMEM, "hipMalloc(16) failed");
+  }
+  const int64_t n = (int64_t)h->B * h->S;
+  unsigned long long host[2] = {0, 0};
+  if (hipDeviceSynchronize() != hipSuccess || hipMemset(h->stats_buf, 0, 16) != hipSuccess)
+    return fail(h, LBSIM_EDEVICE, "sync / memset failed");
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(step_stats_kernel, dim3((unsigned)blocks), dim3(256), 0, nullptr, h->st.chg,
+                     h->st.hc, n, h->stats_buf);
+  if (hipMemcpy(host, h->stats_buf, 16, hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(h, LBSIM_EDEVICE, "step_stats_kernel failed");
+  stats_out[0] = (int64_t)host[0];
+  stats_out[1] = (int64_t)host[1];
+  return LBSIM_OK;
 }
 
 int lbsim_episode_stats(lbsim_t* h, int32_t* length_out, double* return_out, void* stream) {
@@ -783,11 +886,15 @@ int lbsim_profile_begin(lbsim_t* h, int max_launches) {
 }
 
 int lbsim_profile_end(lbsim_t* h, double* ms_out, int64_t* count_out) {
-  if (h == nullptr) return LBSIM_EINVAL;
+  return lbsim_profile_end_ex(h, ms_out, count_out, 4);
+}
+
+int lbsim_profile_end_ex(lbsim_t* h, double* ms_out, int64_t* count_out, int n_classes) {
+  if (h == nullptr || n_classes < 0 || n_classes > LBSIM_PROFILE_CLASSES) return LBSIM_EINVAL;
   DeviceGuard g(h->device);
   Profiler& p = h->prof;
-  double ms[4] = {0, 0, 0, 0};
-  int64_t cnt[4] = {0, 0, 0, 0};
+  double ms[LBSIM_PROFILE_CLASSES] = {0, 0, 0, 0, 0};
+  int64_t cnt[LBSIM_PROFILE_CLASSES] = {0, 0, 0, 0, 0};
   if (p.used > 0 && hipEventSynchronize(p.ev[p.used - 1]) != hipSuccess)
     return fail(h, LBSIM_EDEVICE, "hipEventSynchronize failed");
   for (size_t i = 0; i < p.cls.size(); ++i) {
@@ -803,7 +910,7 @@ int lbsim_profile_end(lbsim_t* h, double* ms_out, int64_t* count_out) {
   p.beg.clear();
   p.end.clear();
   p.chain_ev = -1;
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < n_classes; ++i) {
     if (ms_out) ms_out[i] = ms[i];
     if (count_out) count_out[i] = cnt[i];
   }

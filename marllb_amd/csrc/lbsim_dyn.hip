@@ -41,25 +41,19 @@ void launch_dyn_group(const LaunchCtx& L, const void* action, int dtype, int32_t
 }
 
 template <int MAXS>
-void launch_dyn_policy(const LaunchCtx& L, bool group, const void* action, int dtype,
-                       int32_t* assign, const uint8_t* mask, hipStream_t s) {
+void launch_dyn_policy(const LaunchCtx& L, bool, const void* action, int dtype, int32_t* assign,
+                       const uint8_t* mask, hipStream_t s) {
   switch (L.prm.policy) {
-#define LBSIM_POL(P)                                                  \
-  if (group) launch_dyn_group<MAXS, P>(L, action, dtype, assign, mask, s); \
-  else launch_dyn<MAXS, P>(L, action, dtype, assign, mask, s);        \
-  break;
-    case LBSIM_POLICY_SED: LBSIM_POL(0)
-    case LBSIM_POLICY_SED2: LBSIM_POL(1)
-    case LBSIM_POLICY_LSQ: LBSIM_POL(2)
-    case LBSIM_POLICY_LSQ2: LBSIM_POL(3)
-    default: LBSIM_POL(4)
-#undef LBSIM_POL
+    case LBSIM_POLICY_SED: launch_dyn<MAXS, 0>(L, action, dtype, assign, mask, s); break;
+    case LBSIM_POLICY_SED2: launch_dyn<MAXS, 1>(L, action, dtype, assign, mask, s); break;
+    case LBSIM_POLICY_LSQ: launch_dyn<MAXS, 2>(L, action, dtype, assign, mask, s); break;
+    case LBSIM_POLICY_LSQ2: launch_dyn<MAXS, 3>(L, action, dtype, assign, mask, s); break;
+    default: launch_dyn<MAXS, 4>(L, action, dtype, assign, mask, s); break;
   }
 }
 
-// A group width chosen apart from MAXS: the small-batch 8-lane tier (S <= 4), a forced
-// LBSIM_DYN_GROUP_LANES width, and S > 16 (32 or 64 lanes per env, server-per-lane only: the
-// env-per-lane kernel keeps its per-server state in registers / LDS rows sized for <= 16 servers).
+// G lanes per env (dyn_group_lanes): 2, 4, 8, 16, and 32 / 64 for S > 16 (server-per-lane only:
+// the env-per-lane kernel keeps its per-server state in registers / LDS rows sized for <= 16).
 template <int G>
 void launch_dyn_group_policy(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
                              const uint8_t* mask, hipStream_t s) {
@@ -72,44 +66,27 @@ void launch_dyn_group_policy(const LaunchCtx& L, const void* action, int dtype, 
   }
 }
 
-// Lanes per env of the server-per-lane mapping: LBSIM_DYN_GROUP_LANES = 4 | 8 | 16 | 32 | 64
-// forces the group width (>= S; lanes past S hold no server and only draw arrivals ahead): tests
-// use 4 to run the headline 4-lane kernel on small batches, experiments the wider forms.
-int forced_group_lanes() {
-  static const int g = [] {
-    const char* s = std::getenv("LBSIM_DYN_GROUP_LANES");
-    return s ? std::atoi(s) : 0;
-  }();
-  return g;
-}
-
 // Mapping choice (LBSIM_DYN_AUTO): one lane per server.  With arrivals drawn G at a
 // time (lbsim_dyn_group.h) it is faster than one lane per env at every measured shape
 // (profiles/r02_round2/mapping_sweep.jsonl): 65536 x 4 0.182 vs 0.214 ms, 131072 x 4 0.316 vs
 // 0.402, 65536 x 8 0.267 vs 0.320, configs[2] trace replay 0.317 vs 0.381, 16384 x 4 0.117 vs
-// 0.198.  The env-per-lane kernel stays selectable (LBSIM_DYN_ENV_PER_LANE).
+// 0.198.  The env-per-lane kernel stays selectable (LBSIM_DYN_ENV_PER_LANE).  Group widths:
+// dyn_group_lanes (lbsim_internal.h).
 void launch_dynamics_t(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
                        const uint8_t* mask, hipStream_t stream) {
-  const bool g = L.dyn_mapping != LBSIM_DYN_ENV_PER_LANE;
-  const int fg = g ? forced_group_lanes() : 0;
-  if (fg >= L.S && (fg == 4 || fg == 8 || fg == 16 || fg == 32 || fg == 64)) {
-    if (fg == 4) launch_dyn_group_policy<4>(L, action, dtype, assign, mask, stream);
-    else if (fg == 8) launch_dyn_group_policy<8>(L, action, dtype, assign, mask, stream);
-    else if (fg == 16) launch_dyn_group_policy<16>(L, action, dtype, assign, mask, stream);
-    else if (fg == 32) launch_dyn_group_policy<32>(L, action, dtype, assign, mask, stream);
-    else launch_dyn_group_policy<64>(L, action, dtype, assign, mask, stream);
-  } else if (g && L.S <= 2) launch_dyn_group_policy<2>(L, action, dtype, assign, mask, stream);
-  // small batches (configs[1]: 4096 x 4): 8 lanes per env when 4-lane groups would give at most
-  // one wave per two SIMDs (B * 4 / 64 <= simds / 2: B <= 8192 on 256 CUs) -- twice the waves for
-  // SIMDs that would sit idle, the draw-ahead spread over 8 lanes: 4096 x 4 0.0908 -> 0.0894 ms,
-  // 8192 x 4 0.0962 -> 0.0947 (profiles/r02_round2b/ab_group_lanes_small.txt); slower from 16384
-  else if (g && L.S <= 4 && (int64_t)L.B * 4 / 64 <= L.simds / 2)
-    launch_dyn_group_policy<8>(L, action, dtype, assign, mask, stream);
-  else if (L.S <= 4) launch_dyn_policy<4>(L, g, action, dtype, assign, mask, stream);
-  else if (L.S <= 8) launch_dyn_policy<8>(L, g, action, dtype, assign, mask, stream);
-  else if (L.S <= 16) launch_dyn_policy<16>(L, g, action, dtype, assign, mask, stream);
-  else if (L.S <= 32) launch_dyn_group_policy<32>(L, action, dtype, assign, mask, stream);
-  else launch_dyn_group_policy<64>(L, action, dtype, assign, mask, stream);
+  switch (dyn_group_lanes(L)) {
+    case 0:  // one lane per env
+      if (L.S <= 4) launch_dyn_policy<4>(L, false, action, dtype, assign, mask, stream);
+      else if (L.S <= 8) launch_dyn_policy<8>(L, false, action, dtype, assign, mask, stream);
+      else launch_dyn_policy<16>(L, false, action, dtype, assign, mask, stream);
+      break;
+    case 2: launch_dyn_group_policy<2>(L, action, dtype, assign, mask, stream); break;
+    case 4: launch_dyn_group_policy<4>(L, action, dtype, assign, mask, stream); break;
+    case 8: launch_dyn_group_policy<8>(L, action, dtype, assign, mask, stream); break;
+    case 16: launch_dyn_group_policy<16>(L, action, dtype, assign, mask, stream); break;
+    case 32: launch_dyn_group_policy<32>(L, action, dtype, assign, mask, stream); break;
+    default: launch_dyn_group_policy<64>(L, action, dtype, assign, mask, stream); break;
+  }
 }
 
 }  // namespace

@@ -426,22 +426,34 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
   E.clock += 1u;
 }
 
+// LDS of one dynamics wave (dynamics_group_kernel, fused_step_kernel).
+template <int POLICY>
+struct DynGroupLds {
+  int2 win[kGroupWL * 64];                          // queue windows, [slot][lane]
+  int32_t atab[POLICY == kPolicyAlias ? 2 * 64 : 1];  // ALIAS tables, [word][lane]
+  int4 acache[64];                                  // draw-ahead arrival slots, [group][G]
+  uint32_t chgw[4 * 64];                            // written-slot masks, [word][lane]
+};
+
+// One step (or reset) of the 64 / G envs of wave `wave` (env b = wave * 64 / G + lane / G), lane s
+// of a group owning server s: state in, the event loop, state back to HBM.  Lanes of envs past B
+// (or outside the reset mask) return at once, whole groups together.
 template <int G, int MODE, int POLICY, bool TRACE>
-__global__ void __launch_bounds__(64)
-    dynamics_group_kernel(DevState st, SimParams p, const void* action, int action_dtype,
-                          int32_t* assign_out, const uint8_t* reset_mask) {
+__device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimParams& p,
+                                               const void* action, int action_dtype,
+                                               int32_t* assign_out, const uint8_t* reset_mask,
+                                               uint32_t wave, int lane, DynGroupLds<POLICY>& L) {
   static_assert(G == 2 || G == 4 || G == 8 || G == 16 || G == 32 || G == 64,
                 "group = a power of two lanes of the wave");
   constexpr int WL = kGroupWL;
   constexpr bool alias = POLICY == kPolicyAlias;
-  __shared__ int2 win[WL * 64];
-  __shared__ int32_t atab[alias ? 2 * 64 : 1];
-  __shared__ int4 acache[64];  // draw-ahead arrival slots, [group][G]
-  __shared__ uint32_t chgw[4 * 64];  // written-slot masks, [word][lane]
-  const int lane = (int)threadIdx.x;
+  int2* const win = L.win;
+  int32_t* const atab = L.atab;
+  int4* const acache = L.acache;
+  uint32_t* const chgw = L.chgw;
   const int s = lane & (G - 1);
   const int gbase = lane & ~(G - 1);
-  const uint32_t b = blockIdx.x * (uint32_t)(64 / G) + (uint32_t)(lane / G);
+  const uint32_t b = wave * (uint32_t)(64 / G) + (uint32_t)(lane / G);
   if (b >= (uint32_t)p.B) return;  // whole groups leave together
   const int S = p.S, Q = p.Q;
   if (MODE == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
@@ -553,6 +565,15 @@ __global__ void __launch_bounds__(64)
     st.next_u2[b] = E.u2;
     st.next_u3[b] = E.u3;
   }
+}
+
+template <int G, int MODE, int POLICY, bool TRACE>
+__global__ void __launch_bounds__(64)
+    dynamics_group_kernel(DevState st, SimParams p, const void* action, int action_dtype,
+                          int32_t* assign_out, const uint8_t* reset_mask) {
+  __shared__ DynGroupLds<POLICY> L;
+  dyn_group_wave<G, MODE, POLICY, TRACE>(st, p, action, action_dtype, assign_out, reset_mask,
+                                         blockIdx.x, (int)threadIdx.x, L);
 }
 
 }  // namespace lbk

@@ -11,6 +11,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "../../include/lbsim.h"
 #include "lbsim_kernels.h"
 
@@ -25,6 +27,29 @@ struct LaunchCtx {
   int dyn_mapping;  // lbsim_dyn_mapping
 };
 
+// Lanes per env of the server-per-lane dynamics (0: one lane per env, dyn_mapping ENV_PER_LANE).
+// LBSIM_DYN_GROUP_LANES = 4 | 8 | 16 | 32 | 64 forces the width (>= S; lanes past S hold no server
+// and only draw arrivals ahead): tests use 4 to run the headline 4-lane kernel on small batches,
+// experiments the wider forms.  Otherwise pow2 >= S, except small batches with S <= 4: 8 lanes
+// when 4-lane groups would give at most one wave per two SIMDs (B * 4 / 64 <= simds / 2: B <= 8192
+// on 256 CUs) -- twice the waves for SIMDs that would sit idle, the draw-ahead spread over 8
+// lanes: 4096 x 4 0.0908 -> 0.0894 ms, 8192 x 4 0.0962 -> 0.0947
+// (profiles/r02_round2b/ab_group_lanes_small.txt); slower from 16384 envs on.
+inline int dyn_group_lanes(const LaunchCtx& L) {
+  if (L.dyn_mapping == LBSIM_DYN_ENV_PER_LANE && L.S <= 16) return 0;
+  static const int forced = [] {
+    const char* e = std::getenv("LBSIM_DYN_GROUP_LANES");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (forced >= L.S && (forced == 4 || forced == 8 || forced == 16 || forced == 32 || forced == 64))
+    return forced;
+  if (L.S <= 2) return 2;
+  if (L.S <= 4) return (int64_t)L.B * 4 / 64 <= L.simds / 2 ? 8 : 4;
+  int g = 8;
+  while (g < L.S) g <<= 1;
+  return g;
+}
+
 // Dynamics of one step (mode kModeStep) or of a reset with warm-up (kModeReset).
 void launch_dynamics_step(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
                           const uint8_t* mask, hipStream_t s);
@@ -38,6 +63,11 @@ void launch_observe_reset(const LaunchCtx& L, const ObsOutputs& o, const uint8_t
 
 struct SacActorArgs;
 struct QmixArgs;
+// The fused dynamics + observe step (lbsim_step.hip) for the group width of dyn_group_lanes;
+// false when that width has no fused form (S > 16, one lane per env): use the two launches.
+bool launch_fused_step(const LaunchCtx& L, int group_lanes, const void* action, int dtype,
+                       int32_t* assign, const ObsOutputs& o, hipStream_t s);
+
 // the fused policy kernels (lbsim_pol.hip): LBSIM_OK / LBSIM_EDEVICE / LBSIM_ENOTSUP
 int launch_sac_actor(SacActorArgs& a, int64_t B, int mt, size_t lds, hipStream_t s);
 int launch_qmix_policy(QmixArgs& a, int64_t B, int form, int mt, size_t lds, hipStream_t s);

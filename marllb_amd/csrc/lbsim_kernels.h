@@ -1891,6 +1891,11 @@ struct ObsOutputs {
   float* raw_obs;
   int32_t* ep_len;
   double* ep_ret;
+  // problem-05 facade (multi_agent_env.py:152-188, 240-258): per-agent observations [B, A, 4k +
+  // 7S] of the returned rows, and the global state [B, 4S + 10]
+  float* agent_obs;
+  float* state;
+  int num_agents, servers_per_agent;
 };
 
 // One wave per 4-server chunk (kObsChunk), all chunks of an env in one workgroup: S = 4 -> one
@@ -1900,6 +1905,99 @@ struct ObsOutputs {
 // S (96 VGPRs): the work per wave is the same chunk whatever S is.
 template <int MAXS>
 constexpr int kObsWavesPerEnv = MAXS <= kObsChunk ? 1 : MAXS / kObsChunk;
+
+// The reward, episode bookkeeping and output rows of env b once its (S, 11) rows are in s_obs
+// (rewards.py:290-381, env.py:261-281, env.py:450-470): threads tid < 64 (one wave) compute the
+// reward, all nthr threads write the rows.
+template <int MAXS, int MODE>
+__device__ __forceinline__ void observe_outputs(const DevState& st, const SimParams& p,
+                                                const ObsOutputs& out, size_t b,
+                                                float* s_obs, float* s_act, int tid, int nthr) {
+  const int S = p.S;
+  // active servers (any column > 0): lane s of wave 0 scans its row, one ballot; their
+  // reward-field values compacted into s_act in server order
+  if (tid < 64) {
+    const int lane = tid;
+    bool act = false;
+    if (lane < S)
+      for (int f = 0; f < NF; ++f) act |= s_obs[lane * NF + f] > 0.0f;
+    const uint64_t act_mask = __ballot(act);
+    const bool fok = p.reward_field >= 0 && p.reward_field < NF;
+    if (act && fok) s_act[__popcll(act_mask & ((1ull << lane) - 1ull))] = s_obs[lane * NF + p.reward_field];
+    wave_sync();
+    if (MODE == kModeStep && lane == 0) {
+      const int na = __popcll(act_mask);
+      double r = 0.0;
+      if (fok) {
+        if (S <= kObsChunk && p.reward_metric == 0)  // (observe_kernel<4>; fused G = 8, S <= 4)
+          r = jain_upto4(na, s_act);
+        else
+          r = reward_values(na, [&](int i) { return (double)s_act[i]; }, p.reward_metric);
+      }
+      out.reward[b] = (float)r;
+      const int32_t es = st.ep_step[b] + 1;
+      const double er = st.ep_return[b] + r;
+      st.ep_step[b] = es;
+      st.ep_return[b] = er;
+      out.done[b] = (uint8_t)(es >= p.max_steps ? 1 : 0);
+      if (out.ep_len != nullptr) out.ep_len[b] = es;
+      if (out.ep_ret != nullptr) out.ep_ret[b] = er;
+    }
+  }
+
+  const int nobs = S * NF;
+  float* orow = out.obs + b * (size_t)nobs;
+  const bool facade = out.agent_obs != nullptr || out.state != nullptr;
+  if (out.raw_obs != nullptr)
+    for (int e = tid; e < nobs; e += nthr) out.raw_obs[b * (size_t)nobs + e] = s_obs[e];
+  if (p.normalize) {  // env.py:460-468, float64 running statistics
+    const int32_t cnt = st.norm_count[b] + 1;
+    for (int e = tid; e < nobs; e += nthr) {
+      const size_t gi = b * (size_t)nobs + (size_t)e;
+      const double o = (double)s_obs[e];
+      double m = st.norm_mean[gi];
+      const double sdv = st.norm_std[gi];
+      const double delta = o - m;
+      m = m + delta / (double)cnt;
+      const double delta2 = o - m;
+      double v = (sdv * sdv * (double)(cnt - 1) + delta * delta2) / (double)cnt;
+      v = v > 1e-8 ? v : 1e-8;
+      const double ns = sqrt(v);
+      st.norm_mean[gi] = m;
+      st.norm_std[gi] = ns;
+      const float r = (float)((o - m) / (ns + 1e-8));
+      orow[e] = r;
+      if (facade) s_obs[e] = r;  // the returned rows, for the facade gather below (same thread)
+    }
+    if (tid == 0) st.norm_count[b] = cnt;
+  } else {
+    for (int e = tid; e < nobs; e += nthr) orow[e] = s_obs[e];
+  }
+  if (facade) {
+    if (nthr == 64) wave_sync();
+    else __syncthreads();  // block-uniform
+    const int A = out.num_agents, k = out.servers_per_agent, D = 4 * k + 7 * S;
+    if (out.agent_obs != nullptr) {  // agent a: flat[4 a k, 4 (a+1) k) ++ flat[4 S:]
+      float* ao = out.agent_obs + b * (size_t)A * (size_t)D;
+      for (int e = tid; e < A * D; e += nthr) {
+        const int a = e / D, j = e - a * D;
+        ao[e] = s_obs[j < 4 * k ? 4 * k * a + j : 4 * S + (j - 4 * k)];
+      }
+    }
+    if (out.state != nullptr) {  // get_state: zeros ... then step / max_steps, num_agents
+      const int sd = 4 * S + 10;
+      float* so = out.state + b * (size_t)sd;
+      for (int e = tid; e < sd - 2; e += nthr) so[e] = 0.0f;
+      if (tid == 0) {
+        // the episode step after this step (written by this thread above), or 0 after a reset
+        // (the reset dynamics launch zeroed it)
+        const int32_t es = st.ep_step[b];
+        so[sd - 2] = (float)es / (float)p.max_steps;
+        so[sd - 1] = (float)A;
+      }
+    }
+  }
+}
 
 template <int MAXS, int MODE>
 __global__ void __launch_bounds__(64 * kObsWavesPerEnv<MAXS>, 5)
@@ -1919,62 +2017,21 @@ __global__ void __launch_bounds__(64 * kObsWavesPerEnv<MAXS>, 5)
                                            sc, s_obs, lane);
   }
   __syncthreads();
+  observe_outputs<MAXS, MODE>(st, p, out, b, s_obs, s_act, tid, nthr);
+}
 
-  // active servers (any column > 0): lane s of wave 0 scans its row, one ballot; their
-  // reward-field values compacted into s_act in server order
-  if (wv == 0) {
-    bool act = false;
-    if (lane < S)
-      for (int f = 0; f < NF; ++f) act |= s_obs[lane * NF + f] > 0.0f;
-    const uint64_t act_mask = __ballot(act);
-    const bool fok = p.reward_field >= 0 && p.reward_field < NF;
-    if (act && fok) s_act[__popcll(act_mask & ((1ull << lane) - 1ull))] = s_obs[lane * NF + p.reward_field];
-    wave_sync();
-    if (mode == kModeStep && lane == 0) {
-      const int na = __popcll(act_mask);
-      double r = 0.0;
-      if (fok) {
-        if (MAXS <= kObsChunk && p.reward_metric == 0)
-          r = jain_upto4(na, s_act);
-        else
-          r = reward_values(na, [&](int i) { return (double)s_act[i]; }, p.reward_metric);
-      }
-      out.reward[b] = (float)r;
-      const int32_t es = st.ep_step[b] + 1;
-      const double er = st.ep_return[b] + r;
-      st.ep_step[b] = es;
-      st.ep_return[b] = er;
-      out.done[b] = (uint8_t)(es >= p.max_steps ? 1 : 0);
-      if (out.ep_len != nullptr) out.ep_len[b] = es;
-      if (out.ep_ret != nullptr) out.ep_ret[b] = er;
-    }
-  }
-
-  const int nobs = S * NF;
-  float* orow = out.obs + b * (size_t)nobs;
-  if (out.raw_obs != nullptr)
-    for (int e = tid; e < nobs; e += nthr) out.raw_obs[b * (size_t)nobs + e] = s_obs[e];
-  if (p.normalize) {  // env.py:460-468, float64 running statistics
-    const int32_t cnt = st.norm_count[b] + 1;
-    for (int e = tid; e < nobs; e += nthr) {
-      const size_t gi = b * (size_t)nobs + (size_t)e;
-      const double o = (double)s_obs[e];
-      double m = st.norm_mean[gi];
-      const double sdv = st.norm_std[gi];
-      const double delta = o - m;
-      m = m + delta / (double)cnt;
-      const double delta2 = o - m;
-      double v = (sdv * sdv * (double)(cnt - 1) + delta * delta2) / (double)cnt;
-      v = v > 1e-8 ? v : 1e-8;
-      const double ns = sqrt(v);
-      st.norm_mean[gi] = m;
-      st.norm_std[gi] = ns;
-      orow[e] = (float)((o - m) / (ns + 1e-8));
-    }
-    if (tid == 0) st.norm_count[b] = cnt;
-  } else {
-    for (int e = tid; e < nobs; e += nthr) orow[e] = s_obs[e];
-  }
+// observe_kernel's work for env b by ONE wave, its chunks in sequence (fused_step_kernel's second
+// phase).  Same routines, same order: the same bits.
+template <int MAXS>
+__device__ __forceinline__ void observe_env_wave(const DevState& st, const SimParams& p,
+                                                 const ObsOutputs& out, size_t b, ObsScratch& sc,
+                                                 float* s_obs, float* s_act, int lane) {
+  const int S = p.S;
+  for (int s0 = 0; s0 < S; s0 += kObsChunk)
+    observe_chunk<true, true>(st, p, b, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk, sc, s_obs,
+                              lane);
+  observe_outputs<MAXS, kModeStep>(st, p, out, b, s_obs, s_act, lane, 64);
+  wave_sync();  // s_obs / s_act reused by the next env
 }
 
 }  // namespace lbk

@@ -104,7 +104,7 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
                 server_rates: Optional[List[float]] = None, load: float = 0.8,
                 queue_capacity: int = 32, warmup_steps: int = 8, decay_factor: float = 0.9,
                 assign_policy: str = "sed", trace=None,
-                dyn_mapping: str = "auto") -> _lib.LbsimConfig:
+                dyn_mapping: str = "auto", step_kernel: str = "auto") -> _lib.LbsimConfig:
     """Build and validate an lbsim_config_t from reference-style kwargs.
 
     server_rates defaults to identical servers at utilisation `load`: mu = rate / (load * S).
@@ -112,6 +112,8 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
     replaces arrival_rate.  The arrays themselves go to the handle (Handle.set_trace).
     dyn_mapping: "auto" | "env" (one lane per env) | "server" (one lane per server): how the
     dynamics kernel lays envs onto lanes; results are identical, only speed differs.
+    step_kernel: "auto" | "split" (dynamics launch + observe launch) | "fused" (one launch that
+    simulates then observes each workgroup's envs); results are identical.
     """
     if reward_metric not in _lib.METRICS:  # rewards.py:321-323
         raise ValueError(f"Unsupported metric: {reward_metric}. Supported: {_lib.METRICS}")
@@ -157,6 +159,9 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
     if dyn_mapping not in _lib.DYN_MAPPINGS:
         raise ValueError(f"Unknown dyn_mapping: {dyn_mapping}. Supported: {_lib.DYN_MAPPINGS}")
     cfg.dyn_mapping = _lib.DYN_MAPPINGS.index(dyn_mapping)
+    if step_kernel not in _lib.STEP_KERNELS:
+        raise ValueError(f"Unknown step_kernel: {step_kernel}. Supported: {_lib.STEP_KERNELS}")
+    cfg.step_kernel = _lib.STEP_KERNELS.index(step_kernel)
     _lib.validate(cfg)
     return cfg
 
@@ -325,17 +330,32 @@ class VecLoadBalanceEnv:
         return obs
 
     # -- API
-    def reset(self, mask=None):
+    @staticmethod
+    def _facade_outputs(out, facade):
+        """facade = (num_agents, servers_per_agent, agent_obs, state): the problem-05 outputs the
+        step / reset launch writes beside the observation (lbsim_step_outputs_t)."""
+        if facade is None:
+            return
+        A, k, ao, stt = facade
+        out.num_agents, out.servers_per_agent = A, k
+        out.agent_obs = ao.data_ptr() if ao is not None else None
+        out.state = stt.data_ptr() if stt is not None else None
+
+    def reset(self, mask=None, *, facade=None):
         """Reset all envs (mask None) or those with mask[b] true; returns obs for all envs.
 
         With a mask, rows of envs that are not reset hold the obs of their last step() (or of
-        the previous reset), so the returned tensor is always a complete batch.
+        the previous reset), so the returned tensor is always a complete batch.  facade: see
+        _facade_outputs (rows of reset envs are written).
         """
         torch = _torch()
         if mask is None:
             obs = self._obs_buffer()
-            self.handle.check(self.handle.lib.lbsim_reset(self.handle.h, None, obs.data_ptr(),
-                                                          self._stream()))
+            out = _lib.StepOutputs()
+            out.obs = obs.data_ptr()
+            self._facade_outputs(out, facade)
+            self.handle.check(self.handle.lib.lbsim_reset_ex(self.handle.h, None,
+                                                             ctypes.byref(out), self._stream()))
             self._reset_done = True
             self._step_bound = 0
             if self.feature_mode == "upstream":
@@ -347,8 +367,11 @@ class VecLoadBalanceEnv:
             raise RuntimeError("call reset() without a mask first")
         m = self._mask(mask)
         obs = self._last_obs.clone()
-        self.handle.check(self.handle.lib.lbsim_reset(self.handle.h, m.data_ptr(),
-                                                      obs.data_ptr(), self._stream()))
+        out = _lib.StepOutputs()
+        out.obs = obs.data_ptr()
+        self._facade_outputs(out, facade)
+        self.handle.check(self.handle.lib.lbsim_reset_ex(self.handle.h, m.data_ptr(),
+                                                         ctypes.byref(out), self._stream()))
         if self.feature_mode == "upstream":
             self._upstream(obs, rows=m.bool())
             if self._up_ret is not None:
@@ -356,7 +379,7 @@ class VecLoadBalanceEnv:
         self._last_obs = obs
         return obs
 
-    def step(self, actions, *, assign_counts: bool = False, raw_obs: bool = False
+    def step(self, actions, *, assign_counts: bool = False, raw_obs: bool = False, facade=None
              ) -> Tuple[Any, Any, Any, Dict[str, Any]]:
         torch = _torch()
         if not self._reset_done:
@@ -379,6 +402,7 @@ class VecLoadBalanceEnv:
         ep_ret = torch.empty(B, dtype=torch.float64, device=self.device)
         out.episode_length = ep_len.data_ptr()
         out.episode_return = ep_ret.data_ptr()
+        self._facade_outputs(out, facade)
         self.handle.check(self.handle.lib.lbsim_step_ex(self.handle.h, a.data_ptr(), dt,
                                                         ctypes.byref(out), self._stream()))
         if self.feature_mode == "upstream":
@@ -401,8 +425,11 @@ class VecLoadBalanceEnv:
             if self.keep_terminal_obs:
                 info["terminal_obs"] = obs.clone()
             # envs with done == 0 are untouched by the masked reset (no host sync needed)
-            self.handle.check(self.handle.lib.lbsim_reset(self.handle.h, done.data_ptr(),
-                                                          obs.data_ptr(), self._stream()))
+            rout = _lib.StepOutputs()
+            rout.obs = obs.data_ptr()
+            self._facade_outputs(rout, facade)
+            self.handle.check(self.handle.lib.lbsim_reset_ex(self.handle.h, done.data_ptr(),
+                                                             ctypes.byref(rout), self._stream()))
             if self.feature_mode == "upstream":
                 self._upstream(obs, rows=done)
         self._last_obs = obs

@@ -139,7 +139,7 @@ class VecMultiAgentLoadBalanceEnv:
         self.obs_dim = agent_obs_dim(num_agents, servers_per_agent)
         self.state_dim = self.S * 4 + 10
         self.lib = _lib.load()
-        self._ep_len = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
+        self._state = None  # the state the last step / reset launch wrote (get_state)
 
     def agent_obs(self, obs):
         """(B, S, 11) -> (B, A, 4k + 7S) by lbsim_agent_obs."""
@@ -163,14 +163,25 @@ class VecMultiAgentLoadBalanceEnv:
             return a.reshape(a.shape[0], self.S)
         return a
 
+    def _facade(self, masked: bool):
+        """Fresh per-call output tensors for the launch to fill (callers may keep them: value
+        semantics without a copy kernel); a masked reset starts from the previous state."""
+        torch = _torch()
+        ao = torch.empty((self.num_envs, self.num_agents, self.obs_dim), dtype=torch.float32,
+                         device=self.device)
+        st = (self._state.clone() if masked and self._state is not None else
+              torch.empty((self.num_envs, self.state_dim), dtype=torch.float32, device=self.device))
+        return (self.num_agents, self.k, ao, st)
+
     def reset(self, mask=None):
-        obs = self.vec.reset(mask=mask)
-        if mask is None:
-            self._ep_len.zero_()
-        else:
-            m = mask.to(self.device) if hasattr(mask, "to") else _torch().as_tensor(mask).to(self.device)
-            self._ep_len.masked_fill_(m.bool(), 0)
-        return self.agent_obs(obs)
+        """The per-agent observations and the state come from the reset launch itself."""
+        f = self._facade(mask is not None)
+        obs = self.vec.reset(mask=mask, facade=f)
+        ao = f[2]
+        if mask is not None:  # rows of envs not reset: their last agent observations
+            ao = self.agent_obs(obs)
+        self._state = f[3]
+        return ao
 
     def step(self, actions):
         torch = _torch()
@@ -180,10 +191,9 @@ class VecMultiAgentLoadBalanceEnv:
         # obs, which step() writes over `obs`).  raw_obs is requested only when they can differ.
         need_raw = bool(v.cfg.normalize_obs) or (
             v.autoreset and v._step_bound + 1 >= v.cfg.max_steps)
-        obs, rew, done, info = v.step(self.expand_actions(actions), raw_obs=need_raw)
-        self._ep_len = info["episode_length"].to(torch.int32)
-        if v.autoreset:  # out of place: info["episode_length"] keeps the finished length
-            self._ep_len = self._ep_len.masked_fill(done, 0)
+        f = self._facade(False)
+        obs, rew, done, info = v.step(self.expand_actions(actions), raw_obs=need_raw, facade=f)
+        self._state = f[3]  # written by the step launch (and the auto-reset launch's rows)
         loads = (info["raw_obs"] if need_raw else obs)[:, :, 0]
         info = dict(info)
         info["server_loads"] = loads
@@ -194,16 +204,14 @@ class VecMultiAgentLoadBalanceEnv:
             s, sq = l.sum(2), (l * l).sum(2)
             rewards = torch.where(s == 0, torch.zeros_like(s),
                                   s * s / (self.k * sq + 1e-8)).float()
-        return self.agent_obs(obs), rewards, done, info
+        return f[2], rewards, done, info
 
     def get_state(self):
-        torch = _torch()
-        if getattr(self, "_state", None) is None:  # zeros, then the constant agent-count column
-            self._state = torch.zeros((self.num_envs, self.state_dim), dtype=torch.float32,
-                                      device=self.device)
-            self._state[:, -1] = float(self.num_agents)
-        torch.div(self._ep_len, float(self.max_steps), out=self._state[:, -2])
-        return self._state.clone()  # callers may keep it (replay buffers): value semantics
+        """(B, 4S + 10): written by the last step / reset launch into a tensor of its own, never
+        written again (value semantics without a copy)."""
+        if self._state is None:
+            raise RuntimeError("call reset() before get_state()")
+        return self._state
 
     def close(self):
         self.vec.close()

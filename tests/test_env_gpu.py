@@ -334,7 +334,7 @@ def test_profiler_counts_and_times_every_launch():
     import time
     from marllb_amd import _lib
     from marllb_amd.env import VecLoadBalanceEnv
-    env = VecLoadBalanceEnv(4096, 4, device="cuda:0", seed=3)
+    env = VecLoadBalanceEnv(4096, 4, device="cuda:0", seed=3, step_kernel="split")
     env.reset()
     lib, h = _lib.load(), env.handle
     h.check(lib.lbsim_profile_begin(h.h, 64))
@@ -356,4 +356,17 @@ def test_profiler_counts_and_times_every_launch():
         env.step(torch.randint(0, 3, (4096, 4), device="cuda:0"))
     h.check(lib.lbsim_profile_end(h.h, ms, cnt))
     assert cnt[0] + cnt[1] <= 3 and cnt[0] >= 1
+    env.close()
+    # the fused step kernel: one launch per step, class 4 (lbsim_profile_end_ex)
+    env = VecLoadBalanceEnv(4096, 4, device="cuda:0", seed=3, step_kernel="fused")
+    env.reset()
+    h = env.handle
+    h.check(lib.lbsim_profile_begin(h.h, 64))
+    for _ in range(5):
+        env.step(torch.randint(0, 3, (4096, 4), device="cuda:0"))
+    ms5 = (ctypes.c_double * 5)()
+    cnt5 = (ctypes.c_int64 * 5)()
+    h.check(lib.lbsim_profile_end_ex(h.h, ms5, cnt5, 5))
+    assert list(cnt5) == [0, 0, 0, 0, 5] and ms5[4] > 0
+    assert lib.lbsim_profile_end_ex(h.h, ms5, cnt5, 6) == _lib.EINVAL
     env.close()
