@@ -90,8 +90,9 @@ enum lbsim_dyn_mapping {
 
 /* How lbsim_step runs; every choice produces the same bits.  FUSED: one launch per step whose
  * workgroups simulate their envs and then observe them; SPLIT: a dynamics launch
- * and an observe launch.  AUTO = FUSED where it exists (server-per-lane groups of <= 16 lanes),
- * else SPLIT.  The environment variable LBSIM_STEP_KERNEL=split|fused overrides AUTO. */
+ * and an observe launch.  AUTO = SPLIT (the fused form measured slower); FUSED
+ * exists for server-per-lane groups of <= 16 lanes (else SPLIT).  The environment variable
+ * LBSIM_STEP_KERNEL=split|fused overrides AUTO. */
 enum lbsim_step_kernel { LBSIM_STEP_AUTO = 0, LBSIM_STEP_SPLIT = 1, LBSIM_STEP_FUSED = 2 };
 
 /*
@@ -279,6 +280,9 @@ typedef struct lbsim_sac_actor { /* problem-04 PolicyNetwork (networks.py:19-146
   const float* bh;               /* [2 A], zero-padded to a multiple of 16                    */
   float log_std_min, log_std_max; /* clamp (networks.py:93)                                   */
   float action_scale, action_bias;
+  const uint32_t* step_dev;      /* NULL, or a device u32 read as the Philox `step` counter      */
+                                 /* instead of the argument (hipGraph replays: the caller        */
+                                 /* advances it in the graph)                                     */
 } lbsim_sac_actor_t;
 size_t lbsim_sac_actor_size(void);
 
@@ -310,6 +314,7 @@ typedef struct lbsim_qmix_policy { /* problem-05 QMIXAgent agents + QMixingNetwo
    * [3 he + E, state_dim]; then hyper_w1[2] [A E, he], hyper_w2[2] [E, he], hyper_b2[2] [1, he]
    * (rows padded to 16) with their biases */
   const float *m0, *mb0, *mw1, *mbw1, *mw2, *mbw2, *mb2, *mbb2;
+  const uint32_t* step_dev;      /* as lbsim_sac_actor_t.step_dev                              */
 } lbsim_qmix_policy_t;
 size_t lbsim_qmix_policy_size(void);
 

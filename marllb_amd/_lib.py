@@ -90,7 +90,8 @@ class SacActor(ctypes.Structure):
                  ("hidden_dim", ctypes.c_int32), ("action_dim", ctypes.c_int32)]
                 + [(n, ctypes.c_void_p) for n in _SAC_WEIGHTS]
                 + [("log_std_min", ctypes.c_float), ("log_std_max", ctypes.c_float),
-                   ("action_scale", ctypes.c_float), ("action_bias", ctypes.c_float)])
+                   ("action_scale", ctypes.c_float), ("action_bias", ctypes.c_float),
+                   ("step_dev", ctypes.c_void_p)])
 
 
 class QmixPolicy(ctypes.Structure):
@@ -100,7 +101,8 @@ class QmixPolicy(ctypes.Structure):
                                                "n_actions", "state_dim", "mixing_embed_dim",
                                                "hypernet_embed_dim", "servers_per_agent")]
                 + [("epsilon", ctypes.c_float)]
-                + [(n, ctypes.c_void_p) for n in _QMIX_WEIGHTS])
+                + [(n, ctypes.c_void_p) for n in _QMIX_WEIGHTS]
+                + [("step_dev", ctypes.c_void_p)])
 
 
 class LbsimError(RuntimeError):

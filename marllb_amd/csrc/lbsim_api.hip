@@ -303,8 +303,9 @@ bool use_fused_step(const lbsim_t* h) {
     if (e != nullptr && std::strcmp(e, "fused") == 0) return LBSIM_STEP_FUSED;
     return LBSIM_STEP_AUTO;
   }();
+  // AUTO = SPLIT: the fused kernel measured slower at every shape tried
   const int k = h->cfg.step_kernel != LBSIM_STEP_AUTO ? h->cfg.step_kernel : env;
-  if (k == LBSIM_STEP_SPLIT) return false;
+  if (k != LBSIM_STEP_FUSED) return false;
   const int g = dyn_group_lanes(ctx(h));
   return g >= 2 && g <= 16;
 }
@@ -694,6 +695,7 @@ int lbsim_sac_actor_step(const lbsim_sac_actor_t* n, const float* state, float* 
   a.key0 = (uint32_t)(seed & 0xFFFFFFFFull);
   a.key1 = (uint32_t)(seed >> 32);
   a.step = step;
+  a.step_dev = n->step_dev;
   int mt = fused_mt(B);
   // the [R][ld] tile + split-K scratch of the heads ([4][2][R][16])
   auto lds_of = [&](int m) { return (size_t)16 * m * (a.ld + 128) * 4; };
@@ -767,6 +769,7 @@ int lbsim_qmix_policy_step(const lbsim_qmix_policy_t* n, const float* obs, float
   a.key0 = (uint32_t)(seed & 0xFFFFFFFFull);
   a.key1 = (uint32_t)(seed >> 32);
   a.step = step;
+  a.step_dev = n->step_dev;
   auto lds_of = [&](int mt) {
     const size_t R = 16 * (size_t)mt;
     return (R * a.ld + (size_t)A * R * 16 + R * A + 64 * R) * 4;  // + split-K scratch

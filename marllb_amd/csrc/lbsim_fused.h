@@ -282,10 +282,12 @@ struct SacActorArgs {
   float lo, hi, scale, bias;
   int deterministic;
   uint32_t key0, key1, step;
+  const uint32_t* step_dev;  // when set, the Philox step counter is *step_dev (graph replays)
 };
 
 template <int MT, int H, int F>
 __global__ void __launch_bounds__(256) sac_actor_kernel(SacActorArgs p) {
+  const uint32_t step = p.step_dev != nullptr ? *p.step_dev : p.step;
   extern __shared__ float lds[];
   constexpr int R = 16 * MT;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -324,7 +326,7 @@ __global__ void __launch_bounds__(256) sac_actor_kernel(SacActorArgs p) {
     ls = ls < p.lo ? p.lo : (ls > p.hi ? p.hi : ls);
     float x = mean;
     if (!p.deterministic) {  // the noise of sac_head_kernel (lbsim_nets.h), same counter
-      const u32x4 d = philox4x32_10(u32x4{(uint32_t)b, p.step, (uint32_t)a, 3u << 24}, p.key0,
+      const u32x4 d = philox4x32_10(u32x4{(uint32_t)b, step, (uint32_t)a, 3u << 24}, p.key0,
                                     p.key1);
       const float u1 = u01_open0(d.x), u2 = (float)(d.y >> 8) * 5.9604644775390625e-8f;
       const float eps = sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
@@ -356,6 +358,7 @@ struct QmixArgs {
   int lda;  // qmix_agent_wave_kernel: row stride of a wave's own [16][lda] agent region
   float epsilon;
   uint32_t key0, key1, step;
+  const uint32_t* step_dev;  // when set, the Philox step counter is *step_dev (graph replays)
 };
 
 struct QmixMixAct {
@@ -449,6 +452,7 @@ __device__ __forceinline__ void qmix_mixer(const QmixArgs& p, float* lds, const 
 
 template <int MT, int H, int F>
 __global__ void __launch_bounds__(256) qmix_policy_kernel(QmixArgs p) {
+  const uint32_t step = p.step_dev != nullptr ? *p.step_dev : p.step;
   extern __shared__ float lds[];
   constexpr int R = 16 * MT;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -504,7 +508,7 @@ __global__ void __launch_bounds__(256) qmix_policy_kernel(QmixArgs p) {
     int g = 0;
     for (int j = 1; j < NQ; ++j)
       if (q[j] > q[g]) g = j;
-    const u32x4 d = philox4x32_10(u32x4{(uint32_t)b, p.step, (uint32_t)a, 4u << 24}, p.key0,
+    const u32x4 d = philox4x32_10(u32x4{(uint32_t)b, step, (uint32_t)a, 4u << 24}, p.key0,
                                   p.key1);
     const float u = (float)(d.x >> 8) * 5.9604644775390625e-8f;  // [0, 1)
     const int act = u < p.epsilon ? (int)(((uint64_t)d.y * (uint32_t)NQ) >> 32) : g;
@@ -527,6 +531,7 @@ __global__ void __launch_bounds__(256) qmix_policy_kernel(QmixArgs p) {
 // four tiles at a time); the workgroup meets once, for the mixer.
 template <int H, int F>
 __global__ void __launch_bounds__(256) qmix_agent_wave_kernel(QmixArgs p) {
+  const uint32_t step = p.step_dev != nullptr ? *p.step_dev : p.step;
   extern __shared__ float lds[];
   constexpr int R = 16, UT = H / 16, NT = F / 16;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -629,7 +634,7 @@ __global__ void __launch_bounds__(256) qmix_agent_wave_kernel(QmixArgs p) {
       int g = 0;
       for (int j = 1; j < NQ; ++j)
         if (q[j] > q[g]) g = j;
-      const u32x4 d = philox4x32_10(u32x4{(uint32_t)b, p.step, (uint32_t)a, 4u << 24}, p.key0,
+      const u32x4 d = philox4x32_10(u32x4{(uint32_t)b, step, (uint32_t)a, 4u << 24}, p.key0,
                                     p.key1);
       const float u = (float)(d.x >> 8) * 5.9604644775390625e-8f;
       const int act = u < p.epsilon ? (int)(((uint64_t)d.y * (uint32_t)NQ) >> 32) : g;
@@ -656,6 +661,7 @@ __global__ void __launch_bounds__(256) qmix_agent_wave_kernel(QmixArgs p) {
 // region; every layer boundary is a workgroup barrier (all agents run the same layer sequence).
 template <int H, int F>
 __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
+  const uint32_t step = p.step_dev != nullptr ? *p.step_dev : p.step;
   extern __shared__ float lds[];
   constexpr int R = 16, UT = H / 16, NT = F / 16;
   static_assert(UT % 2 == 0 && NT % 8 == 0, "tiles split in halves of 4-tile passes");
@@ -773,7 +779,7 @@ __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
     int g = 0;
     for (int j = 1; j < NQ; ++j)
       if (q[j] > q[g]) g = j;
-    const u32x4 d = philox4x32_10(u32x4{(uint32_t)b, p.step, (uint32_t)a, 4u << 24}, p.key0,
+    const u32x4 d = philox4x32_10(u32x4{(uint32_t)b, step, (uint32_t)a, 4u << 24}, p.key0,
                                   p.key1);
     const float u = (float)(d.x >> 8) * 5.9604644775390625e-8f;
     const int act = u < p.epsilon ? (int)(((uint64_t)d.y * (uint32_t)NQ) >> 32) : g;

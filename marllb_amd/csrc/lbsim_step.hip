@@ -19,7 +19,7 @@ namespace lbk {
 namespace {
 
 template <int G, int MAXS, int POLICY, bool TRACE>
-__global__ void __launch_bounds__(64, 4)
+__global__ void __launch_bounds__(64)
     fused_step_kernel(DevState st, SimParams p, const void* action, int action_dtype,
                       int32_t* assign_out, ObsOutputs out) {
   __shared__ union {

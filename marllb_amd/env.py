@@ -226,12 +226,19 @@ class VecLoadBalanceEnv:
     With autoreset=True, envs whose episode ended are reset inside step(); their returned obs is
     the first obs of the new episode and info['terminal_obs'] (if keep_terminal_obs) holds the
     last one, as gym/SB3 vector envs do.
+    graph_mode=True makes one step() capturable into a torch.cuda.CUDAGraph (hipGraph) and
+    replayable: every output is a buffer allocated once and rewritten by each step (callers that
+    keep a step's outputs must copy them), and the masked auto-reset launch runs every step (it
+    leaves envs that are not done untouched) instead of being skipped on a host-side count.
     """
 
     def __init__(self, num_envs: int, num_servers: int = 4, *, device=None,
                  autoreset: bool = True, keep_terminal_obs: bool = False,
-                 strict_actions: bool = False, feature_mode: str = "problem01", **kwargs):
+                 strict_actions: bool = False, feature_mode: str = "problem01",
+                 graph_mode: bool = False, **kwargs):
         torch = _torch()
+        self.graph_mode = graph_mode
+        self._static = {}  # graph_mode: output buffers by name
         # feature_mode "upstream": columns 1-10 follow the live agent's process_reservoir
         # (src/lb/shm_proxy.py:518-543: value-decayed mean / p90 over all 128 raw bins, f64) on the
         # simulator's reservoirs seen the VPP way (lbsim_vpp_export + lbsim_vpp_features), and the
@@ -266,10 +273,18 @@ class VecLoadBalanceEnv:
     def _stream(self) -> int:
         return _torch().cuda.current_stream(self.device).cuda_stream
 
-    def _obs_buffer(self):
+    def _buf(self, name, shape, dtype):
+        """An output tensor: fresh per call, or (graph_mode) the same buffer every call."""
         torch = _torch()
-        return torch.empty((self.num_envs, self.num_servers, 11), dtype=torch.float32,
-                           device=self.device)
+        if self.graph_mode:
+            t = self._static.get(name)
+            if t is None:
+                t = self._static[name] = torch.empty(shape, dtype=dtype, device=self.device)
+            return t
+        return torch.empty(shape, dtype=dtype, device=self.device)
+
+    def _obs_buffer(self, name="obs"):
+        return self._buf(name, (self.num_envs, self.num_servers, 11), _torch().float32)
 
     def _action(self, actions):
         torch = _torch()
@@ -366,7 +381,7 @@ class VecLoadBalanceEnv:
         if not self._reset_done:
             raise RuntimeError("call reset() without a mask first")
         m = self._mask(mask)
-        obs = self._last_obs.clone()
+        obs = self._last_obs if self.graph_mode else self._last_obs.clone()
         out = _lib.StepOutputs()
         out.obs = obs.data_ptr()
         self._facade_outputs(out, facade)
@@ -387,19 +402,19 @@ class VecLoadBalanceEnv:
         a, dt = self._action(actions)
         B, S = self.num_envs, self.num_servers
         obs = self._obs_buffer()
-        reward = torch.empty(B, dtype=torch.float32, device=self.device)
-        done = torch.empty(B, dtype=torch.bool, device=self.device)  # 1-byte 0/1, as u8
+        reward = self._buf("reward", (B,), torch.float32)
+        done = self._buf("done", (B,), torch.bool)  # 1-byte 0/1, as u8
         out = _lib.StepOutputs()
         out.obs, out.reward, out.done = obs.data_ptr(), reward.data_ptr(), done.data_ptr()
         assign = raw = None
         if assign_counts:
-            assign = torch.empty((B, S), dtype=torch.int32, device=self.device)
+            assign = self._buf("assign", (B, S), torch.int32)
             out.assign_count = assign.data_ptr()
         if raw_obs:
-            raw = self._obs_buffer()
+            raw = self._obs_buffer("raw_obs")
             out.raw_obs = raw.data_ptr()
-        ep_len = torch.empty(B, dtype=torch.int32, device=self.device)
-        ep_ret = torch.empty(B, dtype=torch.float64, device=self.device)
+        ep_len = self._buf("ep_len", (B,), torch.int32)
+        ep_ret = self._buf("ep_ret", (B,), torch.float64)
         out.episode_length = ep_len.data_ptr()
         out.episode_return = ep_ret.data_ptr()
         self._facade_outputs(out, facade)
@@ -421,7 +436,7 @@ class VecLoadBalanceEnv:
         if raw is not None:
             info["raw_obs"] = raw
         self._step_bound += 1
-        if self.autoreset and self._step_bound >= self.cfg.max_steps:
+        if self.autoreset and (self.graph_mode or self._step_bound >= self.cfg.max_steps):
             if self.keep_terminal_obs:
                 info["terminal_obs"] = obs.clone()
             # envs with done == 0 are untouched by the masked reset (no host sync needed)

@@ -165,12 +165,15 @@ class VecMultiAgentLoadBalanceEnv:
 
     def _facade(self, masked: bool):
         """Fresh per-call output tensors for the launch to fill (callers may keep them: value
-        semantics without a copy kernel); a masked reset starts from the previous state."""
+        semantics without a copy kernel); a masked reset starts from the previous state.  In the
+        inner env's graph_mode: the same two buffers every call (rewritten in place)."""
         torch = _torch()
-        ao = torch.empty((self.num_envs, self.num_agents, self.obs_dim), dtype=torch.float32,
-                         device=self.device)
-        st = (self._state.clone() if masked and self._state is not None else
-              torch.empty((self.num_envs, self.state_dim), dtype=torch.float32, device=self.device))
+        v = self.vec
+        ao = v._buf("agent_obs", (self.num_envs, self.num_agents, self.obs_dim), torch.float32)
+        if masked and self._state is not None and not v.graph_mode:
+            st = self._state.clone()
+        else:
+            st = v._buf("state", (self.num_envs, self.state_dim), torch.float32)
         return (self.num_agents, self.k, ao, st)
 
     def reset(self, mask=None):
@@ -178,8 +181,8 @@ class VecMultiAgentLoadBalanceEnv:
         f = self._facade(mask is not None)
         obs = self.vec.reset(mask=mask, facade=f)
         ao = f[2]
-        if mask is not None:  # rows of envs not reset: their last agent observations
-            ao = self.agent_obs(obs)
+        if mask is not None and not self.vec.graph_mode:  # rows of envs not reset: their last
+            ao = self.agent_obs(obs)                       # agent observations
         self._state = f[3]
         return ao
 
@@ -189,7 +192,7 @@ class VecMultiAgentLoadBalanceEnv:
         # server loads are this step's raw n_flow_on: the un-normalised column, and for envs the
         # masked auto-reset restarts, the terminal step's value (not the next episode's first
         # obs, which step() writes over `obs`).  raw_obs is requested only when they can differ.
-        need_raw = bool(v.cfg.normalize_obs) or (
+        need_raw = bool(v.cfg.normalize_obs) or v.graph_mode or (
             v.autoreset and v._step_bound + 1 >= v.cfg.max_steps)
         f = self._facade(False)
         obs, rew, done, info = v.step(self.expand_actions(actions), raw_obs=need_raw, facade=f)

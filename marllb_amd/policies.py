@@ -350,7 +350,17 @@ class FusedQMIXPolicy:
                                    *[t.data_ptr() for t in self._packed])
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         self.step_no = 0
+        self.step_dev = None
         self._watch = _ParamWatch(self.agents + [mixer])
+
+    def use_device_step(self) -> None:
+        """Keep the Philox step counter on the device (lbsim_qmix_policy_t.step_dev), advanced
+        by a tiny kernel after each launch: a captured call replays with a new step each time,
+        drawing exactly what the eager calls would."""
+        if self.step_dev is None:
+            dev = self._packed[0].device
+            self.step_dev = torch.tensor([self.step_no & 0x7FFFFFFF], dtype=torch.int32, device=dev)
+            self.net.step_dev = self.step_dev.data_ptr()
 
     def _pack_tensors(self):
         agents, m = self.agents, self.mixer
@@ -398,6 +408,8 @@ class FusedQMIXPolicy:
             self.step_no & 0xFFFFFFFF, _ptr(acts), _ptr(sacts), _ptr(q), None, _ptr(q_tot),
             stream)))
         self.step_no += 1
+        if self.step_dev is not None:
+            self.step_dev.add_(1)
         return acts, sacts, q_tot, q
 
 

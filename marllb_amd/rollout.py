@@ -96,6 +96,25 @@ class QMIXRollout:
             self.hidden = [torch.zeros(1, env.num_envs, H, device=dev) for _ in self.agents]
         self.obs = env.reset()
 
+    def capture(self, warmup: int = 2) -> "torch.cuda.CUDAGraph":
+        """One step() captured into a torch.cuda.CUDAGraph: needs the fused kernel and an env in
+        graph_mode (static buffers, auto-reset launched every step); the Philox step counter
+        moves to the device.  `warmup` eager steps first (on a side stream, as torch requires),
+        then g.replay() == step() on the same static buffers (self.obs, self.hidden, ...)."""
+        if self.kernel is None or not self.env.vec.graph_mode:
+            raise ValueError("capture needs the fused QMIX kernel and graph_mode=True")
+        self.kernel.use_device_step()
+        side = torch.cuda.Stream(self.env.device)
+        side.wait_stream(torch.cuda.current_stream(self.env.device))
+        with torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):
+                self.step()
+        torch.cuda.current_stream(self.env.device).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.last = self.step()
+        return g
+
     @torch.no_grad()
     def step(self):
         B, A = self.env.num_envs, self.env.num_agents

@@ -242,16 +242,16 @@ def _compare_state(h_gpu, ora, B, S, Q, norm):
     np.testing.assert_array_equal(statelayout.live_ring(g, B, S, Q), statelayout.live_ring(o, B, S, Q))
 
 
-@pytest.mark.parametrize("mapping", ["env", "server", "server-split"])
+@pytest.mark.parametrize("mapping", ["env", "server", "server-fused"])
 @pytest.mark.parametrize("case", range(len(CONFIGS)))
 def test_simulator_bit_exact_vs_oracle(lib, oracle_mod, case, mapping):
     """Both dynamics mappings (one lane per env / one lane per server) against the oracle; the
-    server mapping both as the fused step kernel (the default, S <= 16) and as two launches."""
+    server mapping both as two launches (the default) and as the fused step kernel (S <= 16)."""
     from marllb_amd.env import VecLoadBalanceEnv, make_config
     c = CONFIGS[case]
     B, S, kw = c["B"], c["S"], resolve_kw(c["kw"])
-    if mapping == "server-split":
-        mapping, kw["step_kernel"] = "server", "split"
+    if mapping == "server-fused":
+        mapping, kw["step_kernel"] = "server", "fused"
     if mapping == "env" and S > 16:
         with pytest.raises(ValueError, match="at most 16 servers"):
             VecLoadBalanceEnv(B, S, device="cuda:0", dyn_mapping=mapping, **kw)
@@ -300,7 +300,7 @@ def test_wider_groups_bit_exact(lanes):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     ks = [f"test_simulator_bit_exact_vs_oracle[{c}-{m}]" for c in range(len(CONFIGS))
-          for m in ("server", "server-split") if CONFIGS[c]["S"] <= int(lanes)]
+          for m in ("server", "server-fused") if CONFIGS[c]["S"] <= int(lanes)]
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p",
                         "no:cacheprovider"] +
                        [os.path.join(root, "tests", "test_gpu_parity.py") + "::" + k for k in ks],

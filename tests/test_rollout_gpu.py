@@ -65,3 +65,73 @@ def test_qmix_rollout_kernel_matches_gemm_form_greedy():
     for (qk, rk, dk), (qg, rg, dg) in zip(*runs):
         assert torch.equal(rk, rg) and torch.equal(dk, dg)
         torch.testing.assert_close(qk, qg, rtol=1e-5, atol=1e-5)
+
+
+def test_env_step_graph_capture_replays_bit_exact():
+    """One VecLoadBalanceEnv.step (dynamics + observe launches + the every-step masked auto-reset
+    of graph_mode) captured into a torch.cuda.CUDAGraph and replayed over two auto-reset boundaries
+    equals eager stepping of an identical env, bit for bit."""
+    from marllb_amd import VecLoadBalanceEnv
+    B, S, T = 1024, 4, 4
+    eager = VecLoadBalanceEnv(B, S, device="cuda:0", seed=8, max_steps=T)
+    graph = VecLoadBalanceEnv(B, S, device="cuda:0", seed=8, max_steps=T, graph_mode=True)
+    eager.reset()
+    graph.reset()
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(1)
+    acts = [torch.randint(0, 3, (B, S), device="cuda:0", generator=g) for _ in range(3 * T)]
+    a_static = acts[0].clone()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):  # warm-up step (eager, graph_mode buffers)
+        o, r, d, _ = graph.step(a_static)
+    torch.cuda.current_stream().wait_stream(side)
+    e = eager.step(acts[0])
+    assert torch.equal(o, e[0]) and torch.equal(r, e[1]) and torch.equal(d, e[2])
+    cg = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(cg):
+        obs, rew, done, info = graph.step(a_static)
+    for k in range(1, 3 * T):
+        a_static.copy_(acts[k])
+        cg.replay()
+        eo, er, ed, ei = eager.step(acts[k])
+        assert torch.equal(obs, eo), k
+        assert torch.equal(rew, er), k
+        assert torch.equal(done, ed), k
+        assert torch.equal(info["episode_return"], ei["episode_return"]), k
+    eager.close()
+    graph.close()
+
+
+def test_qmix_rollout_graph_capture_replays_bit_exact():
+    """One QMIXRollout.step -- the fused QMIX policy kernel (Philox step counter on the device),
+    the fused env step writing the agent observations and the state, the auto-reset -- captured
+    and replayed equals the eager rollout (same weights and seeds) bit for bit, across episode
+    ends (max_steps 3), epsilon-greedy draws included."""
+    from marllb_amd.multi_agent import VecMultiAgentLoadBalanceEnv
+    from marllb_amd.rollout import QMIXRollout
+    B, T = 512, 3
+    outs = []
+    for graph_mode in (False, True):
+        torch.manual_seed(0)
+        env = VecMultiAgentLoadBalanceEnv(B, 4, 4, device="cuda:0", seed=12,
+                                          action_type="discrete", max_steps=T,
+                                          graph_mode=graph_mode)
+        ro = QMIXRollout(env, epsilon=0.3, seed=7)
+        seq = []
+        if graph_mode:
+            cg = ro.capture(warmup=2)  # two eager warm-up steps, then the captured one
+            for _ in range(3 * T):
+                cg.replay()
+                q_tot, rew, done, _ = ro.last
+                seq.append((q_tot.clone(), rew.clone(), done.clone(), ro.obs.clone()))
+        else:
+            for _ in range(2 + 3 * T):
+                q_tot, rew, done, _ = ro.step()
+                seq.append((q_tot.clone(), rew.clone(), done.clone(), ro.obs.clone()))
+            seq = seq[2:]  # align with the graph run's two warm-up steps
+        outs.append(seq)
+        env.close()
+    for k, (a, b) in enumerate(zip(*outs)):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y), k
