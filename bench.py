@@ -52,6 +52,35 @@ def algorithmic_bytes(S: int, slots_per_env: float, inflight_per_env: float):
     return {"observe_kernel": obs, "dynamics_kernel": dyn, "fused_step_kernel": obs + dyn}
 
 
+def valu_roofline(B: int, S: int, avg: dict):
+    """The VALU side of each simulator kernel, from profiles/pmc_valu.json
+    (tools/pmc_valu.py over rocprofv3 SQ counter passes of this workload, VALU issue costs measured
+    by tools/ubench_valu.hip): VALU instructions per env-step and per class, the SIMD issue cycles
+    they cost at the measured rates, and that issue time against this run's HIP-event kernel time
+    (frac = issue_bound_ms / avg_launch_ms: 1.0 = the SIMDs never stop issuing VALU), plus the
+    share of wave cycles parked on s_waitcnt / barriers (SQ_WAIT_ANY).  None when the committed
+    counters are for another shape."""
+    path = os.path.join(ROOT, "profiles", "pmc_valu.json")
+    if not os.path.exists(path):
+        return None
+    t = json.load(open(path))
+    if t.get("batch") != B or t.get("servers") != S:
+        return None
+    out = {"source": "profiles/pmc_valu.json", "simds": t["simds"], "clock_hz": t["clock_hz"],
+           "issue_costs_simd_cyc": t["ubench_simd_cyc_per_inst"]}
+    for full, rec in t["kernels"].items():
+        name = next((n for n in avg if full.startswith(n)), None)
+        if name is None:
+            continue
+        out[name] = {"pmc_kernel": full, "valu_per_env_step": rec["valu_per_env_step"],
+                     "classes_per_env_step": rec["classes_per_env_step"],
+                     "issue_bound_ms": rec["issue_bound_ms"], "avg_launch_ms": avg[name],
+                     "frac": rec["issue_bound_ms"] / avg[name],
+                     "wait_any_share": rec["wait_any_share"],
+                     "active_valu_per_simd_quad": rec["active_valu_per_simd_quad"]}
+    return out
+
+
 def step_accounting(handle, lib, one_step, steps: int, replay=None):
     """Reservoir slots written and flows in flight per step (lbsim_step_stats after each step).
     replay = (state bytes, restore-generator callable): rewind to the timed region's start and
@@ -457,6 +486,7 @@ def main():
         dom = max(avg, key=avg.get)
         ab = abytes[dom] * B
         achieved = ab / (avg[dom] * 1e-3) / 1e9
+        valu = valu_roofline(B, S, avg)
         traffic = None
         tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tfile):
@@ -488,7 +518,7 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "algorithmic_bytes_per_launch": ab,
                          "avg_launch_ms": avg[dom],
-                         "kernel_avg_ms": avg, "kernels": per_kernel,
+                         "kernel_avg_ms": avg, "kernels": per_kernel, "valu": valu,
                          "accounting": {"reservoir_slots_written_per_env_step": slots / B,
                                         "flows_in_flight_per_env": inflight / B,
                                         "basis": "lbsim_step_stats after each step of an exact "

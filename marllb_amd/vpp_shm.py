@@ -12,7 +12,7 @@ Byte-compatible with the reference's data plane and agent:
               (frame first, sequence id last), process_reservoir's features (lbsim_vpp_features)
 
 /dev/shm/shm_vip_<id> (1 MiB), packed from SHM_OFFSET = 42 (offsets pinned against the reference's
-own Shm_Manager.ptrs by tests/golden/vpp_shm.json):
+own Shm_Manager.ptrs by tests/golden/vpp_shm.npz):
 
     u8               n_as                  @ 42
     msg_out_t        msg_out_cache         @ 43      {u32 id, f32 ts, u64 b_header, as_stat_t[64]}  528 B
@@ -76,6 +76,13 @@ for _name, _dt, _n in LAYOUT:
 LAYOUT_END = _off
 assert LAYOUT_END <= SHM_SIZE
 
+# shm_proxy.py:22-23: the agent reads ./shm_layout.json; its "global" section is shm.h's defines
+CONF_FILE = "./shm_layout.json"
+GLOBAL_CONF = {"global": {"SHM_SIZE": SHM_SIZE, "SHM_OFFSET": SHM_OFFSET, "SHM_N_BIN": SHM_N_BIN,
+                          "SHM_N_FRAME": SHM_N_FRAME, "SHM_FRAME_MASK": SHM_FRAME_MASK,
+                          "VIP_ID": VIP_ID, "SHM_UPT_DT": SHM_UPT_DT,
+                          "RESERVOIR_N_BIN": RESERVOIR_N_BIN, "FILE_FMT": "/dev/shm/shm_vip_{}"}}
+
 # shm_proxy.py:151-155
 FEATURE_AS_CNT = ["n_flow_on"]
 FEATURE_AS_CNT_C: List[str] = []
@@ -105,6 +112,29 @@ def header_from_active(active: Sequence[int]) -> int:
 def _torch():
     import torch
     return torch
+
+
+def gen_alias(weights, device=None) -> List[Tuple[float, int]]:
+    """gen_alias (shm_proxy.py:127-146) of a list of weights > 0 -- what register_as_weights
+    hands it -- on the GPU (lbsim_alias_tables: the reference's float64 arithmetic on the float32
+    weights): [(odd, alias)] per weight, odd rounded to the float32 the wire carries."""
+    torch = _torch()
+    w = np.asarray(weights, np.float32).reshape(1, -1)
+    n = w.shape[1]
+    if n == 0:
+        return []
+    if n > _lib.MAX_SERVERS:
+        raise ValueError(f"at most {_lib.MAX_SERVERS} weights")
+    dev = torch.device(device if device is not None else "cuda")
+    wd = torch.from_numpy(w).to(dev)
+    odd = torch.empty((1, n), dtype=torch.float32, device=dev)
+    ali = torch.empty((1, n), dtype=torch.int32, device=dev)
+    act = torch.empty((1, n), dtype=torch.int32, device=dev)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    _lib.check(_lib.load().lbsim_alias_tables(
+        ctypes.c_void_p(wd.data_ptr()), 1, n, ctypes.c_void_p(odd.data_ptr()),
+        ctypes.c_void_p(ali.data_ptr()), ctypes.c_void_p(act.data_ptr()), stream))
+    return [(float(o), int(a)) for o, a in zip(odd.cpu().numpy()[0], ali.cpu().numpy()[0])]
 
 
 class VipShm:

@@ -277,3 +277,18 @@ def test_gpu_upstream_feature_mode(oracle_mod):
         ret += rg.cpu().numpy().astype(np.float64)
         np.testing.assert_allclose(info["episode_return"].cpu().numpy(), ret, rtol=1e-12)
     env.close()
+
+
+@pytest.mark.gpu
+def test_gpu_gen_alias_matches_reference_tables(golden_dir):
+    """vpp_shm.gen_alias (lbsim_alias_tables) equals the reference gen_alias tables recorded by
+    tests/golden/gen_golden.py (odd to float32, alias index exact)."""
+    import json
+    cases = json.load(open(os.path.join(golden_dir, "alias.json")))["cases"]
+    for c in cases[:40]:
+        w = c["weights"]
+        if not all(x > 0 for x in w):
+            continue
+        got = vs.gen_alias(w, device="cuda:0")
+        want = [(float(np.float32(o)), int(a)) for o, a in zip(c["odd"], c["alias"])]
+        assert got == want, w

@@ -12,8 +12,10 @@ the VALU issue micro-benchmark (ubench_valu.jsonl: SIMD cycles per instruction o
   issue_bound_ms          issue_cycles / (SIMDs x clock): the kernel's time if the SIMDs issued
                           VALU back to back at the measured rates
   wait_any_share          SQ_WAIT_ANY / SQ_WAVE_CYCLES (waves parked on s_waitcnt / barriers)
-  active_valu_per_simd_quad  SQ_ACTIVE_INST_VALU / (GRBM_GUI_ACTIVE / 4 x SIMDs): VALU
-                          quad-cycles per SIMD quad-cycle (the 'VALUBusy' basis, counted per SIMD)
+  active_valu_per_simd_quad  SQ_ACTIVE_INST_VALU / (GRBM_GUI_ACTIVE / 8 XCDs / 4 x SIMDs):
+                          VALU quad-cycles per SIMD quad-cycle (the 'VALUBusy' basis per SIMD;
+                          a SIMD dual-issues VALU from two waves, so the ceiling is 2, not 1).
+                          GRBM_GUI_ACTIVE comes summed over the 8 XCDs (8 x the kernel's cycles)
 
     python tools/pmc_valu.py gpurun_out/<tag> --batch 65536 --servers 4 [--out profiles/pmc_valu.json]
 """
@@ -25,6 +27,7 @@ import os
 
 CLOCK_HZ = 2.4e9  # MI355X peak engine clock (MI355X_MICROARCH.md)
 SIMDS = 1024      # 256 CUs x 4
+XCDS = 8
 
 # counter -> ubench_valu op whose measured throughput prices it
 PRICE = {"SQ_INSTS_VALU_INT32": "v_add_u32", "SQ_INSTS_VALU_ADD_F32": "v_fma_f32",
@@ -85,7 +88,12 @@ def main():
         c = {cn: mean(v) for (kn, cn), v in agg.items() if kn == k}
         if "SQ_INSTS_VALU" not in c:
             continue
-        # step-mode launches only (reset launches carry the warm-up): the name holds ", 0" MODE
+        # step-mode launches only (reset launches carry the warm-up): MODE is the second template
+        # argument of dynamics_group_kernel / dynamics_kernel / observe_kernel
+        if ("dynamics" in k or "observe" in k) and "<" in k:
+            targs = [x.strip() for x in k.split("<", 1)[1].rstrip(">").split(",")]
+            if len(targs) > 1 and targs[1] != "0":
+                continue
         cls = {n: c.get(n, 0.0) for n in PRICE if n != "other"}
         cls["other"] = max(0.0, c["SQ_INSTS_VALU"] - sum(cls.values()))
         cyc = 0.0
@@ -101,9 +109,10 @@ def main():
             "issue_bound_ms": cyc / (SIMDS * CLOCK_HZ) * 1e3,
             "wait_any_share": c.get("SQ_WAIT_ANY", float("nan")) / c.get("SQ_WAVE_CYCLES", float("nan")),
             "wait_inst_any_share": c.get("SQ_WAIT_INST_ANY", float("nan")) / c.get("SQ_WAVE_CYCLES", float("nan")),
-            "active_valu_per_simd_quad": c.get("SQ_ACTIVE_INST_VALU", float("nan")) / (gui / 4 * SIMDS),
+            "active_valu_per_simd_quad": c.get("SQ_ACTIVE_INST_VALU", float("nan")) / (gui / XCDS / 4 * SIMDS),
             "valu2_quads_share": c.get("SQ_ACTIVE_INST_VALU2", float("nan")) / c.get("SQ_ACTIVE_INST_VALU", float("nan")),
-            "gui_active_ms": gui / CLOCK_HZ * 1e3,
+            "gui_active_ms": gui / XCDS / CLOCK_HZ * 1e3,
+            "issue_frac_of_gui": cyc / (SIMDS * gui / XCDS),
             "counters": c,
         }
         out["kernels"][k] = rec

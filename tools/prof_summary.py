@@ -10,9 +10,12 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    for key in ("dynamics_kernel", "dynamics_group_kernel", "observe_kernel", "features_kernel", "reward_kernel"):
+    name = name.replace("(anonymous namespace)::", "")
+    for key in ("dynamics_kernel", "dynamics_group_kernel", "observe_kernel", "features_kernel",
+                "reward_kernel", "fused_step_kernel", "step_stats_kernel", "vpp_"):
         if key in name:
-            return name.split("(")[0].replace("void ", "").replace("lbk::", "")
+            return (name.split("(")[0].replace("void ", "").replace("lbk::", "")
+                    .replace("(anonymous namespace)::", ""))
     return name[:60]
 
 
