@@ -142,6 +142,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dyn-mapping", default="auto", choices=["auto", "env", "server"],
                     help="dynamics kernel mapping: one lane per env / per server (same results)")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="skip the graph leg (N=1: the same workload with one step captured in a "
+                         "hipGraph and replayed, reported beside `value` as `graph`)")
     ap.add_argument("--async-groups", type=int, default=0,
                     help="rollout workload at N=1: after the headline, also time the same rollout "
                          "as this many env groups (B / groups envs each, global ids kept), each "
@@ -299,6 +302,54 @@ def async_groups(args, dev, shard, B, S, common, groups):
     return {"groups": groups, "envs_per_group": b, "value": groups * b * args.steps / el,
             "unit": "env-steps/s", "ms_per_step": el / args.steps * 1e3,
             "streams": "one HIP stream per group, no cross-group join per step"}
+
+
+def graph_leg(args, dev, shard, B, S, common, kernel_ms):
+    """The same workload with one step captured into a torch.cuda.CUDAGraph (hipGraph) and
+    replayed: a fresh env in graph_mode (static buffers, the masked auto-reset launched every
+    step), the random policy's torch.randint (default generator, graph-safe) or the fused policy
+    kernel (Philox step counter on the device) inside the graph.  Same kernels and work per step
+    as the eager headline, without the per-launch host path; `gap_ms_per_step` = replayed
+    ms/step - the eager kernels' HIP-event averages = what the launches between the kernels
+    still cost.  Reported beside `value`, never as it."""
+    import torch
+    from marllb_amd.env import VecLoadBalanceEnv
+    common = dict(common, graph_mode=True)
+    if args.workload == "rollout":
+        env = VecLoadBalanceEnv(B, S, max_steps=10000, **common)
+        env.reset()
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                env.step(torch.randint(0, 3, (B, S), device=dev, dtype=torch.int64))
+        torch.cuda.current_stream(dev).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            env.step(torch.randint(0, 3, (B, S), device=dev, dtype=torch.int64))
+    elif args.workload == "sac-gru":
+        from marllb_amd.rollout import SACGRURollout
+        env = VecLoadBalanceEnv(B, S, action_type="continuous", max_steps=10000, **common)
+        g = SACGRURollout(env, seed=args.seed + shard.rank).capture()
+    else:
+        from marllb_amd.multi_agent import VecMultiAgentLoadBalanceEnv
+        from marllb_amd.rollout import QMIXRollout
+        env = VecMultiAgentLoadBalanceEnv(B, 4, S // 4, action_type="discrete", max_steps=100,
+                                          **common)
+        g = QMIXRollout(env, seed=args.seed + shard.rank).capture()
+    for _ in range(args.warmup):
+        g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        g.replay()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    env.close()
+    ms = el / args.steps * 1e3
+    return {"value": B * args.steps / el, "unit": "env-steps/s", "ms_per_step": ms,
+            "kernels_ms_per_step": kernel_ms, "gap_ms_per_step": ms - kernel_ms,
+            "form": "one step captured in a torch.cuda.CUDAGraph, replayed"}
 
 
 def late_episode(args, env, handle, lib, one_step, rate, B, S, done_steps):
@@ -547,6 +598,16 @@ def main():
                     "bound": "mfma", "avg_launch_ms": pms, "flops_per_launch": fl,
                     "achieved_TFLOPs": tf, "peak_TFLOPs": MFMA_F32_PEAK_TFLOPS,
                     "frac": tf / MFMA_F32_PEAK_TFLOPS}
+                # host + torch work between the launches (<= 10 us)
+                out["policy_glue_ms_per_step"] = out["policy_ms_per_step"] - pms
+        if world == 1 and not args.no_graph:
+            kms = sum(avg.values()) + (out["roofline"]["kernels"].get(
+                {"sac-gru": "sac_actor_kernel", "qmix": "qmix_policy_kernel"}.get(
+                    args.workload, ""), {}).get("avg_launch_ms", 0.0))
+            try:
+                out["graph"] = graph_leg(args, dev, shard, B, S, common, kms)
+            except Exception as e:  # reported, never fatal to the headline line
+                out["graph"] = {"error": f"{type(e).__name__}: {e}"}
         if world == 1 and args.workload == "rollout" and args.late_episode:
             out["late_episode"] = late_episode(args, env, handle, lib, one_step, rate, B, S,
                                                args.warmup + args.steps)

@@ -10,7 +10,9 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblbsim.so")
+# LBSIM_LIBRARY: an alternative build of the same ABI (the A/B variants of
+# `python -m marllb_amd.build --variant NAME -DMACRO`, marllb_amd/exp/liblbsim_NAME.so)
+LIB_PATH = os.environ.get("LBSIM_LIBRARY") or os.path.join(_HERE, "liblbsim.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "lbsim.h")
 
 MAX_SERVERS = 64

@@ -47,8 +47,7 @@ def up_to_date() -> bool:
 
 
 def _compile(unit, verbose: bool) -> str:
-    src, defs, obj = unit
-    out = os.path.join(OBJDIR, obj)
+    src, defs, out = unit
     cmd = [hipcc(), *FLAGS, *defs, "-c", "-o", out + ".tmp", os.path.join(CSRC, src)]
     if verbose:
         print(" ".join(cmd), flush=True)
@@ -57,20 +56,32 @@ def _compile(unit, verbose: bool) -> str:
     return out
 
 
-def build_library(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
-    if not force and up_to_date():
+def build_library(force: bool = False, verbose: bool = False, jobs: int = 0,
+                  variant: str | None = None, defines: tuple = ()) -> str:
+    """Build liblbsim.so, or with `variant` an A/B build with extra `defines` into
+    marllb_amd/exp/liblbsim_<variant>.so (loaded through LBSIM_LIBRARY, see _lib.py)."""
+    out, objdir = OUT, OBJDIR
+    if variant:
+        out = os.path.join(HERE, "exp", f"liblbsim_{variant}.so")
+        objdir = os.path.join(ROOT, "build", f"lbsim_{variant}")
+    elif not force and up_to_date():
         return OUT
-    os.makedirs(OBJDIR, exist_ok=True)
+    os.makedirs(objdir, exist_ok=True)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     jobs = jobs or min(len(UNITS), os.cpu_count() or 1, 16)
+    units = [(src, [*defs, *defines], os.path.join(objdir, obj)) for src, defs, obj in UNITS]
     with ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda u: _compile(u, verbose), UNITS))
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs]
+        objs = list(ex.map(lambda u: _compile(u, verbose), units))
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp", *objs]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build_library(force="--force" in sys.argv, verbose=True))
+    args = sys.argv[1:]
+    variant = args[args.index("--variant") + 1] if "--variant" in args else None
+    defines = tuple(a for a in args if a.startswith("-D"))
+    print(build_library(force="--force" in args, verbose=True, variant=variant, defines=defines))

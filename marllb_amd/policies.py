@@ -242,11 +242,23 @@ class FusedGRUPolicy:
         self.wh, self.bh = self._heads()
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         self.step_no = 0
+        self.step_dev = None
         self.kernel = None
         if (kernel and self.w_ih.is_cuda and policy.gru_dim == 128 and policy.hidden_dim == 256
                 and policy.action_dim <= 16 and policy.state_dim <= 512):
             self.kernel = self._pack()
         self._watch = _ParamWatch([policy])
+
+    def use_device_step(self) -> None:
+        """Keep the Philox step counter on the device (lbsim_sac_actor_t.step_dev), advanced by a
+        tiny kernel after each launch: a captured call replays with a new step each time, drawing
+        exactly what the eager calls would.  Needs the one-launch kernel form."""
+        if self.kernel is None:
+            raise ValueError("use_device_step needs the lbsim_sac_actor_step kernel form")
+        if self.step_dev is None:
+            self.step_dev = torch.tensor([self.step_no & 0x7FFFFFFF], dtype=torch.int32,
+                                         device=self.w_ih.device)
+            self.kernel.step_dev = self.step_dev.data_ptr()
 
     def _heads(self):
         p = self.p
@@ -297,6 +309,8 @@ class FusedGRUPolicy:
                 ctypes.byref(self.kernel), _ptr(x), _ptr(h), _ptr(mask), B, int(deterministic),
                 self.seed, self.step_no & 0xFFFFFFFF, _ptr(action), _ptr(log_std), stream)))
             self.step_no += 1
+            if self.step_dev is not None:
+                self.step_dev.add_(1)
             return action, h, log_std
         h0 = hidden if mask is None else hidden * (~mask.bool()).unsqueeze(1).to(hidden.dtype)
         gi = torch.addmm(self.b_ih, state, self.w_ih.t())

@@ -46,6 +46,24 @@ class SACGRURollout:
             return self._h
         return self._h * (~self._reset).view(1, -1, 1).to(self._h.dtype)
 
+    def capture(self, warmup: int = 2) -> "torch.cuda.CUDAGraph":
+        """One step() captured into a torch.cuda.CUDAGraph (as QMIXRollout.capture): needs the
+        one-launch actor kernel and an env in graph_mode; `warmup` eager steps first on a side
+        stream, then g.replay() == step() on the same static buffers (self.obs, self.last)."""
+        if self.fused is None or self.fused.kernel is None or not self.env.graph_mode:
+            raise ValueError("capture needs the fused SAC actor kernel and graph_mode=True")
+        self.fused.use_device_step()
+        side = torch.cuda.Stream(self.env.device)
+        side.wait_stream(torch.cuda.current_stream(self.env.device))
+        with torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):
+                self.step()
+        torch.cuda.current_stream(self.env.device).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.last = self.step()
+        return g
+
     @torch.no_grad()
     def step(self):
         B = self.env.num_envs

@@ -135,3 +135,35 @@ def test_qmix_rollout_graph_capture_replays_bit_exact():
     for k, (a, b) in enumerate(zip(*outs)):
         for x, y in zip(a, b):
             assert torch.equal(x, y), k
+
+
+def test_sac_rollout_graph_capture_replays_bit_exact():
+    """One SACGRURollout.step -- the one-launch SAC-GRU actor (Philox step counter on the device,
+    hidden state updated in place, finished envs restarted from h = 0) and the env step -- captured
+    and replayed equals the eager rollout bit for bit across episode ends (max_steps 3)."""
+    from marllb_amd import VecLoadBalanceEnv
+    from marllb_amd.rollout import SACGRURollout
+    B, S, T = 512, 8, 3
+    outs = []
+    for graph_mode in (False, True):
+        torch.manual_seed(0)
+        env = VecLoadBalanceEnv(B, S, device="cuda:0", seed=5, action_type="continuous",
+                                max_steps=T, graph_mode=graph_mode)
+        ro = SACGRURollout(env, seed=3)
+        seq = []
+        if graph_mode:
+            cg = ro.capture(warmup=2)
+            for _ in range(3 * T):
+                cg.replay()
+                rew, done, _ = ro.last
+                seq.append((rew.clone(), done.clone(), ro.obs.clone(), ro._h.clone()))
+        else:
+            for _ in range(2 + 3 * T):
+                rew, done, _ = ro.step()
+                seq.append((rew.clone(), done.clone(), ro.obs.clone(), ro._h.clone()))
+            seq = seq[2:]
+        outs.append(seq)
+        env.close()
+    for k, (a, b) in enumerate(zip(*outs)):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y), k

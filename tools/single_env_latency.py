@@ -29,6 +29,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--servers", type=int, default=4)
+    ap.add_argument("--dyn-mapping", default="auto", choices=["auto", "env", "server"])
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -38,13 +39,14 @@ def main():
     rng = np.random.default_rng(0)
     disc = [rng.integers(0, 3, S) for _ in range(256)]
     cont = [rng.uniform(-1, 1, S).astype(np.float32) for _ in range(256)]
-    out = {"servers": S, "steps": args.steps, "unit": "us/step"}
+    out = {"servers": S, "steps": args.steps, "unit": "us/step", "dyn_mapping": args.dyn_mapping}
+    dm = {"dyn_mapping": args.dyn_mapping}
     if torch.cuda.is_available():
         out["gpu_discrete"] = timed(LoadBalanceEnv(num_servers=S, max_steps=10**9, seed=1,
-                                                   step_interval=0.0), disc, args.steps)
+                                                   step_interval=0.0, **dm), disc, args.steps)
         out["gpu_continuous_normalized"] = timed(
             LoadBalanceEnv(num_servers=S, action_type="continuous", normalize_obs=True,
-                           max_steps=10**9, seed=1, step_interval=0.0), cont, args.steps)
+                           max_steps=10**9, seed=1, step_interval=0.0, **dm), cont, args.steps)
     out["reference_plumbing_host"] = timed(
         LoadBalanceEnv(num_servers=S, max_steps=10**9, seed=1, step_interval=0.0,
                        reference_plumbing=True), disc, args.steps)
