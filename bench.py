@@ -83,12 +83,18 @@ def valu_roofline(B: int, S: int, avg: dict):
 
 def step_accounting(handle, lib, one_step, steps: int, replay=None):
     """Reservoir slots written and flows in flight per step (lbsim_step_stats after each step).
-    replay = (state bytes, restore-generator callable): rewind to the timed region's start and
-    re-run exactly its steps; else `steps` more steps of the same trajectory."""
+    replay = (twin factory, warm-up steps): the factory builds a second env from the same seeds
+    and config with its own action generator (same seed), which walks the same trajectory bit for
+    bit; its warm-up steps run uncounted, then exactly the timed steps are counted.  (A 0.5 GB
+    state snapshot taken in the timed process slowed the timed steps by 1-3.5 %,
+    profiles/r03/regress_r02_r03.txt.)  Else `steps` more steps of the same trajectory."""
     import torch
+    twin = None
     if replay is not None:
-        handle.load_state(replay[0])
-        replay[1]()
+        twin, one_step = replay[0]()
+        handle = twin.handle
+        for _ in range(replay[1]):
+            one_step()
     st = (ctypes.c_int64 * 2)()
     slots = flows = 0
     for _ in range(steps):
@@ -97,6 +103,8 @@ def step_accounting(handle, lib, one_step, steps: int, replay=None):
         handle.check(lib.lbsim_step_stats(handle.h, st))
         slots += st[0]
         flows += st[1]
+    if twin is not None:
+        twin.close()
     return slots / steps, flows / steps
 
 
@@ -486,6 +494,19 @@ def main():
         def one_step():
             ro.step()
 
+    replay = None
+    if args.workload == "rollout" and rank == 0:  # exact accounting replay of warm-up + timed steps
+
+        def twin():
+            e2 = VecLoadBalanceEnv(B, S, max_steps=10000, **common)
+            e2.reset()
+            g2 = torch.Generator(device=dev)
+            g2.manual_seed(args.seed + rank)
+
+            def step2():
+                e2.step(torch.randint(0, 3, (B, S), device=dev, dtype=torch.int64, generator=g2))
+            return e2, step2
+        replay = (twin, args.warmup)
     for _ in range(args.warmup):
         one_step()
     torch.cuda.synchronize()
@@ -493,10 +514,6 @@ def main():
         dist.barrier()
     lib = _lib.load()
     from marllb_amd import policies
-    replay = None
-    if args.workload == "rollout" and rank == 0:  # exact accounting replay of the timed steps
-        gstate = gen.get_state()
-        replay = (handle.state_bytes(), lambda: gen.set_state(gstate))
     if args.workload != "rollout":  # HIP events around each fused policy launch
         policies.profile_events = []
     handle.check(lib.lbsim_profile_begin(handle.h, 4 * args.steps + 8))

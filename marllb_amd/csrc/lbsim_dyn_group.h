@@ -430,9 +430,10 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
 template <int POLICY>
 struct DynGroupLds {
   int2 win[kGroupWL * 64];                          // queue windows, [slot][lane]
-  int32_t atab[POLICY == kPolicyAlias ? 2 * 64 : 1];  // ALIAS tables, [word][lane]
   int4 acache[64];                                  // draw-ahead arrival slots, [group][G]
   uint32_t chgw[4 * 64];                            // written-slot masks, [word][lane]
+  int32_t atab[POLICY == kPolicyAlias ? 2 * 64 : 1];  // ALIAS tables, [word][lane] (last: the
+                                                      // others keep their 16-B aligned offsets)
 };
 
 // One step (or reset) of the 64 / G envs of wave `wave` (env b = wave * 64 / G + lane / G), lane s

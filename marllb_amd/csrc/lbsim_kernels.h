@@ -1909,7 +1909,7 @@ constexpr int kObsWavesPerEnv = MAXS <= kObsChunk ? 1 : MAXS / kObsChunk;
 // The reward, episode bookkeeping and output rows of env b once its (S, 11) rows are in s_obs
 // (rewards.py:290-381, env.py:261-281, env.py:450-470): threads tid < 64 (one wave) compute the
 // reward, all nthr threads write the rows.
-template <int MAXS, int MODE>
+template <int MAXS, int MODE, bool FAC>
 __device__ __forceinline__ void observe_outputs(const DevState& st, const SimParams& p,
                                                 const ObsOutputs& out, size_t b,
                                                 float* s_obs, float* s_act, int tid, int nthr) {
@@ -1929,7 +1929,8 @@ __device__ __forceinline__ void observe_outputs(const DevState& st, const SimPar
       const int na = __popcll(act_mask);
       double r = 0.0;
       if (fok) {
-        if (S <= kObsChunk && p.reward_metric == 0)  // (observe_kernel<4>; fused G = 8, S <= 4)
+        // (compile-time for observe_kernel<4>; fused G = 8 with S <= 4 at run time)
+        if ((MAXS <= kObsChunk || S <= kObsChunk) && p.reward_metric == 0)
           r = jain_upto4(na, s_act);
         else
           r = reward_values(na, [&](int i) { return (double)s_act[i]; }, p.reward_metric);
@@ -1947,7 +1948,9 @@ __device__ __forceinline__ void observe_outputs(const DevState& st, const SimPar
 
   const int nobs = S * NF;
   float* orow = out.obs + b * (size_t)nobs;
-  const bool facade = out.agent_obs != nullptr || out.state != nullptr;
+  // FAC: the launch writes the problem-05 facade rows (a separate instantiation, so the plain
+  // step carries none of that code)
+  const bool facade = FAC && (out.agent_obs != nullptr || out.state != nullptr);
   if (out.raw_obs != nullptr)
     for (int e = tid; e < nobs; e += nthr) out.raw_obs[b * (size_t)nobs + e] = s_obs[e];
   if (p.normalize) {  // env.py:460-468, float64 running statistics
@@ -1999,7 +2002,7 @@ __device__ __forceinline__ void observe_outputs(const DevState& st, const SimPar
   }
 }
 
-template <int MAXS, int MODE>
+template <int MAXS, int MODE, bool FAC>
 __global__ void __launch_bounds__(64 * kObsWavesPerEnv<MAXS>, 5)
     observe_kernel(DevState st, SimParams p, ObsOutputs out, const uint8_t* reset_mask) {
   constexpr int mode = MODE;
@@ -2017,7 +2020,7 @@ __global__ void __launch_bounds__(64 * kObsWavesPerEnv<MAXS>, 5)
                                            sc, s_obs, lane);
   }
   __syncthreads();
-  observe_outputs<MAXS, MODE>(st, p, out, b, s_obs, s_act, tid, nthr);
+  observe_outputs<MAXS, MODE, FAC>(st, p, out, b, s_obs, s_act, tid, nthr);
 }
 
 // observe_kernel's work for env b by ONE wave, its chunks in sequence (fused_step_kernel's second
@@ -2030,7 +2033,7 @@ __device__ __forceinline__ void observe_env_wave(const DevState& st, const SimPa
   for (int s0 = 0; s0 < S; s0 += kObsChunk)
     observe_chunk<true, true>(st, p, b, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk, sc, s_obs,
                               lane);
-  observe_outputs<MAXS, kModeStep>(st, p, out, b, s_obs, s_act, lane, 64);
+  observe_outputs<MAXS, kModeStep, true>(st, p, out, b, s_obs, s_act, lane, 64);
   wave_sync();  // s_obs / s_act reused by the next env
 }
 

@@ -5,7 +5,7 @@
 namespace lbk {
 namespace {
 
-template <int MODE>
+template <int MODE, bool FAC>
 void launch_observe_t(const LaunchCtx& L, const ObsOutputs& o, const uint8_t* mask,
                       hipStream_t stream) {
   const int nw = (L.S + kObsChunk - 1) / kObsChunk;
@@ -13,30 +13,44 @@ void launch_observe_t(const LaunchCtx& L, const ObsOutputs& o, const uint8_t* ma
   const size_t lds = (size_t)nw * sizeof(ObsScratch);
   if (lds > 65536) {  // S > 32: 9-16 chunk waves
     static const bool ok = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&observe_kernel<64, MODE>),
+        reinterpret_cast<const void*>(&observe_kernel<64, MODE, FAC>),
         hipFuncAttributeMaxDynamicSharedMemorySize, 16 * (int)sizeof(ObsScratch)) == hipSuccess;
     (void)ok;
   }
   if (L.S <= 4)
-    hipLaunchKernelGGL((observe_kernel<4, MODE>), grid, block, lds, stream, L.st, L.prm, o, mask);
+    hipLaunchKernelGGL((observe_kernel<4, MODE, FAC>), grid, block, lds, stream, L.st, L.prm, o,
+                       mask);
   else if (L.S <= 8)
-    hipLaunchKernelGGL((observe_kernel<8, MODE>), grid, block, lds, stream, L.st, L.prm, o, mask);
+    hipLaunchKernelGGL((observe_kernel<8, MODE, FAC>), grid, block, lds, stream, L.st, L.prm, o,
+                       mask);
   else if (L.S <= 16)
-    hipLaunchKernelGGL((observe_kernel<16, MODE>), grid, block, lds, stream, L.st, L.prm, o, mask);
+    hipLaunchKernelGGL((observe_kernel<16, MODE, FAC>), grid, block, lds, stream, L.st, L.prm, o,
+                       mask);
   else
-    hipLaunchKernelGGL((observe_kernel<64, MODE>), grid, block, lds, stream, L.st, L.prm, o, mask);
+    hipLaunchKernelGGL((observe_kernel<64, MODE, FAC>), grid, block, lds, stream, L.st, L.prm, o,
+                       mask);
+}
+
+// the problem-05 facade rows (agent_obs / state) come from their own instantiation
+template <int MODE>
+void launch_observe_m(const LaunchCtx& L, const ObsOutputs& o, const uint8_t* mask,
+                      hipStream_t stream) {
+  if (o.agent_obs != nullptr || o.state != nullptr)
+    launch_observe_t<MODE, true>(L, o, mask, stream);
+  else
+    launch_observe_t<MODE, false>(L, o, mask, stream);
 }
 
 }  // namespace
 
 void launch_observe_step(const LaunchCtx& L, const ObsOutputs& o, const uint8_t* mask,
                          hipStream_t s) {
-  launch_observe_t<kModeStep>(L, o, mask, s);
+  launch_observe_m<kModeStep>(L, o, mask, s);
 }
 
 void launch_observe_reset(const LaunchCtx& L, const ObsOutputs& o, const uint8_t* mask,
                           hipStream_t s) {
-  launch_observe_t<kModeReset>(L, o, mask, s);
+  launch_observe_m<kModeReset>(L, o, mask, s);
 }
 
 }  // namespace lbk
