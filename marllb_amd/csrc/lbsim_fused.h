@@ -68,18 +68,36 @@ __device__ __forceinline__ void mma_tile(f4 (&acc)[MT], const float* lds, int ld
   }
 }
 
+// The first two k-blocks' B fragments of NB tiles, loaded ahead of mma_multi: a caller issues
+// them before the barrier that precedes the layer, so their L2 latency overlaps the wait.
+template <int NB>
+struct BPrime {
+  f4 b0[NB], b1[NB];
+};
+template <int NB>
+__device__ __forceinline__ BPrime<NB> mma_prime(const f4* const (&wp)[NB], int nkb, int lane) {
+  BPrime<NB> bp;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    bp.b0[j] = wp[j][lane];
+    bp.b1[j] = wp[j][(nkb > 1 ? 64 : 0) + lane];
+  }
+  return bp;
+}
+
 // NB output tiles over the same input columns in one pipelined loop: the A fragments are read
 // once per block for all of them, and NB x MT independent accumulator chains keep the MFMA pipe
 // busy even at MT = 1 (a single chain waits out the 40-cycle dependent latency every MFMA).
 template <int MT, int NB>
 __device__ __forceinline__ void mma_multi(f4 (&acc)[NB][MT], const float* lds, int ld, int col0,
-                                          const f4* const (&wp)[NB], int nkb, int lane) {
+                                          const f4* const (&wp)[NB], int nkb, int lane,
+                                          const BPrime<NB>& bp) {
   const float* arow = lds + (lane & 15) * ld + col0 + 4 * (lane >> 4);
   f4 b0[NB], b1[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    b0[j] = wp[j][lane];
-    b1[j] = wp[j][(nkb > 1 ? 64 : 0) + lane];
+    b0[j] = bp.b0[j];
+    b1[j] = bp.b1[j];
   }
   f4 a[MT];
 #pragma unroll
@@ -108,6 +126,11 @@ __device__ __forceinline__ void mma_multi(f4 (&acc)[NB][MT], const float* lds, i
       b1[j] = b2[j];
     }
   }
+}
+template <int MT, int NB>
+__device__ __forceinline__ void mma_multi(f4 (&acc)[NB][MT], const float* lds, int ld, int col0,
+                                          const f4* const (&wp)[NB], int nkb, int lane) {
+  mma_multi<MT, NB>(acc, lds, ld, col0, wp, nkb, lane, mma_prime<NB>(wp, nkb, lane));
 }
 
 // Dense layer, accumulate phase: wave w owns output tiles nt = w, w + 4, ... < ntiles, all in
@@ -356,6 +379,7 @@ struct QmixArgs {
   int64_t B;
   int A, I, kxp, Ds, ksp, ld, n_act, k, he, E;
   int lda;  // qmix_agent_wave_kernel: row stride of a wave's own [16][lda] agent region
+  int sld;  // qmix_agent_pair_kernel: row stride of its prefetched [16][sld] state rows
   float epsilon;
   uint32_t key0, key1, step;
   const uint32_t* step_dev;  // when set, the Philox step counter is *step_dev (graph replays)
@@ -370,20 +394,27 @@ struct QmixMixAct {
 
 // QMixingNetwork.forward (mixing_network.py:78-117) of the tile, all 4 waves, after the agents:
 // chosen[R][A] holds the chosen Q-values; the LDS tile [R][p.ld] is free.
+// pre: the state rows already staged (qmix_agent_pair_kernel loads them at its start, so their
+// HBM latency hides behind the agents), [R][pre_ld]; else they are staged here.
 template <int MT>
 __device__ __forceinline__ void qmix_mixer(const QmixArgs& p, float* lds, const float* chosen,
-                                           int64_t row0, int wave, int lane) {
+                                           int64_t row0, int wave, int lane,
+                                           const float* pre = nullptr, int pre_ld = 0) {
   constexpr int R = 16 * MT;
   const int ld = p.ld, A = p.A;
-  stage_rows(lds, ld, 0, p.state, p.Ds, p.Ds, p.ksp, R, row0, p.B, nullptr);
-  __syncthreads();
+  if (pre == nullptr) {
+    stage_rows(lds, ld, 0, p.state, p.Ds, p.Ds, p.ksp, R, row0, p.B, nullptr);
+    __syncthreads();
+  }
+  const float* x0 = pre != nullptr ? pre : lds;
+  const int x0_ld = pre != nullptr ? pre_ld : ld;
   const int he = p.he, E = p.E;
   const bool mw = wave < 4;  // the mixer's GEMMs run on waves 0-3 (8-wave workgroups: the others
                              // only meet the barriers)
   {
     const int nt0 = (3 * he + E) / 16;  // <= 16
     f4 acc[4][MT];
-    if (mw) dense_acc<MT, 4>(acc, lds, ld, 0, p.m0, p.ksp / 16, nt0, p.mb0, wave, lane);
+    if (mw) dense_acc<MT, 4>(acc, x0, x0_ld, 0, p.m0, p.ksp / 16, nt0, p.mb0, wave, lane);
     __syncthreads();
     if (mw) dense_store<MT, 4>(acc, lds, ld, 0, nt0, wave, lane, QmixMixAct{3 * he});
   }
@@ -673,8 +704,29 @@ __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
   float* qv = lds + 4 * R * lda;    // [A][R][16]
   float* chosen = qv + A * R * 16;  // [R][A]
   float* part = chosen + R * A;     // [A][R][16] fc3 partials of the h = 1 waves
+  float* pre = part + A * R * 16;   // [R][p.sld] the mixer's state rows, staged now
   const int kbx = kxp / 16;
   const int t2 = lane + 64 * h;     // the pair's 128 threads
+  const f4* wi = (const f4*)(p.w_ih + (size_t)a * 3 * H * kxp);
+  const f4* wh = (const f4*)(p.w_hh + (size_t)a * 3 * H * H);
+  auto gru_wx = [&](int u, const f4* (&wx)[3]) {
+    wx[0] = wi + (size_t)(2 * UT + u) * kbx * 64;
+    wx[1] = wi + (size_t)u * kbx * 64;
+    wx[2] = wi + (size_t)(UT + u) * kbx * 64;
+  };
+  // the first GRU pass's weights, the epsilon-greedy draw (independent of the network) and the
+  // mixer's state rows go out first: their latency hides behind the staging
+  BPrime<3> bp_gru;
+  {
+    const f4* wx[3];
+    gru_wx(h, wx);
+    bp_gru = mma_prime<3>(wx, kbx, lane);
+  }
+  u32x4 eps_d{};
+  if (h == 0 && lane < R)
+    eps_d = philox4x32_10(u32x4{(uint32_t)(row0 + lane), step, (uint32_t)a, 4u << 24}, p.key0,
+                          p.key1);
+  stage_rows(pre, p.sld, 0, p.state, p.Ds, p.Ds, p.ksp, R, row0, p.B, nullptr);
   for (int e = t2; e < R * kxp; e += 128) {  // obs rows of agent a, zero padded
     const int r = e / kxp, c = e - r * kxp;
     const int64_t b = row0 + r;
@@ -687,8 +739,6 @@ __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
     mine[r * lda + kxp + c] = live ? p.hidden[(b * A + a) * H + c] : 0.0f;
   }
   __syncthreads();
-  const f4* wi = (const f4*)(p.w_ih + (size_t)a * 3 * H * kxp);
-  const f4* wh = (const f4*)(p.w_hh + (size_t)a * 3 * H * H);
   const float* bi = p.b_ih + a * 3 * H;
   const float* bh = p.b_hh + a * 3 * H;
   f4 hn[UT / 2][1];
@@ -701,11 +751,12 @@ __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
     g[1][0] = splat4(bi[col] + bh[col]);
     g[2][0] = splat4(bi[H + col] + bh[H + col]);
     g[3][0] = splat4(bh[2 * H + col]);
-    const f4* const wx[3] = {wi + (size_t)(2 * UT + u) * kbx * 64, wi + (size_t)u * kbx * 64,
-                             wi + (size_t)(UT + u) * kbx * 64};
+    const f4* wx[3];
+    gru_wx(u, wx);
     const f4* const wy[3] = {wh + (size_t)u * UT * 64, wh + (size_t)(UT + u) * UT * 64,
                              wh + (size_t)(2 * UT + u) * UT * 64};
-    mma_multi<1, 3>(*reinterpret_cast<f4(*)[3][1]>(&g[0]), mine, lda, 0, wx, kbx, lane);
+    mma_multi<1, 3>(*reinterpret_cast<f4(*)[3][1]>(&g[0]), mine, lda, 0, wx, kbx, lane,
+                    uu == 0 ? bp_gru : mma_prime<3>(wx, kbx, lane));
     mma_multi<1, 3>(*reinterpret_cast<f4(*)[3][1]>(&g[1]), mine, lda, kxp, wy, UT, lane);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -715,6 +766,21 @@ __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
       const float n = tanhf(g[0][0][i] + r * g[3][0][i]);
       hn[uu][0][i] = (1.0f - z) * n + z * hp;
     }
+  }
+  // fc1 / fc2: this wave's NT / 2 = 4 tiles of a layer in one mma_multi pass; a layer's first
+  // weights are requested before the barrier that precedes it
+  static_assert(NT / 2 == 4, "one four-tile pass per layer");
+  auto fc_wp = [&](int layer, const f4* (&wp)[4]) {
+    const float* w = layer == 0 ? p.w1 + (size_t)a * F * H : p.w2 + (size_t)a * F * F;
+    const int nkb = layer == 0 ? H / 16 : F / 16;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wp[j] = (const f4*)w + (size_t)(h * (NT / 2) + j) * nkb * 64;
+  };
+  BPrime<4> bp_fc;
+  {
+    const f4* wp[4];
+    fc_wp(0, wp);
+    bp_fc = mma_prime<4>(wp, H / 16, lane);
   }
   __syncthreads();  // both halves have read the old hidden state
 #pragma unroll
@@ -726,27 +792,24 @@ __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
       if (row0 + r < p.B) p.hidden[((row0 + r) * A + a) * H + col] = hn[uu][0][i];
     }
   __syncthreads();
-  // fc1 (H -> F) then fc2 (F -> F), ReLU: this wave's NT / 2 tiles, four per mma_multi pass
 #pragma unroll
-  for (int layer = 0; layer < 2; ++layer) {
+  for (int layer = 0; layer < 2; ++layer) {  // fc1 (H -> F) then fc2 (F -> F), ReLU
     const int col0 = layer == 0 ? kxp : 0, nkb = layer == 0 ? H / 16 : F / 16;
-    const float* w = layer == 0 ? p.w1 + (size_t)a * F * H : p.w2 + (size_t)a * F * F;
     const float* bias = (layer == 0 ? p.b1 : p.b2) + a * F;
-    f4 acc[NT / 2][1];
+    f4 acc[4][1];
+    const f4* wp[4];
+    fc_wp(layer, wp);
 #pragma unroll
-    for (int t0 = 0; t0 < NT / 2; t0 += 4) {
-      const f4* wp[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int t = h * (NT / 2) + t0 + j;
-        wp[j] = (const f4*)w + (size_t)t * nkb * 64;
-        acc[t0 + j][0] = splat4(bias[t * 16 + (lane & 15)]);
-      }
-      mma_multi<1, 4>(*reinterpret_cast<f4(*)[4][1]>(&acc[t0]), mine, lda, col0, wp, nkb, lane);
+    for (int j = 0; j < 4; ++j) acc[j][0] = splat4(bias[(h * (NT / 2) + j) * 16 + (lane & 15)]);
+    mma_multi<1, 4>(acc, mine, lda, col0, wp, nkb, lane, bp_fc);
+    if (layer == 0) {
+      const f4* wn[4];
+      fc_wp(1, wn);
+      bp_fc = mma_prime<4>(wn, F / 16, lane);
     }
     __syncthreads();
 #pragma unroll
-    for (int t = 0; t < NT / 2; ++t)
+    for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float v = acc[t][0][i];
@@ -779,8 +842,7 @@ __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
     int g = 0;
     for (int j = 1; j < NQ; ++j)
       if (q[j] > q[g]) g = j;
-    const u32x4 d = philox4x32_10(u32x4{(uint32_t)b, step, (uint32_t)a, 4u << 24}, p.key0,
-                                  p.key1);
+    const u32x4 d = eps_d;  // drawn at the start
     const float u = (float)(d.x >> 8) * 5.9604644775390625e-8f;
     const int act = u < p.epsilon ? (int)(((uint64_t)d.y * (uint32_t)NQ) >> 32) : g;
     chosen[r * A + a] = q[act];
@@ -794,7 +856,7 @@ __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
     }
   }
   __syncthreads();
-  qmix_mixer<1>(p, lds, chosen, row0, wave, lane);
+  qmix_mixer<1>(p, lds, chosen, row0, wave, lane, pre, p.sld);
 }
 
 }  // namespace lbk
