@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-launch VALU accounting of the simulator kernels from a tools/gpu_pmc_r03.sh run.
+"""Per-launch VALU accounting of the simulator kernels from a tools/gpu_pmc.sh run.
 
 SQ counters (sq1, sq2: totals, wave cycles, waits; vc1, vc2: VALU instructions per op class) and
 the VALU issue micro-benchmark (ubench_valu.jsonl: SIMD cycles per instruction of each class with
