@@ -787,9 +787,12 @@ int lbsim_qmix_policy_step(const lbsim_qmix_policy_t* n, const float* obs, float
   if (mt == 1 && form != 0) {  // one or two waves per agent, 16 envs per workgroup
     a.lda = fused_ld(std::max(a.kxp + 64, 128));
     if (form == 2 && A == 4) {  // two waves per agent: 8-wave workgroups
-      a.sld = fused_ld(a.ksp);    // + the mixer's state rows, staged at the start
-      const size_t lds = ((size_t)4 * 16 * a.lda + 2 * (size_t)A * 16 * 16 + 16 * (size_t)A +
-                          16 * (size_t)a.sld) * 4;
+      // + the mixer's state rows, staged at the start when they fit (a.sld = 0: staged by the
+      // mixer, as the other forms)
+      const size_t base = ((size_t)4 * 16 * a.lda + 2 * (size_t)A * 16 * 16 + 16 * (size_t)A) * 4;
+      a.sld = fused_ld(a.ksp);
+      if (base + (size_t)16 * a.sld * 4 > kFusedLdsMax) a.sld = 0;
+      const size_t lds = base + (size_t)16 * a.sld * 4;
       if (a.ld > 4 * a.lda || lds > kFusedLdsMax) return LBSIM_ENOTSUP;
       return launch_qmix_policy(a, B, 2, 1, lds, s);
     }

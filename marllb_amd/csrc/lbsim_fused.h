@@ -704,7 +704,7 @@ __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
   float* qv = lds + 4 * R * lda;    // [A][R][16]
   float* chosen = qv + A * R * 16;  // [R][A]
   float* part = chosen + R * A;     // [A][R][16] fc3 partials of the h = 1 waves
-  float* pre = part + A * R * 16;   // [R][p.sld] the mixer's state rows, staged now
+  float* pre = part + A * R * 16;   // [R][p.sld] the mixer's state rows, staged now (sld > 0)
   const int kbx = kxp / 16;
   const int t2 = lane + 64 * h;     // the pair's 128 threads
   const f4* wi = (const f4*)(p.w_ih + (size_t)a * 3 * H * kxp);
@@ -726,7 +726,7 @@ __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
   if (h == 0 && lane < R)
     eps_d = philox4x32_10(u32x4{(uint32_t)(row0 + lane), step, (uint32_t)a, 4u << 24}, p.key0,
                           p.key1);
-  stage_rows(pre, p.sld, 0, p.state, p.Ds, p.Ds, p.ksp, R, row0, p.B, nullptr);
+  if (p.sld > 0) stage_rows(pre, p.sld, 0, p.state, p.Ds, p.Ds, p.ksp, R, row0, p.B, nullptr);
   for (int e = t2; e < R * kxp; e += 128) {  // obs rows of agent a, zero padded
     const int r = e / kxp, c = e - r * kxp;
     const int64_t b = row0 + r;
@@ -856,7 +856,7 @@ __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
     }
   }
   __syncthreads();
-  qmix_mixer<1>(p, lds, chosen, row0, wave, lane, pre, p.sld);
+  qmix_mixer<1>(p, lds, chosen, row0, wave, lane, p.sld > 0 ? pre : nullptr, p.sld);
 }
 
 }  // namespace lbk

@@ -162,6 +162,31 @@ def test_qmix_policy_kernel_matches_modules(g):
 
 
 @pytest.mark.gpu
+def test_qmix_policy_kernel_wide_obs_matches_modules():
+    """configs[4] literal: 4 agents x 16 servers (agent obs 4 k + 7 S = 512, state 4 S + 10 =
+    266): the pair kernel's LDS is too full there to also hold the mixer's state rows at the
+    start, so the mixer stages them itself -- same results as the torch modules."""
+    dev = "cuda:0"
+    torch.manual_seed(11)
+    agents = [AgentQNet(512, 3, 128, 64).to(dev) for _ in range(4)]
+    mix = QMixer(4, 266, 32, 64).to(dev)
+    gen = torch.Generator(device=dev).manual_seed(4)
+    B = 70
+    obs = torch.randn(B, 4, 512, device=dev, generator=gen) * 0.3
+    hid = torch.randn(B, 4, 64, device=dev, generator=gen) * 0.5
+    state = torch.randn(B, 266, device=dev, generator=gen)
+    pol = FusedQMIXPolicy(agents, mix, 3, epsilon=0.0, seed=1, servers_per_agent=16)
+    hk = hid.clone()
+    acts, _, q_tot, q = pol(obs, hk, state, q_values=True)
+    with torch.no_grad():
+        for a, net in enumerate(agents):
+            rq, rh = net(obs[:, a], hid[:, a].unsqueeze(0).contiguous())
+            close(q[:, a], rq)
+            close(hk[:, a], rh[0])
+        close(q_tot, mix(q.gather(2, acts.unsqueeze(2)).squeeze(2), state))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("env", [{"LBSIM_QMIX_KERNEL": "wave"},
                                  {"LBSIM_QMIX_KERNEL": "tile"},
                                  {"LBSIM_FUSED_MT": "2", "LBSIM_QMIX_KERNEL": "tile"},
