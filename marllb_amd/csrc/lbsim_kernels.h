@@ -2037,4 +2037,25 @@ __device__ __forceinline__ void observe_env_wave(const DevState& st, const SimPa
   wave_sync();  // s_obs / s_act reused by the next env
 }
 
+// Reset-mode observation of S <= 4 envs, kObsResetEnvs envs per workgroup, one wave each (its own
+// scratch; only wave-level ordering, so waves of envs outside the mask simply leave).  A masked
+// reset (graph_mode's every-step auto-reset, or the eager one past max_steps) then dispatches B / 8
+// workgroups instead of B: when few envs are done, the launch costs its dispatch, not B
+// single-wave workgroups that each read one mask byte.
+constexpr int kObsResetEnvs = 8;
+static_assert(kObsResetEnvs * sizeof(ObsScratch) <= 65536, "default dynamic LDS limit");
+template <bool FAC>
+__global__ void __launch_bounds__(64 * kObsResetEnvs, 4)
+    observe_reset_kernel(DevState st, SimParams p, ObsOutputs out, const uint8_t* reset_mask) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t b = (size_t)blockIdx.x * kObsResetEnvs + (size_t)wv;
+  if (b >= (size_t)p.B || (reset_mask != nullptr && reset_mask[b] == 0)) return;
+  extern __shared__ double obs_dyn[];
+  ObsScratch& sc = reinterpret_cast<ObsScratch*>(obs_dyn)[wv];
+  __shared__ float s_obs[kObsResetEnvs][kObsChunk * NF];
+  __shared__ float s_act[kObsResetEnvs][kObsChunk];
+  observe_chunk<true, false>(st, p, b, 0, p.S, sc, s_obs[wv], lane);  // S <= kObsChunk: one chunk
+  observe_outputs<kObsChunk, kModeReset, FAC>(st, p, out, b, s_obs[wv], s_act[wv], lane, 64);
+}
+
 }  // namespace lbk

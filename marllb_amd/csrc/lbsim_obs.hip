@@ -35,7 +35,20 @@ void launch_observe_t(const LaunchCtx& L, const ObsOutputs& o, const uint8_t* ma
 template <int MODE>
 void launch_observe_m(const LaunchCtx& L, const ObsOutputs& o, const uint8_t* mask,
                       hipStream_t stream) {
-  if (o.agent_obs != nullptr || o.state != nullptr)
+  const bool fac = o.agent_obs != nullptr || o.state != nullptr;
+  if (MODE == kModeReset && L.S <= kObsChunk) {  // kObsResetEnvs single-wave envs per workgroup
+    const dim3 grid((unsigned)((L.B + kObsResetEnvs - 1) / kObsResetEnvs)),
+        block(64 * kObsResetEnvs);
+    const size_t lds = kObsResetEnvs * sizeof(ObsScratch);
+    if (fac)
+      hipLaunchKernelGGL(observe_reset_kernel<true>, grid, block, lds, stream, L.st, L.prm, o,
+                         mask);
+    else
+      hipLaunchKernelGGL(observe_reset_kernel<false>, grid, block, lds, stream, L.st, L.prm, o,
+                         mask);
+    return;
+  }
+  if (fac)
     launch_observe_t<MODE, true>(L, o, mask, stream);
   else
     launch_observe_t<MODE, false>(L, o, mask, stream);
