@@ -268,6 +268,10 @@ class VecLoadBalanceEnv:
         # upper bound on every env's episode step since the last full reset: while it is below
         # max_steps no env can be done, so the masked auto-reset launch is provably a no-op
         self._step_bound = 0
+        # every env at the same episode step (since a full reset, and kept by auto-resets: done
+        # is exactly ep_step >= max_steps, so all envs end their episodes together and the
+        # auto-reset restarts all of them); a masked reset() or set_state() clears it
+        self._synced = False
 
     # -- helpers
     def _stream(self) -> int:
@@ -373,6 +377,7 @@ class VecLoadBalanceEnv:
                                                              ctypes.byref(out), self._stream()))
             self._reset_done = True
             self._step_bound = 0
+            self._synced = True
             if self.feature_mode == "upstream":
                 self._upstream(obs)
                 self._up_ret = None
@@ -380,6 +385,7 @@ class VecLoadBalanceEnv:
             return obs
         if not self._reset_done:
             raise RuntimeError("call reset() without a mask first")
+        self._synced = False  # the reset envs restart at episode step 0, the others do not
         m = self._mask(mask)
         obs = self._last_obs if self.graph_mode else self._last_obs.clone()
         out = _lib.StepOutputs()
@@ -439,6 +445,8 @@ class VecLoadBalanceEnv:
         if self.autoreset and (self.graph_mode or self._step_bound >= self.cfg.max_steps):
             if self.keep_terminal_obs:
                 info["terminal_obs"] = obs.clone()
+            if self._synced and not self.graph_mode:
+                self._step_bound = 0  # every env is done now and restarts at episode step 0
             # envs with done == 0 are untouched by the masked reset (no host sync needed)
             rout = _lib.StepOutputs()
             rout.obs = obs.data_ptr()
@@ -463,6 +471,7 @@ class VecLoadBalanceEnv:
         self.handle.load_state(data)
         self._reset_done = True
         self._step_bound = self.cfg.max_steps  # unknown episode steps: keep auto-reset armed
+        self._synced = False
 
     def close(self) -> None:
         self.handle.close()

@@ -175,6 +175,41 @@ def test_vec_autoreset_matches_oracle(oracle_mod):
         np.testing.assert_array_equal(info["episode_length"].cpu().numpy()[do == 0], ln[do == 0])
 
 
+def test_vec_synced_autoreset_matches_oracle(oracle_mod):
+    """Envs reset together stay in step: every env ends its episode at the same step, so the
+    auto-reset launches only then (env._synced) -- three episodes equal the oracle step by step,
+    and between episode ends no reset launch is made."""
+    from marllb_amd import VecLoadBalanceEnv
+    from marllb_amd.env import make_config
+    B, S, T = 64, 4, 4
+    kw = dict(seed=5, max_steps=T)
+    env = VecLoadBalanceEnv(B, S, device="cuda:0", autoreset=True, **kw)
+    ora = oracle_mod.OracleEnv(make_config(B, S, **kw), threads=4)
+    np.testing.assert_array_equal(env.reset().cpu().numpy(), ora.reset())
+    rng = np.random.default_rng(2)
+    lib = env.handle.lib  # the shared CDLL: count its reset calls, restore it whatever happens
+    real = lib.lbsim_reset_ex
+    calls = []
+    lib.lbsim_reset_ex = lambda *a: (calls.append(1), real(*a))[1]
+    resets_at = []
+    try:
+        for k in range(3 * T):
+            a = rng.integers(0, 3, (B, S)).astype(np.int64)
+            n0 = len(calls)
+            obs, rew, done, info = env.step(torch.from_numpy(a))
+            if len(calls) > n0:
+                resets_at.append(k)
+            oo, ro, do, _ = ora.step(a)
+            np.testing.assert_array_equal(rew.cpu().numpy(), ro)
+            np.testing.assert_array_equal(done.cpu().numpy(), do.astype(bool))
+            if do.any():
+                oo = ora.reset(mask=do, obs=oo)
+            np.testing.assert_array_equal(obs.cpu().numpy(), oo, err_msg=f"step {k}")
+    finally:
+        lib.lbsim_reset_ex = real
+    assert resets_at == [T - 1, 2 * T - 1, 3 * T - 1]
+
+
 def test_vec_actions_any_dtype_and_device():
     from marllb_amd import VecLoadBalanceEnv
     B, S = 64, 4
