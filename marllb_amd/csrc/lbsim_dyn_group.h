@@ -122,10 +122,13 @@ struct GroupAliasTab {
   __device__ int32_t& operator()(int f, int k) const { return t[f * 64 + gbase + k]; }
 };
 
-// Loop constants of one step (as dynamics_kernel's EvConst): Philox round keys and the scalars the
-// loop reads, pinned in VGPRs so the loop never reloads them from the kernarg segment.
+// Loop constants of one step: the Philox keys and the scalars the loop reads, pinned in VGPRs so
+// the loop never reloads them from the kernarg segment.  Only the two base keys are kept: round
+// r's keys (k + r * the Weyl constants) are formed inside the draw-ahead block, 20 adds per G
+// iterations instead of 18 more live VGPRs (116 -> 100; dynamics 1-2 % faster at 4096 x 4,
+// 65536 x 8 and 262144 x 4, unchanged at 65536 x 4: profiles/r03/ab_dyn_round_keys.txt).
 struct GroupConst {
-  uint32_t rk0[10], rk1[10];
+  uint32_t k0, k1;
   float mean_gap;
   int32_t dt;
   uint32_t base_ms, base_rem;
@@ -133,14 +136,8 @@ struct GroupConst {
 __device__ __forceinline__ GroupConst group_const(const SimParams& p, uint32_t base_ms,
                                                   uint32_t base_rem) {
   GroupConst c;
-  uint32_t k0 = p.key0, k1 = p.key1;
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    c.rk0[r] = vpin(k0);
-    c.rk1[r] = vpin(k1);
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
-  }
+  c.k0 = vpin(p.key0);
+  c.k1 = vpin(p.key1);
   c.mean_gap = vpin(p.mean_gap_us);
   c.dt = vpin(p.dt_us);
   c.base_ms = vpin(base_ms);
@@ -183,7 +180,13 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
     if ((it & (uint32_t)(G - 1)) == 0u) {
       cbase = E.arr_idx + 1u;
       const uint32_t k = cbase + (uint32_t)s;
-      const u32x4 d = philox_rk(u32x4{k, E.gid, E.episode, kStreamArrival << 24}, gc.rk0, gc.rk1);
+      uint32_t rk0[10], rk1[10];
+#pragma unroll
+      for (int r = 0; r < 10; ++r) {
+        rk0[r] = gc.k0 + (uint32_t)r * 0x9E3779B9u;
+        rk1[r] = gc.k1 + (uint32_t)r * 0xBB67AE85u;
+      }
+      const u32x4 d = philox_rk(u32x4{k, E.gid, E.episode, kStreamArrival << 24}, rk0, rk1);
       int32_t gap;
       float wk;
       if constexpr (TRACE) {
