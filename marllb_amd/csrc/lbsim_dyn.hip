@@ -32,6 +32,18 @@ void launch_dyn_group(const LaunchCtx& L, const void* action, int dtype, int32_t
                       const uint8_t* mask, hipStream_t stream) {
   constexpr int epw = 64 / G;
   const dim3 block(64), grid((unsigned)((L.B + epw - 1) / epw));
+  // a step grid of more than 4 waves per SIMD: the 5-wave register budget (SED, 4 / 8 lanes)
+  if constexpr (MODE == kModeStep && POLICY == 0 && (G == 4 || G == 8)) {
+    if ((int64_t)grid.x > 4 * (int64_t)L.simds) {
+      if (L.prm.trace)
+        hipLaunchKernelGGL((dynamics_group_kernel<G, MODE, POLICY, true, 5>), grid, block, 0,
+                           stream, L.st, L.prm, action, dtype, assign, mask);
+      else
+        hipLaunchKernelGGL((dynamics_group_kernel<G, MODE, POLICY, false, 5>), grid, block, 0,
+                           stream, L.st, L.prm, action, dtype, assign, mask);
+      return;
+    }
+  }
   if (L.prm.trace)
     hipLaunchKernelGGL((dynamics_group_kernel<G, MODE, POLICY, true>), grid, block, 0, stream,
                        L.st, L.prm, action, dtype, assign, mask);

@@ -571,8 +571,12 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
   }
 }
 
-template <int G, int MODE, int POLICY, bool TRACE>
-__global__ void __launch_bounds__(64)
+// WAVES: the occupancy the register allocation targets (1 = unconstrained: 100 VGPRs, 4 waves per
+// SIMD).  WAVES = 5 (96 VGPRs, 2 spilled) pays only when the grid holds more than 4 waves per
+// SIMD (262144 x 4: -6 %, 65536 x 8: -1.6 %) and costs 9 % at 65536 x 4, whose 4,096 waves are
+// exactly 4 per SIMD (profiles/r03/ab_dyn_round_keys.txt): the launcher picks it by grid size.
+template <int G, int MODE, int POLICY, bool TRACE, int WAVES = 1>
+__global__ void __launch_bounds__(64, WAVES)
     dynamics_group_kernel(DevState st, SimParams p, const void* action, int action_dtype,
                           int32_t* assign_out, const uint8_t* reset_mask) {
   __shared__ DynGroupLds<POLICY> L;

@@ -362,6 +362,27 @@ def test_full_size_properties(lib, oracle_mod):
     assert st["dropped"].sum() == 0
 
 
+def test_grid_above_four_waves_per_simd_s4(lib, oracle_mod):
+    """A 4-lane step grid of more than 4 waves per SIMD (B > 65536 at S = 4 on 256 CUs) runs the
+    5-wave register budget of dynamics_group_kernel: an oracle slice of the same global ids stays
+    bit-exact."""
+    from marllb_amd.env import VecLoadBalanceEnv, make_config
+    B, S, steps = 70000, 4, 3
+    env = VecLoadBalanceEnv(B, S, device="cuda:0", seed=21, autoreset=False)
+    env.reset()
+    rng = np.random.default_rng(4)
+    acts = [rng.integers(0, 3, (B, S)) for _ in range(steps)]
+    for a in acts:
+        obs, rew, done, _ = env.step(torch.from_numpy(a))
+    off, n = 66000, 384  # the slice straddles the last 4-wave-per-SIMD boundary of the grid
+    ora = oracle_mod.OracleEnv(make_config(n, S, seed=21, env_id_offset=off), threads=8)
+    ora.reset()
+    for a in acts:
+        oo, ro, _, _ = ora.step(np.ascontiguousarray(a[off:off + n]))
+    np.testing.assert_array_equal(obs[off:off + n].cpu().numpy(), oo)
+    np.testing.assert_array_equal(rew[off:off + n].cpu().numpy(), ro)
+
+
 def test_full_size_trace_replay_c3(lib, oracle_mod):
     """BASELINE configs[2]: 65536 envs x 8 servers replaying data/trace poisson_for_loop
     rate_500 (the Wikipedia-trace stand-in).  Arrival conservation against the
