@@ -3,6 +3,7 @@
 // so the two halves of the template instantiations compile in parallel.
 #include "lbsim_internal.h"
 #include "lbsim_dyn_group.h"
+#include "lbsim_dyn_wave.h"
 
 #ifndef LBSIM_DYN_MODE
 #error "build with -DLBSIM_DYN_MODE=0 (step) or 1 (reset)"
@@ -78,6 +79,30 @@ void launch_dyn_group_policy(const LaunchCtx& L, const void* action, int dtype, 
   }
 }
 
+// one wave per env: NR ring registers of 16 positions per server
+template <int NR, int POLICY>
+void launch_dyn_wave(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
+                     const uint8_t* mask, hipStream_t stream) {
+  const dim3 block(64), grid((unsigned)L.B);
+  if (L.prm.trace)
+    hipLaunchKernelGGL((dynamics_wave_kernel<NR, MODE, POLICY, true>), grid, block, 0, stream,
+                       L.st, L.prm, action, dtype, assign, mask);
+  else
+    hipLaunchKernelGGL((dynamics_wave_kernel<NR, MODE, POLICY, false>), grid, block, 0, stream,
+                       L.st, L.prm, action, dtype, assign, mask);
+}
+
+template <int NR>
+void launch_dyn_wave_policy(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
+                            const uint8_t* mask, hipStream_t s) {
+  switch (L.prm.policy) {
+    case LBSIM_POLICY_SED: launch_dyn_wave<NR, 0>(L, action, dtype, assign, mask, s); break;
+    case LBSIM_POLICY_SED2: launch_dyn_wave<NR, 1>(L, action, dtype, assign, mask, s); break;
+    case LBSIM_POLICY_LSQ: launch_dyn_wave<NR, 2>(L, action, dtype, assign, mask, s); break;
+    default: launch_dyn_wave<NR, 3>(L, action, dtype, assign, mask, s); break;
+  }
+}
+
 // Mapping choice (LBSIM_DYN_AUTO): one lane per server.  With arrivals drawn G at a
 // time (lbsim_dyn_group.h) it is faster than one lane per env at every measured shape
 // (profiles/r02_round2/mapping_sweep.jsonl): 65536 x 4 0.182 vs 0.214 ms, 131072 x 4 0.316 vs
@@ -86,6 +111,11 @@ void launch_dyn_group_policy(const LaunchCtx& L, const void* action, int dtype, 
 // dyn_group_lanes (lbsim_internal.h).
 void launch_dynamics_t(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
                        const uint8_t* mask, hipStream_t stream) {
+  if (dyn_wave_ok(L)) {
+    if (L.prm.Q <= kWaveRingLanes) launch_dyn_wave_policy<1>(L, action, dtype, assign, mask, stream);
+    else launch_dyn_wave_policy<2>(L, action, dtype, assign, mask, stream);
+    return;
+  }
   switch (dyn_group_lanes(L)) {
     case 0:  // one lane per env
       if (L.S <= 4) launch_dyn_policy<4>(L, false, action, dtype, assign, mask, stream);

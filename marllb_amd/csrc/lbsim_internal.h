@@ -50,6 +50,25 @@ inline int dyn_group_lanes(const LaunchCtx& L) {
   return g;
 }
 
+// One wave per env (lbsim_dyn_wave.h): S <= 4, Q <= 32, SED / SED2 / LSQ / LSQ2, the default
+// mapping, and a batch small enough that one env's event-loop chain, not issue throughput, sets
+// the step time: B <= LBSIM_DYN_WAVE_MAX_B (default 8192).  LBSIM_DYN_WAVE = 0 disables it, 1 uses
+// it at every batch size it applies to; a forced LBSIM_DYN_GROUP_LANES width wins over both.
+inline bool dyn_wave_ok(const LaunchCtx& L) {
+  static const int mode = [] {
+    const char* e = std::getenv("LBSIM_DYN_WAVE");
+    return e ? std::atoi(e) : -1;
+  }();
+  static const int64_t max_b = [] {
+    const char* e = std::getenv("LBSIM_DYN_WAVE_MAX_B");
+    return e ? (int64_t)std::atoll(e) : (int64_t)8192;
+  }();
+  static const bool forced_lanes = std::getenv("LBSIM_DYN_GROUP_LANES") != nullptr;
+  if (mode == 0 || forced_lanes || L.dyn_mapping == LBSIM_DYN_ENV_PER_LANE) return false;
+  if (L.S > 4 || L.prm.Q > 32 || L.prm.policy == LBSIM_POLICY_ALIAS) return false;
+  return mode == 1 || (int64_t)L.B <= max_b;
+}
+
 // Dynamics of one step (mode kModeStep) or of a reset with warm-up (kModeReset).
 void launch_dynamics_step(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
                           const uint8_t* mask, hipStream_t s);

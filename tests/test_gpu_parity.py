@@ -208,6 +208,14 @@ CONFIGS = [
                         "step_interval": 10.0, "queue_capacity": 64}),
     # above the small-batch threshold (B > 8192, S <= 4): the 4-lane groups of the headline shape
     dict(B=8256, S=4, kw={}),
+    # one wave per env (lbsim_dyn_wave.h, S <= 4, Q <= 32): overloaded servers whose rings fill
+    # (full-ring pushes keep the last completion, drops) with one ring register (Q <= 16) and
+    # two (Q = 32), LSQ / LSQ2 on small envs, NaN SED scores on 4 servers
+    dict(B=72, S=3, kw={"assign_policy": "lsq", "queue_capacity": 6, "load": 1.3}),
+    dict(B=40, S=2, kw={"assign_policy": "lsq2", "server_rates": [100.0, 150.0]}),
+    dict(B=36, S=4, kw={"load": 1.25, "discrete_weights": [0.5, 1.0, 8.0]}),
+    dict(B=30, S=4, kw={"queue_capacity": 16, "load": 1.4, "action_type": "continuous"}),
+    dict(B=60, S=4, kw={"action_type": "continuous", "_nan_actions": 0.2}),
 ]
 
 
@@ -305,6 +313,28 @@ def test_wider_groups_bit_exact(lanes):
                         "no:cacheprovider"] +
                        [os.path.join(root, "tests", "test_gpu_parity.py") + "::" + k for k in ks],
                        cwd=root, env={**os.environ, "LBSIM_DYN_GROUP_LANES": lanes},
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_wave_kernel_bit_exact():
+    """LBSIM_DYN_WAVE=1 runs the one-wave-per-env dynamics (lbsim_dyn_wave.h) on every simulator
+    case it applies to (S <= 4, queue capacity <= 32, every policy but ALIAS) at any batch size,
+    the 8256-env case included, both as two launches and under the fused step (whose reset
+    launch is then the wave kernel): bit-exact vs the oracle.  The setting is read once per
+    process, so the cases run in a child process."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ks = [f"test_simulator_bit_exact_vs_oracle[{c}-{m}]" for c in range(len(CONFIGS))
+          for m in ("server", "server-fused")
+          if CONFIGS[c]["S"] <= 4 and CONFIGS[c]["kw"].get("queue_capacity", 32) <= 32
+          and CONFIGS[c]["kw"].get("assign_policy") != "alias"]
+    assert len(ks) >= 20
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p",
+                        "no:cacheprovider"] +
+                       [os.path.join(root, "tests", "test_gpu_parity.py") + "::" + k for k in ks],
+                       cwd=root, env={**os.environ, "LBSIM_DYN_WAVE": "1"},
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
 
