@@ -79,7 +79,7 @@ void launch_dyn_group_policy(const LaunchCtx& L, const void* action, int dtype, 
   }
 }
 
-// one wave per env: NR ring registers of 16 positions per server
+// one wave per env: NG ring registers, two servers of 32 positions each
 template <int NR, int POLICY>
 void launch_dyn_wave(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
                      const uint8_t* mask, hipStream_t stream) {
@@ -112,7 +112,7 @@ void launch_dyn_wave_policy(const LaunchCtx& L, const void* action, int dtype, i
 void launch_dynamics_t(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
                        const uint8_t* mask, hipStream_t stream) {
   if (dyn_wave_ok(L)) {
-    if (L.prm.Q <= kWaveRingLanes) launch_dyn_wave_policy<1>(L, action, dtype, assign, mask, stream);
+    if (L.S <= 2) launch_dyn_wave_policy<1>(L, action, dtype, assign, mask, stream);
     else launch_dyn_wave_policy<2>(L, action, dtype, assign, mask, stream);
     return;
   }

@@ -1,25 +1,34 @@
 // lbsim_dyn_wave.h — dynamics with one WAVE per env, for batches too small to fill the chip
-// (BASELINE configs[0] 1 x 4, configs[1] at 4096 x 4): the event loop is one env's dependent chain,
-// so its length per arrival, not issue throughput, sets the step time.
+// (BASELINE configs[0] 1 x 4, configs[1] at 4096 x 4): there the event loop is one env's dependent
+// chain, so the instructions per arrival on that chain, not issue throughput, set the step time.
 //
-// The server-per-lane kernel (lbsim_dyn_group.h) spends ~150 dependent instructions per event-loop
+// The server-per-lane kernel (lbsim_dyn_group.h) spends ~150 instructions per event-loop
 // iteration: a pop per iteration (extra iterations when two completions fall between arrivals), an
-// LDS round trip for the next queue head and one for the next drawn arrival, two DPP reductions
-// and the draw-ahead refill every G iterations.  Here the whole env is one wave and its state is
-// laid out so that an arrival costs a few wave-wide instructions:
-//   * ring lanes: the FIFO of server s is lanes 16 s .. 16 s + 15 of NR VGPR pairs {t_complete,
-//     t_arrival}; ring position pos of server s is register pos >> 4, lane 16 s + (pos & 15), so
-//     the HBM ring loads and stores lane for lane.  A 64-bit `live` mask per
-//     register marks the flows still queued.  The pops before an arrival at ta are one v_cmp per
-//     register (live &= ballot(t_complete > ta)): the completions due by ta leave in one step,
-//     whatever their number (the oracle's pop_until, lbsim_oracle.c sim_step);
+// LDS round trip for the next queue head and one for the next drawn arrival, two DPP reductions,
+// the reservoir insert and the draw-ahead refill every G iterations.  Here the whole env is one
+// wave and its state is laid out so that an arrival is a short straight-line block:
+//   * ring lanes: servers 2g and 2g + 1 own the two 32-lane halves of ring register g (NG = 1 or
+//     2 registers each of {t_complete, t_arrival}); ring position pos of server s is register
+//     s >> 1, lane 32 (s & 1) + pos, so the HBM ring loads and stores lane for
+//     lane.  With FIFO service and arrival times that never decrease, a slot's flow is queued at
+//     time t iff its t_complete > t (free slots hold kDead): the pops before an arrival at ta are
+//     implicit, and a server's flow count at ta is the popcount of its half of one ballot per
+//     register (the oracle's pop_until, lbsim_oracle.c sim_step, however many complete);
+//   * the counts for the NEXT arrival are taken while the current one is chosen (its time is
+//     known: arrivals are drawn ahead), so the chain from one choice to the next is the pushed
+//     flow's +1 on its server, the SED score (3 f64 ops), one DPP minimum and a ballot of the ties;
 //   * server lanes: lane s < S holds server s's fields (write position, tail, Algorithm R count,
-//     SED denominator); its flow count is the popcount of its 16 bits of `live`.  The choice is
-//     the group kernel's lexicographic minimum (one DPP min over the quad, then a ballot of the
-//     ties), the push one select in ring lane 16 c + (pos & 15) and one in server lane c;
-//   * arrivals: 64 at a time, lane j drawing arrival base + j (its Philox block, gap and work, or
-//     its trace row) with the arrival times as one wave prefix sum; the loop reads arrival k with
-//     v_readlane (uniform, in SGPRs), so no LDS access and no draw sits on the chain.
+//     SED denominator); the push is a select in ring lane 32 (c & 1) + wp_c and one in lane c;
+//   * arrivals: 64 at a time (lane j: arrival base + j, its Philox block, gap and work or its
+//     trace row, times by one wave prefix sum); consecutive batches overlap by one arrival (the
+//     look-ahead), and the loop reads arrival k with v_readlane (SGPRs): no LDS on the chain;
+//   * reservoir inserts are deferred to the end of each batch: every arrival logs its server and
+//     completion time in its batch lane; the flush gives each completed flow its Algorithm R count
+//     (the server's count + the earlier inserts of the batch into it, a masked bit count), its slot
+//     from its arrival's draw word, keeps the LAST insert into each (server, slot) (an LDS
+//     atomic max over arrival order) and stores the records in one pass.  Per server the inserts
+//     happen in arrival order = FIFO completion order, after the carried-in flows, exactly as
+//     the oracle's pops make them.
 // Same event sequence, same arithmetic, same state layout as the other two
 // mappings: interchangeable between launches, bit-identical to the oracle.  S <= 4, Q <= 32 and the
 // SED / SED2 / LSQ / LSQ2 policies (ALIAS and larger shapes use the group kernel: dyn_wave_ok in
@@ -30,12 +39,14 @@
 
 namespace lbk {
 
-constexpr int kWaveRingLanes = 16;  // ring positions per server per VGPR (4 servers per wave)
-
-template <int NR>
+// Register g, lane l: ring position l & 31 of server 2g + (l >> 5).  FIFO service and arrival
+// times that never decrease make a slot's flow queued at time t iff its t_complete > t: a popped
+// flow completed no later than the arrival that popped it, and a free slot holds kDead.  So no
+// queue bookkeeping survives between arrivals but the slots themselves.
+constexpr int32_t kDead = kLastNone;
+template <int NG>
 struct WaveRing {
-  int32_t tc[NR], ta[NR];  // lane 16 s + k: ring position 16 r + k of server s
-  uint64_t live[NR];       // lanes holding a queued flow (uniform)
+  int32_t tc[NG], ta[NG];
 };
 
 // Server lane s (s < S; the other lanes carry inactive copies).
@@ -61,9 +72,19 @@ struct WaveEnv {
   uint32_t u2, u3;
 };
 
+// One batch of drawn arrivals (lane j: arrival base + j) and the log of the processed ones.
+struct WaveBatch {
+  int32_t ta;     // arrival time (relative us)
+  float wk;       // Exp(1) work
+  uint32_t u2, u3;
+  int32_t lc;     // logged: chosen server (-1: dropped)
+  int32_t ltc;    // logged: t_complete of the pushed flow
+};
+
 struct WaveLds {
-  int2 img[32 * 4];      // ring image [pos][server] for the carried-in walk and `last`
-  uint32_t chg[4 * 4];   // written-slot masks [word][server]
+  int2 img[32 * 4];       // ring image [pos][server] for the carried-in walk and `last`
+  uint32_t own[4 * 128];  // insert owner of each (server, slot) in a flush: seq << 6 | lane
+  uint32_t chg[4 * 4];    // written-slot masks [word][server]
 };
 
 __device__ __forceinline__ int32_t rdl(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -73,14 +94,18 @@ __device__ __forceinline__ uint32_t rdl(uint32_t v, int l) {
 __device__ __forceinline__ float rdl(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
+__device__ __forceinline__ uint32_t sat_add(uint32_t a, uint32_t b) {
+  const uint32_t s = a + b;
+  return s < a ? 0xFFFFFFFFu : s;  // count_inc applied b times
+}
 
-// Arrivals base .. base + 63 (lane j: arrival base + j), their times as offsets from t_prev, the
-// time of arrival base - 1 (the oracle's draw_arrival chain next_arr = t_prev + gap).
+// Arrivals base .. base + 63 (lane j: arrival base + j), t0 = the time of arrival base: lane j's
+// time is t0 + the gaps of arrivals base + 1 .. base + j (the oracle's draw_arrival chain
+// next_arr = t_prev + gap; integer sums, so any order is exact).
 template <bool TRACE>
 __device__ __forceinline__ void wave_draw_batch(const DevState& st, const SimParams& p,
-                                                const WaveEnv& E, uint32_t base, int32_t t_prev,
-                                                int lane, int32_t& bta, float& bwk,
-                                                uint32_t& bu2, uint32_t& bu3) {
+                                                const WaveEnv& E, uint32_t base, int32_t t0,
+                                                int lane, WaveBatch& Bt) {
   const uint32_t k = base + (uint32_t)lane;
   const u32x4 d = philox4x32_10(u32x4{k, E.gid, E.episode, kStreamArrival << 24}, p.key0, p.key1);
   int32_t gap;
@@ -93,164 +118,237 @@ __device__ __forceinline__ void wave_draw_batch(const DevState& st, const SimPar
     gap = (int32_t)(-lb_logf(u01_open0(d.x)) * p.mean_gap_us);
     wk = -lb_logf(u01_open0(d.y));
   }
-  int32_t t = gap;  // inclusive prefix sum over the wave (integer: any order is exact)
+  int32_t t = lane == 0 ? 0 : gap;  // inclusive prefix sum over the wave
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const int32_t v = __shfl_up(t, (unsigned)o, 64);
     t += lane >= o ? v : 0;
   }
-  bta = t_prev + t;
-  bwk = wk;
-  bu2 = d.z;
-  bu3 = d.w;
+  Bt.ta = t0 + t;
+  Bt.wk = wk;
+  Bt.u2 = d.z;
+  Bt.u3 = d.w;
+  Bt.lc = -1;
+  Bt.ltc = 0;
 }
 
-// Flows of server lane s queued now (its 16 bits of each live mask).
-template <int NR>
-__device__ __forceinline__ int32_t wave_count(const WaveRing<NR>& R, int s4) {
-  int32_t n = 0;
+// Flows of server lane s in the ring-lane masks `live` (its half of register s >> 1).
+template <int NG>
+__device__ __forceinline__ int32_t wave_count(const uint64_t (&live)[NG], int lane) {
+  const bool odd = lane & 1;
+  uint32_t w = odd ? (uint32_t)(live[0] >> 32) : (uint32_t)live[0];
+  if constexpr (NG > 1) {
+    const uint32_t w1 = odd ? (uint32_t)(live[NG - 1] >> 32) : (uint32_t)live[NG - 1];
+    w = (lane & 2) ? w1 : w;
+  }
+  return __builtin_popcount(w);
+}
+
+// The reservoir inserts of batch lanes [0, nproc): flows that completed in this step, per server in
+// arrival order (reservoir.py:64-85 with the arrival's draw word, reservoir_slot_r32).
+__device__ __forceinline__ void wave_flush(const SimParams& p, WaveSrv& V, const WaveBatch& Bt,
+                                           int nproc, int lane, uint3* const res_b, WaveLds& Ld,
+                                           uint32_t seq, uint32_t base_ms, uint32_t base_rem) {
+  const int S = p.S;
+  const int32_t dt = p.dt_us;
+  const bool valid = lane < nproc && Bt.lc >= 0;
+  const bool ins = valid && Bt.ltc <= dt;
+  uint32_t pre = 0u, rcb = 0u;
+  float scale = p.svc_scale[0];
 #pragma unroll
-  for (int r = 0; r < NR; ++r)
-    n += __builtin_popcount((uint32_t)(R.live[r] >> (16 * s4)) & 0xFFFFu);
-  return n;
+  for (int s = 0; s < 4; ++s) {
+    if (s < S) {
+      const bool mine = Bt.lc == s;
+      const uint64_t m = __ballot(ins && mine);
+      const uint32_t below = __mbcnt_hi((uint32_t)(m >> 32), __mbcnt_lo((uint32_t)m, 0u));
+      const uint32_t rs = rdl(V.rcnt, s);
+      pre = mine ? below : pre;
+      rcb = mine ? rs : rcb;
+      if (s > 0) scale = mine ? p.svc_scale[s] : scale;
+      const uint32_t npush = (uint32_t)__builtin_popcountll(__ballot(valid && mine));
+      const bool me = lane == s;
+      V.rcnt = me ? sat_add(rs, (uint32_t)__builtin_popcountll(m)) : V.rcnt;
+      V.pushed += me ? (int32_t)npush : 0;
+      V.assigned += me ? (int32_t)npush : 0;
+    }
+  }
+  const uint32_t cres = sat_add(rcb, pre);  // the count before this insert
+  const int slot = ins ? reservoir_slot_r32(cres, Bt.u3) : -1;
+  const uint32_t key = (uint32_t)Bt.lc * K + (uint32_t)slot;
+  const uint32_t me_tag = (seq << 6) | (uint32_t)lane;
+  if (slot >= 0) {
+    atomicMax(&Ld.own[key], me_tag);  // the last insert into a slot is the one that stays
+    atomicOr(&Ld.chg[((uint32_t)slot >> 5) * 4u + (uint32_t)Bt.lc], 1u << (slot & 31));
+  }
+  wave_sync();
+  if (slot >= 0 && Ld.own[key] == me_tag) {
+    int32_t svc = (int32_t)(Bt.wk * scale);
+    svc = svc < 1 ? 1 : svc;
+    res_b[key] = make_uint3((uint32_t)(Bt.ltc - Bt.ta), (uint32_t)svc,
+                            base_ms + (base_rem + (uint32_t)Bt.ltc) / 1000u);
+  }
 }
 
-// One step of the env, w_own = this server lane's weight.
-template <int NR, int POLICY, bool TRACE, bool FAST>
+// The arrivals of one step.
+template <int NG, int POLICY, bool TRACE, bool FAST>
 __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimParams& p,
-                                                WaveEnv& E, WaveSrv& V, WaveRing<NR>& R,
-                                                int lane, uint3* const res_b, uint32_t* chg,
-                                                uint32_t base_ms, uint32_t base_rem) {
+                                                WaveEnv& E, WaveSrv& V, WaveRing<NG>& R,
+                                                int lane, uint3* const res_b, WaveLds& Ld,
+                                                uint32_t& seq, uint32_t base_ms,
+                                                uint32_t base_rem) {
   constexpr bool two_choice = (POLICY == 1 || POLICY == 3);
   constexpr bool lsq = (POLICY == 2 || POLICY == 3);
   const int S = p.S, Q = p.Q;
   const int32_t dt = p.dt_us;
-  const int s4 = lane & 3;
-  int bi = 64;  // batch lane of the next arrival (64: draw a batch first)
-  int32_t bta = 0;
-  float bwk = 0.f;
-  uint32_t bu2 = 0u, bu3 = 0u;
-  while (E.next_arr < dt) {
-    const int32_t ta = E.next_arr;
-    // ---- completions due by ta leave the queues
-#pragma unroll
-    for (int r = 0; r < NR; ++r) R.live[r] &= __ballot(R.tc[r] > ta);
-    const int32_t n = wave_count<NR>(R, s4);
+  if (E.next_arr >= dt) return;
 
-    // ---- the arrival's server (node.c:388-441); full servers are not eligible
-    float score = 0.f;
+  // batch 0: lane 0 is the pending arrival (its stored draw), lanes 1..63 the next ones
+  uint32_t base = E.arr_idx;
+  WaveBatch Bt;
+  wave_draw_batch<TRACE>(st, p, E, base, E.next_arr, lane, Bt);
+  Bt.wk = lane == 0 ? E.next_work : Bt.wk;
+  Bt.u2 = lane == 0 ? E.u2 : Bt.u2;
+  Bt.u3 = lane == 0 ? E.u3 : Bt.u3;
+  int bi = 0;  // batch lane of the current arrival
+  int32_t ta = E.next_arr;
+
+  // per-lane constants: the shift that brings server lane s's half of a ring mask to bits 0..31
+  const uint32_t half_sh = (uint32_t)(lane & 1) * 32u;
+  const bool hi_reg = (lane & 2) != 0;
+  auto count_at = [&](int32_t t) -> int32_t {  // server lane's flows queued at time t
+    const uint32_t w0 = (uint32_t)(__ballot(R.tc[0] > t) >> half_sh);
+    if constexpr (NG > 1) {
+      const uint32_t w1 = (uint32_t)(__ballot(R.tc[NG - 1] > t) >> half_sh);
+      return __builtin_popcount(hi_reg ? w1 : w0);
+    }
+    return __builtin_popcount(w0);
+  };
+  auto score_of = [&](int32_t nn) -> float {  // node.c:393-404 (SED) / the count (LSQ)
     if constexpr (lsq) {
-      score = (float)n;
+      return (float)nn;
     } else {
-      const double c = (double)(n + 1);
-      const double q0 = c * V.rcp;
-      double q = fma(fma(-q0, V.den, c), V.rcp, q0);
+      const double c1 = (double)(nn + 1);
+      const double q0 = c1 * V.rcp;
+      double q = fma(fma(-q0, V.den, c1), V.rcp, q0);
       if (!FAST && q != q) {
         asm volatile("");
-        q = c / V.den;
+        q = c1 / V.den;
       }
-      score = (float)q;
+      return (float)q;
     }
-    const bool elig = V.act && n < Q;
-    int c = -1;
-    if constexpr (two_choice) {
-      const int h1 = two_choice_h1(E.u2, S);
-      const int h2 = two_choice_h2(E.u2, S);
-      const uint32_t em = (uint32_t)__ballot(elig) & 0xFu;
-      const float s1 = rdl(score, h1), s2 = rdl(score, h2);
-      const bool ok1 = (em >> h1) & 1u, ok2 = (em >> h2) & 1u;
-      c = (ok1 && ok2) ? ((s2 < s1) ? h2 : h1) : (ok1 ? h1 : (ok2 ? h2 : -1));
-    } else if constexpr (FAST) {
-      // finite scores: the eligible minimum, h among equal minima, else the lowest such server
-      const int32_t key = elig ? f32_key(score) : 0x7FFFFFFF;
-      const int32_t mk = __builtin_amdgcn_readfirstlane(group_min_i32<4>(key));
-      if (mk != 0x7FFFFFFF) {
-        const int h = (int)__umulhi(E.u2, (uint32_t)S);
-        const uint32_t tie = (uint32_t)__ballot(elig && key == mk) & 0xFu;
-        c = ((tie >> h) & 1u) ? h : __builtin_ctz(tie);
-      }
-    } else {
-      const bool num = elig && score == score;
-      const float m = key_f32(
-          __builtin_amdgcn_readfirstlane(group_min_i32<4>(num ? f32_key(score) : 0x7f800000)));
-      const int h = (int)__umulhi(E.u2, (uint32_t)S);
-      const uint32_t em = (uint32_t)__ballot(elig) & 0xFu;
-      const int c0 = ((em >> h) & 1u) ? h : (em ? __builtin_ctz(em) : -1);
-      const uint32_t tie = (uint32_t)__ballot(num && score == m) & 0xFu;
-      const uint32_t nan = (uint32_t)__ballot(score != score) & 0xFu;
-      c = c0 < 0 ? -1 : ((((tie | nan) >> c0) & 1u) ? c0 : (tie ? __builtin_ctz(tie) : -1));
-    }
+  };
+  const uint32_t smask = (1u << S) - 1u;  // server lanes
+  int32_t n = count_at(ta);
+  float score = score_of(n);
+  for (;;) {      // batches
+    bool done = false;
+    for (; bi < 63; ++bi) {  // arrivals bi = 0 .. 62 (lane 63 opens the next batch)
+      const float work = rdl(Bt.wk, bi);
+      const uint32_t u2 = rdl(Bt.u2, bi);
+      // ---- look-ahead: the next arrival's queue counts without the flow pushed now, and the
+      //      scores for both outcomes (off the choice -> choice chain)
+      const int32_t ta_n = rdl(Bt.ta, bi + 1);
+      const int32_t n_n = count_at(ta_n);
+      const float sc0 = score_of(n_n), sc1 = score_of(n_n + 1);
+      // issue them here, before the choice (the in-order wave would otherwise run them after it)
+      asm volatile("" ::"v"(n_n), "v"(sc0), "v"(sc1));
 
-    if (c >= 0) {
-      // ---- FIFO service on server c: every server lane prices the flow, lane c's is pushed
-      const int32_t start_l = n > 0 ? (V.tail > ta ? V.tail : ta) : ta;
-      int32_t svc_l = (int32_t)(E.next_work * V.scale);
-      svc_l = svc_l < 1 ? 1 : svc_l;
-      const int32_t tc = rdl(start_l + svc_l, c);
-      const int pos = rdl(V.wp, c);
-      const int L = c * kWaveRingLanes + (pos & (kWaveRingLanes - 1));
-      const bool me = lane == c;
-      if (NR == 1 || pos < kWaveRingLanes) {
-        if (rdl(n, c) == Q - 1) {  // this push fills the ring: keep the last popped t_complete
-          const int32_t old = rdl(R.tc[0], L);
-          V.saved = me ? old : V.saved;
-        }
-        R.tc[0] = lane == L ? tc : R.tc[0];
-        R.ta[0] = lane == L ? ta : R.ta[0];
-        R.live[0] |= 1ull << L;
+      // ---- the arrival's server (node.c:388-441); full servers are not eligible
+      const bool elig = n < Q && lane < S;
+      const uint32_t em = (uint32_t)__ballot(n < Q) & smask;
+      int c = -1;
+      if constexpr (two_choice) {
+        const int h1 = two_choice_h1(u2, S);
+        const int h2 = two_choice_h2(u2, S);
+        const float s1 = rdl(score, h1), s2 = rdl(score, h2);
+        const bool ok1 = (em >> h1) & 1u, ok2 = (em >> h2) & 1u;
+        c = (ok1 && ok2) ? ((s2 < s1) ? h2 : h1) : (ok1 ? h1 : (ok2 ? h2 : -1));
+      } else if constexpr (FAST) {
+        // finite scores: the eligible minimum, h among equal minima, else the lowest such server
+        const int32_t key = elig ? f32_key(score) : 0x7FFFFFFF;
+        const int32_t mk = __builtin_amdgcn_readfirstlane(group_min_i32<4>(key));
+        const int h = (int)__umulhi(u2, (uint32_t)S);
+        const uint32_t tie = (uint32_t)__ballot(key == mk) & em;
+        c = ((tie >> h) & 1u) ? h : __builtin_ctz(tie);
+        c = tie == 0u ? -1 : c;
       } else {
-        if (rdl(n, c) == Q - 1) {
-          const int32_t old = rdl(R.tc[NR - 1], L);
-          V.saved = me ? old : V.saved;
-        }
-        R.tc[NR - 1] = lane == L ? tc : R.tc[NR - 1];
-        R.ta[NR - 1] = lane == L ? ta : R.ta[NR - 1];
-        R.live[NR - 1] |= 1ull << L;
+        const bool num = elig && score == score;
+        const float m = key_f32(__builtin_amdgcn_readfirstlane(
+            group_min_i32<4>(num ? f32_key(score) : 0x7f800000)));
+        const int h = (int)__umulhi(u2, (uint32_t)S);
+        const int c0 = ((em >> h) & 1u) ? h : (em ? __builtin_ctz(em) : -1);
+        const uint32_t tie = (uint32_t)__ballot(num && score == m) & 0xFu;
+        const uint32_t nan = (uint32_t)__ballot(score != score) & 0xFu;
+        c = c0 < 0 ? -1 : ((((tie | nan) >> c0) & 1u) ? c0 : (tie ? __builtin_ctz(tie) : -1));
       }
+
+      // ---- FIFO service: every server lane prices the flow, server c's lane is pushed
+      const int32_t start_l = n > 0 ? (V.tail > ta ? V.tail : ta) : ta;
+      int32_t svc_l = (int32_t)(work * V.scale);
+      svc_l = svc_l < 1 ? 1 : svc_l;
+      const uint32_t fm = (uint32_t)__ballot(n == Q - 1) & 0xFu;  // servers one flow from full
+      const int cc = c < 0 ? 0 : c;
+      const int32_t tc = rdl(start_l + svc_l, cc);
+      const int wpc = rdl(V.wp, cc);
+      // ring lane (+ 64 x register) of the push; 128: none (dropped)
+      const int T = c < 0 ? 128 : cc * 32 + wpc;
+      if ((fm >> (c & 31)) & 1u) {  // rare: this push fills the ring -- keep the t_complete it
+        int32_t old = rdl(R.tc[0], T & 63);  // overwrites (the last completion)
+        if constexpr (NG > 1) old = T >= 64 ? rdl(R.tc[NG - 1], T & 63) : old;
+        V.saved = lane == c ? old : V.saved;
+      }
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        const bool w = lane + 64 * g == T;
+        R.tc[g] = w ? tc : R.tc[g];
+        R.ta[g] = w ? ta : R.ta[g];
+      }
+      const bool me = lane == c;
       V.tail = me ? tc : V.tail;
       V.wp = me ? (V.wp + 1 == Q ? 0 : V.wp + 1) : V.wp;
-      V.assigned += me ? 1 : 0;
-      V.pushed += me ? 1 : 0;
-      if (tc <= dt) {  // completes in this step: its sample now, with its arrival's draw word
-        const uint32_t rc = rdl(V.rcnt, c);
-        const int slot = reservoir_slot_r32(rc, E.u3);
-        if (slot >= 0 && me) {
-          res_b[(uint32_t)c * K + (uint32_t)slot] =
-              make_uint3((uint32_t)(tc - ta), (uint32_t)(tc - rdl(start_l, c)),
-                         base_ms + (base_rem + (uint32_t)tc) / 1000u);
-          atomicOr(chg + ((uint32_t)slot >> 5) * 4u + (uint32_t)c, 1u << (slot & 31));
-        }
-        V.rcnt = me ? count_inc(rc) : V.rcnt;
-      }
-    } else {
-      E.dropped += 1u;
-    }
+      E.dropped += c < 0 ? 1u : 0u;
+      // log for the batch's reservoir inserts
+      const bool lg = lane == bi;
+      Bt.lc = lg ? c : Bt.lc;
+      Bt.ltc = lg ? tc : Bt.ltc;
 
-    // ---- the next arrival: arrival arr_idx + 1 from the batch
-    if (bi == 64) {
-      wave_draw_batch<TRACE>(st, p, E, E.arr_idx + 1u, ta, lane, bta, bwk, bu2, bu3);
-      bi = 0;
+      // ---- the next arrival: the pushed flow is still queued at ta_n if tc > ta_n
+      const bool adj = me && tc > ta_n;
+      n = adj ? n_n + 1 : n_n;
+      score = adj ? sc1 : sc0;
+      ta = ta_n;
+      if (ta >= dt) {
+        done = true;
+        ++bi;
+        break;
+      }
     }
-    E.next_arr = rdl(bta, bi);
-    E.next_work = rdl(bwk, bi);
-    E.u2 = rdl(bu2, bi);
-    E.u3 = rdl(bu3, bi);
-    E.arr_idx += 1u;
-    ++bi;
+    wave_flush(p, V, Bt, bi, lane, res_b, Ld, seq++, base_ms, base_rem);
+    if (done) break;
+    base += 63u;
+    wave_draw_batch<TRACE>(st, p, E, base, ta, lane, Bt);
+    bi = 0;
   }
+  // the pending arrival (its time >= dt)
+  E.arr_idx = base + (uint32_t)bi;
+  E.next_arr = ta;
+  E.next_work = rdl(Bt.wk, bi);
+  E.u2 = rdl(Bt.u2, bi);
+  E.u3 = rdl(Bt.u3, bi);
 }
 
-template <int NR, int POLICY, bool TRACE>
+template <int NG, int POLICY, bool TRACE>
 __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParams& p, WaveEnv& E,
-                                              WaveSrv& V, WaveRing<NR>& R, int lane,
-                                              uint3* const res_b, WaveLds& Ld, float w_own) {
+                                              WaveSrv& V, WaveRing<NG>& R, int lane,
+                                              uint3* const res_b, WaveLds& Ld, uint32_t& seq,
+                                              float w_own) {
   constexpr bool lsq = (POLICY == 2 || POLICY == 3);
   const int S = p.S, Q = p.Q;
   const int32_t dt = p.dt_us;
   const uint64_t base_us = (uint64_t)E.clock * (uint64_t)dt;
   const uint32_t base_ms = (uint32_t)(base_us / 1000u);
   const uint32_t base_rem = (uint32_t)(base_us - (uint64_t)base_ms * 1000u);
-  const int rs = lane >> 4, rk = lane & (kWaveRingLanes - 1);  // ring lane: server, position
+  const int rpos = lane & 31;
   if (V.act && !lsq) {
     V.den = (double)w_own + 1e-9;
     V.rcp = 1.0 / V.den;
@@ -260,9 +358,9 @@ __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParam
   // ---- 1. carried-in flows that complete in this step, server lane by server lane, in FIFO
   //      order (their Algorithm R draws from the reservoir stream)
 #pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    const int pos = r * kWaveRingLanes + rk;
-    if (rs < S && pos < Q) Ld.img[pos * 4 + rs] = make_int2(R.tc[r], R.ta[r]);
+  for (int g = 0; g < NG; ++g) {
+    const int srv = 2 * g + (lane >> 5);
+    if (srv < S && rpos < Q) Ld.img[rpos * 4 + srv] = make_int2(R.tc[g], R.ta[g]);
   }
   wave_sync();
   if (V.act && V.cnt0 > 0) {
@@ -289,24 +387,26 @@ __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParam
     }
     V.rcnt = rc;
   }
+  wave_sync();
 
   // ---- 2. the arrivals (SED / SED2 scores are finite unless some den is 0 / inf / NaN)
   const bool finite = lsq || !V.act || (fabs(V.den) >= 1e-30 && fabs(V.den) <= 1e300);
   if (__all(finite))
-    wave_event_loop<NR, POLICY, TRACE, true>(st, p, E, V, R, lane, res_b, Ld.chg, base_ms,
+    wave_event_loop<NG, POLICY, TRACE, true>(st, p, E, V, R, lane, res_b, Ld, seq, base_ms,
                                              base_rem);
   else
-    wave_event_loop<NR, POLICY, TRACE, false>(st, p, E, V, R, lane, res_b, Ld.chg, base_ms,
+    wave_event_loop<NG, POLICY, TRACE, false>(st, p, E, V, R, lane, res_b, Ld, seq, base_ms,
                                               base_rem);
 
   // ---- 3. completions up to dt; the server's count, head and last completion
+  uint64_t live[NG];
 #pragma unroll
-  for (int r = 0; r < NR; ++r) R.live[r] &= __ballot(R.tc[r] > dt);
-  const int32_t n = wave_count<NR>(R, lane & 3);
+  for (int g = 0; g < NG; ++g) live[g] = __ballot(R.tc[g] > dt);
+  const int32_t n = wave_count<NG>(live, lane);
 #pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    const int pos = r * kWaveRingLanes + rk;
-    if (rs < S && pos < Q) Ld.img[pos * 4 + rs].x = R.tc[r];
+  for (int g = 0; g < NG; ++g) {
+    const int srv = 2 * g + (lane >> 5);
+    if (srv < S && rpos < Q) Ld.img[rpos * 4 + srv].x = R.tc[g];
   }
   wave_sync();
   if (V.act && V.cnt0 + V.pushed > n) {  // a flow completed this step: the newest one
@@ -314,7 +414,6 @@ __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParam
       V.last = V.saved;
     } else {
       int pl = V.wp - n - 1;
-      pl = pl < 0 ? pl + Q : pl;
       pl = pl < 0 ? pl + Q : pl;
       V.last = Ld.img[pl * 4 + lane].x;
     }
@@ -324,9 +423,9 @@ __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParam
   // ---- rebase to the next step's start
   E.next_arr -= dt;
 #pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    R.tc[r] -= dt;
-    R.ta[r] -= dt;
+  for (int g = 0; g < NG; ++g) {  // completed flows free their slots
+    R.tc[g] = R.tc[g] > dt ? R.tc[g] - dt : kDead;
+    R.ta[g] -= dt;
   }
   V.tail -= dt;
   V.last = (V.last < kLastNone + dt) ? kLastNone : V.last - dt;
@@ -334,7 +433,7 @@ __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParam
 }
 
 // One dynamics launch for env b (one wave): state in, the step (or reset + warm-up), state out.
-template <int NR, int MODE, int POLICY, bool TRACE>
+template <int NG, int MODE, int POLICY, bool TRACE>
 __global__ void __launch_bounds__(64)
     dynamics_wave_kernel(DevState st, SimParams p, const void* action, int action_dtype,
                          int32_t* assign_out, const uint8_t* reset_mask) {
@@ -344,7 +443,7 @@ __global__ void __launch_bounds__(64)
   if (MODE == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
   const int lane = (int)threadIdx.x;
   const int S = p.S, Q = p.Q;
-  const int rs = lane >> 4, rk = lane & (kWaveRingLanes - 1);
+  const int rpos = lane & 31;
   uint3* const res_b = st.res + (size_t)b * (size_t)S * K;
 
   WaveEnv E;
@@ -359,12 +458,14 @@ __global__ void __launch_bounds__(64)
   V.assigned = 0;
   V.saved = 0;
   if (lane < 16) Ld.chg[lane] = 0u;
-  WaveRing<NR> R;
 #pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    R.tc[r] = 0;
-    R.ta[r] = 0;
-    R.live[r] = 0ull;
+  for (int i = 0; i < 8; ++i) Ld.own[i * 64 + lane] = 0u;
+  uint32_t seq = 1u;
+  WaveRing<NG> R;
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    R.tc[g] = kDead;
+    R.ta[g] = 0;
   }
   const uint32_t sb = b * (uint32_t)S + (uint32_t)lane;  // server lane's server (lane < S)
 
@@ -398,7 +499,7 @@ __global__ void __launch_bounds__(64)
     V.rcnt = 0u;
     wave_sync();
     for (int k = 0; k < p.warmup_steps; ++k)
-      sim_step_wave<NR, POLICY, TRACE>(st, p, E, V, R, lane, res_b, Ld, 1.0f);
+      sim_step_wave<NG, POLICY, TRACE>(st, p, E, V, R, lane, res_b, Ld, seq, 1.0f);
     if (lane == 0) {
       st.ep_step[b] = 0;
       st.ep_return[b] = 0.0;
@@ -413,30 +514,21 @@ __global__ void __launch_bounds__(64)
     E.u2 = st.next_u2[b];
     E.u3 = st.next_u3[b];
     // ring lanes: this lane's ring positions, live if within [head, head + count)
-    bool lv[NR];
 #pragma unroll
-    for (int r = 0; r < NR; ++r) lv[r] = false;
-    if (rs < S) {
-      const uint32_t hc = st.hc[b * (uint32_t)S + (uint32_t)rs];
-      const int head = (int)(hc & 0xFFFFu), cnt = (int)(hc >> 16);
-      const int2* ring = st.ring + (size_t)(b * (uint32_t)S + (uint32_t)rs) * (size_t)Q;
-#pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        const int pos = r * kWaveRingLanes + rk;
-        if (pos < Q) {
-          int rel = pos - head;
-          rel = rel < 0 ? rel + Q : rel;
-          lv[r] = rel < cnt;
-          if (lv[r]) {
-            const int2 e = ring[pos];
-            R.tc[r] = e.x;
-            R.ta[r] = e.y;
-          }
+    for (int g = 0; g < NG; ++g) {
+      const int srv = 2 * g + (lane >> 5);
+      if (srv < S && rpos < Q) {
+        const uint32_t hc = st.hc[b * (uint32_t)S + (uint32_t)srv];
+        const int head = (int)(hc & 0xFFFFu), cnt = (int)(hc >> 16);
+        int rel = rpos - head;
+        rel = rel < 0 ? rel + Q : rel;
+        if (rel < cnt) {
+          const int2 e = st.ring[(size_t)(b * (uint32_t)S + (uint32_t)srv) * (size_t)Q + rpos];
+          R.tc[g] = e.x;
+          R.ta[g] = e.y;
         }
       }
     }
-#pragma unroll
-    for (int r = 0; r < NR; ++r) R.live[r] = __ballot(lv[r]);
     V.cnt0 = 0;
     V.wp = 0;
     V.tail = 0;
@@ -447,7 +539,7 @@ __global__ void __launch_bounds__(64)
       const uint32_t hc = st.hc[sb];
       const int head = (int)(hc & 0xFFFFu);
       V.cnt0 = (int32_t)(hc >> 16);
-      int wp = head + V.cnt0;
+      const int wp = head + V.cnt0;
       V.wp = wp >= Q ? wp - Q : wp;
       V.last = st.last_tc[sb];
       V.rcnt = st.res_count[sb];
@@ -458,17 +550,16 @@ __global__ void __launch_bounds__(64)
       w_own = action_weight(p, action, action_dtype, (size_t)sb);
     }
     wave_sync();
-    sim_step_wave<NR, POLICY, TRACE>(st, p, E, V, R, lane, res_b, Ld, w_own);
+    sim_step_wave<NG, POLICY, TRACE>(st, p, E, V, R, lane, res_b, Ld, seq, w_own);
   }
 
   // ---- state out: the queued flows, the server fields, the env words
-  if (rs < S) {
-    int2* ring = st.ring + (size_t)(b * (uint32_t)S + (uint32_t)rs) * (size_t)Q;
 #pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      const int pos = r * kWaveRingLanes + rk;
-      if (pos < Q && ((R.live[r] >> lane) & 1ull)) ring[pos] = make_int2(R.tc[r], R.ta[r]);
-    }
+  for (int g = 0; g < NG; ++g) {
+    const int srv = 2 * g + (lane >> 5);
+    if (srv < S && rpos < Q && R.tc[g] > 0)  // queued (rebased: t_complete > 0)
+      st.ring[(size_t)(b * (uint32_t)S + (uint32_t)srv) * (size_t)Q + rpos] =
+          make_int2(R.tc[g], R.ta[g]);
   }
   wave_sync();
   if (V.act) {
