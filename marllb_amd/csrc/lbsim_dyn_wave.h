@@ -81,8 +81,10 @@ struct WaveBatch {
   int32_t ltc;    // logged: t_complete of the pushed flow
 };
 
+constexpr int kWaveKeyStride = 34;  // key table entries per server: n = 0 .. Q + 1 (Q <= 32)
 struct WaveLds {
   int2 img[32 * 4];       // ring image [pos][server] for the carried-in walk and `last`
+  int32_t kt[4 * kWaveKeyStride];  // FAST single-choice keys of this step [server][n]
   uint32_t own[4 * 128];  // insert owner of each (server, slot) in a flush: seq << 6 | lane
   uint32_t chg[4 * 4];    // written-slot masks [word][server]
 };
@@ -118,12 +120,15 @@ __device__ __forceinline__ void wave_draw_batch(const DevState& st, const SimPar
     gap = (int32_t)(-lb_logf(u01_open0(d.x)) * p.mean_gap_us);
     wk = -lb_logf(u01_open0(d.y));
   }
-  int32_t t = lane == 0 ? 0 : gap;  // inclusive prefix sum over the wave
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int32_t v = __shfl_up(t, (unsigned)o, 64);
-    t += lane >= o ? v : 0;
-  }
+  // inclusive prefix sum over the wave by DPP: row_shr 1 / 2 / 4 / 8 within each row of 16, then
+  // row_bcast:15 and row_bcast:31 carry the row totals (no LDS round trips)
+  int32_t t = lane == 0 ? 0 : gap;
+  t += __builtin_amdgcn_update_dpp(0, t, 0x111, 0xF, 0xF, false);  // row_shr:1
+  t += __builtin_amdgcn_update_dpp(0, t, 0x112, 0xF, 0xF, false);  // row_shr:2
+  t += __builtin_amdgcn_update_dpp(0, t, 0x114, 0xF, 0xF, false);  // row_shr:4
+  t += __builtin_amdgcn_update_dpp(0, t, 0x118, 0xF, 0xF, false);  // row_shr:8
+  t += __builtin_amdgcn_update_dpp(0, t, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  t += __builtin_amdgcn_update_dpp(0, t, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
   Bt.ta = t0 + t;
   Bt.wk = wk;
   Bt.u2 = d.z;
@@ -190,6 +195,12 @@ __device__ __forceinline__ void wave_flush(const SimParams& p, WaveSrv& V, const
 }
 
 // The arrivals of one step.
+//
+// FAST single-choice policies (SED / LSQ with finite scores) read their keys from a per-step LDS
+// table kt[s][n] = the order key of server s's score at n queued flows (0x7FFFFFFF: full): an
+// iteration fetches the keys for both outcomes of its push (n and n + 1 at the next arrival) in
+// one ds_read2 before it chooses, and the choice -> choice chain is a select, a DPP minimum and
+// a ballot.  SED2 / LSQ2 and non-finite SED compute their scores in the loop.
 template <int NG, int POLICY, bool TRACE, bool FAST>
 __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimParams& p,
                                                 WaveEnv& E, WaveSrv& V, WaveRing<NG>& R,
@@ -198,9 +209,40 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
                                                 uint32_t base_rem) {
   constexpr bool two_choice = (POLICY == 1 || POLICY == 3);
   constexpr bool lsq = (POLICY == 2 || POLICY == 3);
+  constexpr bool TAB = FAST && !two_choice;
+  constexpr int KT = kWaveKeyStride;
   const int S = p.S, Q = p.Q;
   const int32_t dt = p.dt_us;
   if (E.next_arr >= dt) return;
+
+  auto score_of = [&](int32_t nn, double den, double rcp) -> float {  // node.c:393-404
+    if constexpr (lsq) {
+      return (float)nn;
+    } else {
+      const double c1 = (double)(nn + 1);
+      const double q0 = c1 * rcp;
+      double q = fma(fma(-q0, den, c1), rcp, q0);
+      if (!FAST && q != q) {
+        asm volatile("");
+        q = c1 / den;
+      }
+      return (float)q;
+    }
+  };
+  const int s4 = lane & 3;  // the server whose queue count this lane holds
+  int32_t* const kt_s = Ld.kt + s4 * KT;
+  if constexpr (TAB) {
+    // the step's key table: lanes 16 s .. 16 s + 15 fill server s's entries n = 0 .. Q + 1
+    const int ts = lane >> 4;
+    const double den = __shfl(V.den, ts, 64), rcp = __shfl(V.rcp, ts, 64);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int nn = (lane & 15) + 16 * k;
+      if (nn < Q + 2)  // servers past S: never eligible
+        Ld.kt[ts * KT + nn] = (nn < Q && ts < S) ? f32_key(score_of(nn, den, rcp)) : 0x7FFFFFFF;
+    }
+    wave_sync();
+  }
 
   // batch 0: lane 0 is the pending arrival (its stored draw), lanes 1..63 the next ones
   uint32_t base = E.arr_idx;
@@ -212,66 +254,68 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
   int bi = 0;  // batch lane of the current arrival
   int32_t ta = E.next_arr;
 
-  // per-lane constants: the shift that brings server lane s's half of a ring mask to bits 0..31
-  const uint32_t half_sh = (uint32_t)(lane & 1) * 32u;
-  const bool hi_reg = (lane & 2) != 0;
-  auto count_at = [&](int32_t t) -> int32_t {  // server lane's flows queued at time t
-    const uint32_t w0 = (uint32_t)(__ballot(R.tc[0] > t) >> half_sh);
+  // server lane s's flows queued at time t: the popcounts of the four ring-lane halves (scalar),
+  // packed as 16-bit fields and unpacked by one shift per lane
+  const uint32_t cnt_sh = (uint32_t)(lane & 3) * 16u;
+  auto count_at = [&](int32_t t) -> int32_t {
+    const uint64_t m0 = __ballot(R.tc[0] > t);
+    uint64_t packed = (uint64_t)__builtin_popcount((uint32_t)m0) |
+                      ((uint64_t)__builtin_popcount((uint32_t)(m0 >> 32)) << 16);
     if constexpr (NG > 1) {
-      const uint32_t w1 = (uint32_t)(__ballot(R.tc[NG - 1] > t) >> half_sh);
-      return __builtin_popcount(hi_reg ? w1 : w0);
+      const uint64_t m1 = __ballot(R.tc[NG - 1] > t);
+      packed |= ((uint64_t)__builtin_popcount((uint32_t)m1) << 32) |
+                ((uint64_t)__builtin_popcount((uint32_t)(m1 >> 32)) << 48);
     }
-    return __builtin_popcount(w0);
-  };
-  auto score_of = [&](int32_t nn) -> float {  // node.c:393-404 (SED) / the count (LSQ)
-    if constexpr (lsq) {
-      return (float)nn;
-    } else {
-      const double c1 = (double)(nn + 1);
-      const double q0 = c1 * V.rcp;
-      double q = fma(fma(-q0, V.den, c1), V.rcp, q0);
-      if (!FAST && q != q) {
-        asm volatile("");
-        q = c1 / V.den;
-      }
-      return (float)q;
-    }
+    return (int32_t)((uint32_t)(packed >> cnt_sh) & 0xFFFFu);
   };
   const uint32_t smask = (1u << S) - 1u;  // server lanes
+  // push lane of server lane s: ring register (s >> 1) x 64 + lane 32 (s & 1) + write position
+  int32_t pl = lane * 32 + V.wp;
+  const int32_t pl_wrap = lane * 32 + Q;
   int32_t n = count_at(ta);
-  float score = score_of(n);
+  int32_t key = 0;
+  float score = 0.f;
+  if constexpr (TAB) key = kt_s[n];
+  else score = score_of(n, V.den, V.rcp);
   for (;;) {      // batches
-    bool done = false;
-    for (; bi < 63; ++bi) {  // arrivals bi = 0 .. 62 (lane 63 opens the next batch)
+    for (;;) {    // arrivals bi = 0 .. 62 (lane 63 opens the next batch)
       const float work = rdl(Bt.wk, bi);
       const uint32_t u2 = rdl(Bt.u2, bi);
       // ---- look-ahead: the next arrival's queue counts without the flow pushed now, and the
-      //      scores for both outcomes (off the choice -> choice chain)
+      //      keys / scores for both outcomes (off the choice -> choice chain)
       const int32_t ta_n = rdl(Bt.ta, bi + 1);
       const int32_t n_n = count_at(ta_n);
-      const float sc0 = score_of(n_n), sc1 = score_of(n_n + 1);
-      // issue them here, before the choice (the in-order wave would otherwise run them after it)
-      asm volatile("" ::"v"(n_n), "v"(sc0), "v"(sc1));
+      int32_t k0 = 0, k1 = 0;
+      float sc0 = 0.f, sc1 = 0.f;
+      if constexpr (TAB) {
+        k0 = kt_s[n_n];
+        k1 = kt_s[n_n + 1];
+      } else {
+        sc0 = score_of(n_n, V.den, V.rcp);
+        sc1 = score_of(n_n + 1, V.den, V.rcp);
+        // issue them before the choice (the in-order wave would otherwise run them after it)
+        asm volatile("" ::"v"(sc0), "v"(sc1));
+      }
 
       // ---- the arrival's server (node.c:388-441); full servers are not eligible
-      const bool elig = n < Q && lane < S;
-      const uint32_t em = (uint32_t)__ballot(n < Q) & smask;
       int c = -1;
-      if constexpr (two_choice) {
+      if constexpr (TAB) {
+        // finite scores: the eligible minimum, h among equal minima, else the lowest such server
+        const int32_t mk = __builtin_amdgcn_readfirstlane(group_min_i32<4>(key));
+        const int h = (int)__umulhi(u2, (uint32_t)S);
+        const uint32_t tie = (uint32_t)__ballot(key == mk) & smask;
+        c = ((tie >> h) & 1u) ? h : __builtin_ctz(tie);
+        c = mk == 0x7FFFFFFF ? -1 : c;
+      } else if constexpr (two_choice) {
+        const uint32_t em = (uint32_t)__ballot(n < Q) & smask;
         const int h1 = two_choice_h1(u2, S);
         const int h2 = two_choice_h2(u2, S);
         const float s1 = rdl(score, h1), s2 = rdl(score, h2);
         const bool ok1 = (em >> h1) & 1u, ok2 = (em >> h2) & 1u;
         c = (ok1 && ok2) ? ((s2 < s1) ? h2 : h1) : (ok1 ? h1 : (ok2 ? h2 : -1));
-      } else if constexpr (FAST) {
-        // finite scores: the eligible minimum, h among equal minima, else the lowest such server
-        const int32_t key = elig ? f32_key(score) : 0x7FFFFFFF;
-        const int32_t mk = __builtin_amdgcn_readfirstlane(group_min_i32<4>(key));
-        const int h = (int)__umulhi(u2, (uint32_t)S);
-        const uint32_t tie = (uint32_t)__ballot(key == mk) & em;
-        c = ((tie >> h) & 1u) ? h : __builtin_ctz(tie);
-        c = tie == 0u ? -1 : c;
       } else {
+        const bool elig = n < Q && lane < S;
+        const uint32_t em = (uint32_t)__ballot(n < Q) & smask;
         const bool num = elig && score == score;
         const float m = key_f32(__builtin_amdgcn_readfirstlane(
             group_min_i32<4>(num ? f32_key(score) : 0x7f800000)));
@@ -281,18 +325,17 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
         const uint32_t nan = (uint32_t)__ballot(score != score) & 0xFu;
         c = c0 < 0 ? -1 : ((((tie | nan) >> c0) & 1u) ? c0 : (tie ? __builtin_ctz(tie) : -1));
       }
+      const bool lg = lane == bi;  // this arrival's batch lane (the insert log)
 
-      // ---- FIFO service: every server lane prices the flow, server c's lane is pushed
-      const int32_t start_l = n > 0 ? (V.tail > ta ? V.tail : ta) : ta;
+      // ---- FIFO service on server c: every server lane prices the flow (an empty server's tail
+      //      completed by ta, so max(tail, ta) is the start either way).  A dropped flow (c = -1:
+      //      every server full, rare) runs the same straight line: lane -1 reads lane 63, whose
+      //      push lane (>= 128) matches no ring lane, and no lane is `me`.
       int32_t svc_l = (int32_t)(work * V.scale);
       svc_l = svc_l < 1 ? 1 : svc_l;
-      const uint32_t fm = (uint32_t)__ballot(n == Q - 1) & 0xFu;  // servers one flow from full
-      const int cc = c < 0 ? 0 : c;
-      const int32_t tc = rdl(start_l + svc_l, cc);
-      const int wpc = rdl(V.wp, cc);
-      // ring lane (+ 64 x register) of the push; 128: none (dropped)
-      const int T = c < 0 ? 128 : cc * 32 + wpc;
-      if ((fm >> (c & 31)) & 1u) {  // rare: this push fills the ring -- keep the t_complete it
+      const int32_t tc = rdl((V.tail > ta ? V.tail : ta) + svc_l, c);
+      const int T = rdl(pl, c);  // ring register x 64 + lane of the push
+      if (rdl(n, c) == Q - 1) {  // rare: this push fills the ring -- keep the t_complete it
         int32_t old = rdl(R.tc[0], T & 63);  // overwrites (the last completion)
         if constexpr (NG > 1) old = T >= 64 ? rdl(R.tc[NG - 1], T & 63) : old;
         V.saved = lane == c ? old : V.saved;
@@ -305,30 +348,27 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
       }
       const bool me = lane == c;
       V.tail = me ? tc : V.tail;
-      V.wp = me ? (V.wp + 1 == Q ? 0 : V.wp + 1) : V.wp;
+      const int32_t pl1 = pl + 1 == pl_wrap ? lane * 32 : pl + 1;
+      pl = me ? pl1 : pl;
       E.dropped += c < 0 ? 1u : 0u;
-      // log for the batch's reservoir inserts
-      const bool lg = lane == bi;
       Bt.lc = lg ? c : Bt.lc;
       Bt.ltc = lg ? tc : Bt.ltc;
-
       // ---- the next arrival: the pushed flow is still queued at ta_n if tc > ta_n
       const bool adj = me && tc > ta_n;
       n = adj ? n_n + 1 : n_n;
+      key = adj ? k1 : k0;
       score = adj ? sc1 : sc0;
+      ++bi;
       ta = ta_n;
-      if (ta >= dt) {
-        done = true;
-        ++bi;
-        break;
-      }
+      if (ta >= dt || bi == 63) break;
     }
     wave_flush(p, V, Bt, bi, lane, res_b, Ld, seq++, base_ms, base_rem);
-    if (done) break;
+    if (ta >= dt) break;
     base += 63u;
     wave_draw_batch<TRACE>(st, p, E, base, ta, lane, Bt);
     bi = 0;
   }
+  V.wp = pl - lane * 32;
   // the pending arrival (its time >= dt)
   E.arr_idx = base + (uint32_t)bi;
   E.next_arr = ta;

@@ -7,3 +7,4 @@ done
 for w in 1 0; do
   LBSIM_DYN_WAVE=$w timeout -k 10 200 python tools/single_env_latency.py --steps 1000 >> $O/latency.jsonl 2>> $O/err.log || exit 13
 done
+timeout -k 10 200 python tools/single_env_breakdown.py --steps 1000 > $O/breakdown.json 2>> $O/err.log || exit 14
