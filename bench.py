@@ -535,10 +535,12 @@ def main():
 
     if rank == 0:
         value = lbdist.throughput(shard, args.steps, elapsed)
-        # a step is one fused_step_kernel launch (default) or dynamics_group_kernel (one lane per
-        # server) / dynamics_kernel (one lane per env, --dyn-mapping env) then observe_kernel;
+        # a step is one fused_step_kernel launch (opt-in) or a dynamics launch -- dynamics_group_kernel
+        # (one lane per server), dynamics_wave_kernel (one wave per env, small S <= 4 batches) or
+        # dynamics_kernel (one lane per env, --dyn-mapping env) -- then observe_kernel;
         # lbsim_profile times each class
-        dyn = "dynamics_kernel" if args.dyn_mapping == "env" else "dynamics_group_kernel"
+        dyn = ("dynamics_kernel", "dynamics_group_kernel",
+               "dynamics_wave_kernel")[lib.lbsim_dynamics_kernel(handle.h)]
         names = {0: dyn, 1: "observe_kernel", 4: "fused_step_kernel"}
         avg = {names[i]: ms[i] / cnt[i] for i in names if cnt[i] > 0}
         rate = tr.rate if tr is not None else ARRIVAL_RATE

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define LBSIM_ABI_VERSION 3
+#define LBSIM_ABI_VERSION 4
 #define LBSIM_MAX_SERVERS 64   /* S <= 64: BASELINE configs[4] read literally is 4 agents x 16 */
                                /* servers = 64 (S > 16: server-per-lane dynamics only)       */
 #define LBSIM_RESERVOIR_K 128  /* reservoir.py:31 capacity=128, reservoir.h:24               */
@@ -85,7 +85,16 @@ enum lbsim_dyn_mapping {
   LBSIM_DYN_ENV_PER_LANE = 1,    /* one lane = one env                                        */
   LBSIM_DYN_SERVER_PER_LANE = 2  /* a group of G lanes = one env, one lane per server: G =     */
                                  /* pow2 >= S, except S <= 4 on small batches (B*4/64 <= half */
-                                 /* the device's SIMDs), which get G = 8 (twice the waves)     */
+                                 /* the device's SIMDs), which get G = 8 (twice the waves);    */
+                                 /* S <= 4 batches of at most 4 envs per SIMD (Q <= 32, no     */
+                                 /* ALIAS) run one WAVE per env instead         */
+};
+
+/* The dynamics kernel a handle's launches use (lbsim_dynamics_kernel). */
+enum lbsim_dyn_kernel {
+  LBSIM_DYN_KERNEL_ENV_LANE = 0,  /* dynamics_kernel: one lane per env                        */
+  LBSIM_DYN_KERNEL_GROUP = 1,     /* dynamics_group_kernel: one lane per server, G-lane groups */
+  LBSIM_DYN_KERNEL_WAVE = 2       /* dynamics_wave_kernel: one wave per env                    */
 };
 
 /* How lbsim_step runs; every choice produces the same bits.  FUSED: one launch per step whose
@@ -152,6 +161,11 @@ const char* lbsim_last_error(const lbsim_t* h);
 
 /* Re-key the RNG and rewind every env's episode counter (env.py:327-330 seed()). */
 int lbsim_seed(lbsim_t* h, uint64_t seed);
+
+/* Which dynamics kernel (lbsim_dyn_kernel) this handle's step and reset launches use, for the
+ * handle's shape, config and the LBSIM_DYN_* environment overrides; -1 on a NULL handle.  No
+ * GPU work (measurement labels; the reference has no counterpart). */
+int lbsim_dynamics_kernel(const lbsim_t* h);
 
 /*
  * Reset the envs whose env_mask[b] != 0 (env_mask == NULL: all envs) and write their first

@@ -127,6 +127,7 @@ _SIGNATURES = {
     "lbsim_destroy": (ctypes.c_int, [_P]),
     "lbsim_last_error": (ctypes.c_char_p, [_P]),
     "lbsim_seed": (ctypes.c_int, [_P, ctypes.c_uint64]),
+    "lbsim_dynamics_kernel": (ctypes.c_int, [_P]),
     "lbsim_reset": (ctypes.c_int, [_P, _P, _P, _P]),
     "lbsim_step": (ctypes.c_int, [_P, _P, ctypes.c_int, _P, _P, _P, _P, _P]),
     "lbsim_step_ex": (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.POINTER(StepOutputs), _P]),

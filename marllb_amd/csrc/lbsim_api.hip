@@ -447,6 +447,13 @@ const char* lbsim_last_error(const lbsim_t* h) {
   return h ? h->err.c_str() : g_create_err.c_str();
 }
 
+int lbsim_dynamics_kernel(const lbsim_t* h) {
+  if (h == nullptr) return -1;
+  const LaunchCtx L = ctx(h);
+  if (dyn_wave_ok(L)) return LBSIM_DYN_KERNEL_WAVE;
+  return dyn_group_lanes(L) == 0 ? LBSIM_DYN_KERNEL_ENV_LANE : LBSIM_DYN_KERNEL_GROUP;
+}
+
 int lbsim_seed(lbsim_t* h, uint64_t seed) {
   if (h == nullptr) return LBSIM_EINVAL;
   DeviceGuard g(h->device);

@@ -278,7 +278,11 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
   if constexpr (TAB) key = kt_s[n];
   else score = score_of(n, V.den, V.rcp);
   for (;;) {      // batches
-    for (;;) {    // arrivals bi = 0 .. 62 (lane 63 opens the next batch)
+    // arrivals bi .. lim - 1 of this batch come before dt (times increase with the lane); lane 63
+    // opens the next batch
+    const int lim = __builtin_ctzll(__ballot(Bt.ta >= dt) | (1ull << 63));
+    for (; bi < lim; ++bi) {
+      const int32_t ta = rdl(Bt.ta, bi);
       const float work = rdl(Bt.wk, bi);
       const uint32_t u2 = rdl(Bt.u2, bi);
       // ---- look-ahead: the next arrival's queue counts without the flow pushed now, and the
@@ -358,11 +362,9 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
       n = adj ? n_n + 1 : n_n;
       key = adj ? k1 : k0;
       score = adj ? sc1 : sc0;
-      ++bi;
-      ta = ta_n;
-      if (ta >= dt || bi == 63) break;
     }
     wave_flush(p, V, Bt, bi, lane, res_b, Ld, seq++, base_ms, base_rem);
+    ta = rdl(Bt.ta, bi);
     if (ta >= dt) break;
     base += 63u;
     wave_draw_batch<TRACE>(st, p, E, base, ta, lane, Bt);
@@ -557,16 +559,14 @@ __global__ void __launch_bounds__(64)
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       const int srv = 2 * g + (lane >> 5);
-      if (srv < S && rpos < Q) {
+      if (srv < S && rpos < Q) {  // the slot and its server's head / count, loaded together
+        const int2 e = st.ring[(size_t)(b * (uint32_t)S + (uint32_t)srv) * (size_t)Q + rpos];
         const uint32_t hc = st.hc[b * (uint32_t)S + (uint32_t)srv];
         const int head = (int)(hc & 0xFFFFu), cnt = (int)(hc >> 16);
         int rel = rpos - head;
         rel = rel < 0 ? rel + Q : rel;
-        if (rel < cnt) {
-          const int2 e = st.ring[(size_t)(b * (uint32_t)S + (uint32_t)srv) * (size_t)Q + rpos];
-          R.tc[g] = e.x;
-          R.ta[g] = e.y;
-        }
+        R.tc[g] = rel < cnt ? e.x : kDead;
+        R.ta[g] = e.y;
       }
     }
     V.cnt0 = 0;
@@ -583,11 +583,15 @@ __global__ void __launch_bounds__(64)
       V.wp = wp >= Q ? wp - Q : wp;
       V.last = st.last_tc[sb];
       V.rcnt = st.res_count[sb];
-      if (V.cnt0 > 0) {
-        const int tp = V.wp == 0 ? Q - 1 : V.wp - 1;
-        V.tail = st.ring[(size_t)sb * (size_t)Q + (size_t)tp].x;
-      }
       w_own = action_weight(p, action, action_dtype, (size_t)sb);
+    }
+    {  // tail = t_complete of the last queued flow, from the ring lanes (no dependent load)
+      const int tp = V.wp == 0 ? Q - 1 : V.wp - 1;
+      const int src = (lane & 1) * 32 + (tp & 31);
+      const int32_t t0 = __shfl(R.tc[0], src, 64);
+      const int32_t t1 = __shfl(R.tc[NG - 1], src, 64);
+      const int32_t tl = (lane & 2) ? t1 : t0;
+      V.tail = (V.act && V.cnt0 > 0) ? tl : 0;
     }
     wave_sync();
     sim_step_wave<NG, POLICY, TRACE>(st, p, E, V, R, lane, res_b, Ld, seq, w_own);

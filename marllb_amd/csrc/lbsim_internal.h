@@ -52,8 +52,11 @@ inline int dyn_group_lanes(const LaunchCtx& L) {
 
 // One wave per env (lbsim_dyn_wave.h): S <= 4, Q <= 32, SED / SED2 / LSQ / LSQ2, the default
 // mapping, and a batch small enough that one env's event-loop chain, not issue throughput, sets
-// the step time: B <= LBSIM_DYN_WAVE_MAX_B (default 8192).  LBSIM_DYN_WAVE = 0 disables it, 1 uses
-// it at every batch size it applies to; a forced LBSIM_DYN_GROUP_LANES width wins over both.
+// the step time: at most 4 waves (envs) per SIMD, B <= 4096 on 256 CUs.  Measured S = 4 dynamics,
+// wave vs server-per-lane groups (profiles/r03w/wave_sweep.txt): 1024 envs 0.041 vs 0.084 ms,
+// 4096 0.066 vs 0.090, 8192 0.108 vs 0.095 (8 waves per SIMD: issue-bound, the groups win).
+// LBSIM_DYN_WAVE_MAX_B overrides the limit; LBSIM_DYN_WAVE = 0 disables the kernel, 1 uses it at
+// every batch size it applies to; a forced LBSIM_DYN_GROUP_LANES width wins over both.
 inline bool dyn_wave_ok(const LaunchCtx& L) {
   static const int mode = [] {
     const char* e = std::getenv("LBSIM_DYN_WAVE");
@@ -61,12 +64,12 @@ inline bool dyn_wave_ok(const LaunchCtx& L) {
   }();
   static const int64_t max_b = [] {
     const char* e = std::getenv("LBSIM_DYN_WAVE_MAX_B");
-    return e ? (int64_t)std::atoll(e) : (int64_t)8192;
+    return e ? (int64_t)std::atoll(e) : (int64_t)-1;
   }();
   static const bool forced_lanes = std::getenv("LBSIM_DYN_GROUP_LANES") != nullptr;
   if (mode == 0 || forced_lanes || L.dyn_mapping == LBSIM_DYN_ENV_PER_LANE) return false;
   if (L.S > 4 || L.prm.Q > 32 || L.prm.policy == LBSIM_POLICY_ALIAS) return false;
-  return mode == 1 || (int64_t)L.B <= max_b;
+  return mode == 1 || (int64_t)L.B <= (max_b >= 0 ? max_b : 4 * (int64_t)L.simds);
 }
 
 // Dynamics of one step (mode kModeStep) or of a reset with warm-up (kModeReset).

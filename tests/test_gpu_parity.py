@@ -443,3 +443,21 @@ def test_full_size_trace_replay_c3(lib, oracle_mod):
         oo, ro, _, _ = ora.step(np.ascontiguousarray(a[off:off + n]))
     np.testing.assert_array_equal(obs[off:off + n].cpu().numpy(), oo)
     np.testing.assert_array_equal(rew[off:off + n].cpu().numpy(), ro)
+
+
+def test_dynamics_kernel_dispatch(lib):
+    """lbsim_dynamics_kernel names the kernel the launches use: one wave per env for small S <= 4
+    batches (at most 4 envs per SIMD, queue capacity <= 32, not ALIAS), server-per-lane groups
+    otherwise, one lane per env when asked for."""
+    from marllb_amd.env import VecLoadBalanceEnv
+    cases = [(dict(num_envs=257, num_servers=4), 2), (dict(num_envs=1, num_servers=4), 2),
+             (dict(num_envs=8256, num_servers=4), 1), (dict(num_envs=64, num_servers=8), 1),
+             (dict(num_envs=64, num_servers=4, assign_policy="alias"), 1),
+             (dict(num_envs=64, num_servers=4, queue_capacity=64), 1),
+             (dict(num_envs=64, num_servers=4, dyn_mapping="env"), 0)]
+    for kw, want in cases:
+        kw = dict(kw)
+        B, S = kw.pop("num_envs"), kw.pop("num_servers")
+        env = VecLoadBalanceEnv(B, S, device="cuda:0", **kw)
+        assert env.handle.lib.lbsim_dynamics_kernel(env.handle.h) == want, (B, S, kw)
+        env.close()
