@@ -98,10 +98,11 @@ enum lbsim_dyn_kernel {
 };
 
 /* How lbsim_step runs; every choice produces the same bits.  FUSED: one launch per step whose
- * workgroups simulate their envs and then observe them; SPLIT: a dynamics launch
- * and an observe launch.  AUTO = SPLIT (the fused form measured slower); FUSED
- * exists for server-per-lane groups of <= 16 lanes (else SPLIT).  The environment variable
- * LBSIM_STEP_KERNEL=split|fused overrides AUTO. */
+ * workgroups simulate their envs and then observe them: step_wave_kernel for
+ * one-wave-per-env handles, fused_step_kernel for server-per-lane groups of <= 16 lanes (else
+ * SPLIT); SPLIT: a dynamics launch and an observe launch.  AUTO = SPLIT (both fused forms
+ * measured slower).  The environment variable LBSIM_STEP_KERNEL=split|fused
+ * overrides AUTO. */
 enum lbsim_step_kernel { LBSIM_STEP_AUTO = 0, LBSIM_STEP_SPLIT = 1, LBSIM_STEP_FUSED = 2 };
 
 /*

@@ -294,18 +294,30 @@ ObsOutputs obs_outputs(const lbsim_step_outputs_t* out, bool reset) {
   return o;
 }
 
-// The fused step for this handle: its config (LBSIM_STEP_KERNEL=split|fused overrides AUTO) and
-// a group width that has a fused form.
-bool use_fused_step(const lbsim_t* h) {
+// The step kernel a handle asks for: its config, else LBSIM_STEP_KERNEL=split|fused, else AUTO.
+int step_kernel_of(const lbsim_t* h) {
   static const int env = [] {
     const char* e = std::getenv("LBSIM_STEP_KERNEL");
     if (e != nullptr && std::strcmp(e, "split") == 0) return LBSIM_STEP_SPLIT;
     if (e != nullptr && std::strcmp(e, "fused") == 0) return LBSIM_STEP_FUSED;
     return LBSIM_STEP_AUTO;
   }();
+  return h->cfg.step_kernel != LBSIM_STEP_AUTO ? h->cfg.step_kernel : env;
+}
+
+// The one-launch wave step (step_wave_kernel): one wave per env and FUSED asked for.  AUTO is the
+// two launches here too: the one-launch form measured slower (4096 x 4: 0.141 ms against 0.066 +
+// 0.019 ms, profiles/r03w/ab_step_wave_fused.txt -- the observe phase needs ~190 VGPRs inlined,
+// and out of line its call frames go through scratch).
+bool use_step_wave(const lbsim_t* h) {
+  return step_kernel_of(h) == LBSIM_STEP_FUSED && dyn_wave_ok(ctx(h));
+}
+
+// The fused step for this handle: its config (LBSIM_STEP_KERNEL=split|fused overrides AUTO) and
+// a group width that has a fused form.
+bool use_fused_step(const lbsim_t* h) {
   // AUTO = SPLIT: the fused kernel measured slower at every shape tried
-  const int k = h->cfg.step_kernel != LBSIM_STEP_AUTO ? h->cfg.step_kernel : env;
-  if (k != LBSIM_STEP_FUSED) return false;
+  if (step_kernel_of(h) != LBSIM_STEP_FUSED) return false;
   const int g = dyn_group_lanes(ctx(h));
   return g >= 2 && g <= 16;
 }
@@ -523,6 +535,11 @@ int lbsim_step_ex(lbsim_t* h, const void* action, int action_dtype,
   DeviceGuard g(h->device);
   const hipStream_t s = (hipStream_t)stream;
   const ObsOutputs o = obs_outputs(out, false);
+  if (use_step_wave(h)) {
+    ProfScope ps(h, s, 4);
+    launch_step_wave(ctx(h), action, action_dtype, out->assign_count, o, s);
+    return launch_check(h, "step_wave_kernel");
+  }
   if (use_fused_step(h)) {
     ProfScope ps(h, s, 4);
     const LaunchCtx L = ctx(h);

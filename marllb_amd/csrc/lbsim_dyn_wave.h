@@ -474,16 +474,15 @@ __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParam
   E.clock += 1u;
 }
 
-// One dynamics launch for env b (one wave): state in, the step (or reset + warm-up), state out.
+// One dynamics launch's work for env b by one wave: state in, the step (or reset + warm-up),
+// state out.  Returns false (having done nothing) for an env outside the batch or the reset mask.
 template <int NG, int MODE, int POLICY, bool TRACE>
-__global__ void __launch_bounds__(64)
-    dynamics_wave_kernel(DevState st, SimParams p, const void* action, int action_dtype,
-                         int32_t* assign_out, const uint8_t* reset_mask) {
-  __shared__ WaveLds Ld;
-  const uint32_t b = blockIdx.x;
-  if (b >= (uint32_t)p.B) return;
-  if (MODE == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
-  const int lane = (int)threadIdx.x;
+__device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams& p,
+                                             const void* action, int action_dtype,
+                                             int32_t* assign_out, const uint8_t* reset_mask,
+                                             uint32_t b, int lane, WaveLds& Ld) {
+  if (b >= (uint32_t)p.B) return false;
+  if (MODE == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return false;
   const int S = p.S, Q = p.Q;
   const int rpos = lane & 31;
   uint3* const res_b = st.res + (size_t)b * (size_t)S * K;
@@ -626,6 +625,16 @@ __global__ void __launch_bounds__(64)
     st.next_u2[b] = E.u2;
     st.next_u3[b] = E.u3;
   }
+  return true;
+}
+
+template <int NG, int MODE, int POLICY, bool TRACE>
+__global__ void __launch_bounds__(64)
+    dynamics_wave_kernel(DevState st, SimParams p, const void* action, int action_dtype,
+                         int32_t* assign_out, const uint8_t* reset_mask) {
+  __shared__ WaveLds Ld;
+  dyn_wave_env<NG, MODE, POLICY, TRACE>(st, p, action, action_dtype, assign_out, reset_mask,
+                                        blockIdx.x, (int)threadIdx.x, Ld);
 }
 
 }  // namespace lbk

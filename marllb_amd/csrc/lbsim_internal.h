@@ -90,6 +90,11 @@ struct QmixArgs;
 bool launch_fused_step(const LaunchCtx& L, int group_lanes, const void* action, int dtype,
                        int32_t* assign, const ObsOutputs& o, hipStream_t s);
 
+// The one-launch small-batch step (lbsim_step.hip): dynamics_wave then observe per env; only for
+// a handle with dyn_wave_ok.
+void launch_step_wave(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
+                      const ObsOutputs& o, hipStream_t s);
+
 // the fused policy kernels (lbsim_pol.hip): LBSIM_OK / LBSIM_EDEVICE / LBSIM_ENOTSUP
 int launch_sac_actor(SacActorArgs& a, int64_t B, int mt, size_t lds, hipStream_t s);
 int launch_qmix_policy(QmixArgs& a, int64_t B, int form, int mt, size_t lds, hipStream_t s);

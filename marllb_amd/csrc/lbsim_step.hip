@@ -1,5 +1,6 @@
-// lbsim_step.hip — the fused step: one launch per step runs a wave's dynamics and then observes the
-// same envs ("fused step").
+// lbsim_step.hip — the fused steps: one launch per step runs a wave's dynamics and then observes
+// the same envs ("fused step").  step_wave_kernel (one wave per env, the default
+// for small S <= 4 batches) is below; fused_step_kernel (server-per-lane groups, opt-in):
 //
 // fused_step_kernel<G, MAXS, POLICY, TRACE>: one 64-lane workgroup = the 64 / G envs of one
 // dynamics wave (dyn_group_wave, lbsim_dyn_group.h).  Phase 1 steps them; a workgroup barrier makes
@@ -14,6 +15,7 @@
 // Same routines in the same order per env, so the same bits as the two-launch step (tested).
 #include "lbsim_internal.h"
 #include "lbsim_dyn_group.h"
+#include "lbsim_dyn_wave.h"
 
 namespace lbk {
 namespace {
@@ -37,6 +39,68 @@ __global__ void __launch_bounds__(64)
     const size_t b = (size_t)blockIdx.x * EPW + (size_t)i;
     if (b >= (size_t)p.B) break;
     observe_env_wave<MAXS>(st, p, out, b, L.obs, s_obs, s_act, lane);
+  }
+}
+
+// The small-batch step (dyn_wave_ok: S <= 4, at most 4 envs per SIMD): one wave per env steps it
+// (dyn_wave_env) and then observes it (observe_env_wave: S <= 4 is one chunk, one wave), so the
+// step is ONE launch and each env's observation runs as soon as its own event loop ends, while
+// slower envs still simulate.  Same routines, same order: the same bits as the two launches.
+// The two phases as separate (not inlined) functions: each gets the register file to itself
+// (inlined, the allocator kept both phases' registers live together and spilled at 128 VGPRs).
+template <int NG, int POLICY, bool TRACE>
+__device__ __attribute__((noinline)) bool step_wave_dyn(const DevState& st, const SimParams& p,
+                                                        const void* action, int action_dtype,
+                                                        int32_t* assign_out, uint32_t b,
+                                                        int lane, WaveLds& Ld) {
+  return dyn_wave_env<NG, kModeStep, POLICY, TRACE>(st, p, action, action_dtype, assign_out,
+                                                    nullptr, b, lane, Ld);
+}
+__device__ __attribute__((noinline)) void step_wave_obs(const DevState& st, const SimParams& p,
+                                                        const ObsOutputs& out, size_t b,
+                                                        ObsScratch& sc, float* s_obs,
+                                                        float* s_act, int lane) {
+  observe_env_wave<kObsChunk>(st, p, out, b, sc, s_obs, s_act, lane);
+}
+
+template <int NG, int POLICY, bool TRACE>
+__global__ void __launch_bounds__(64, 4)
+    step_wave_kernel(DevState st, SimParams p, const void* action, int action_dtype,
+                     int32_t* assign_out, ObsOutputs out) {
+  __shared__ union {
+    WaveLds dyn;
+    ObsScratch obs;
+  } L;
+  __shared__ float s_obs[kObsChunk * NF];
+  __shared__ float s_act[kObsChunk];
+  const int lane = (int)threadIdx.x;
+  if (!step_wave_dyn<NG, POLICY, TRACE>(st, p, action, action_dtype, assign_out, blockIdx.x, lane,
+                                        L.dyn))
+    return;
+  __syncthreads();  // state stores complete and visible to this workgroup; LDS reused below
+  step_wave_obs(st, p, out, blockIdx.x, L.obs, s_obs, s_act, lane);
+}
+
+template <int NG, int POLICY>
+void launch_w(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
+              const ObsOutputs& o, hipStream_t s) {
+  const dim3 block(64), grid((unsigned)L.B);
+  if (L.prm.trace)
+    hipLaunchKernelGGL((step_wave_kernel<NG, POLICY, true>), grid, block, 0, s, L.st, L.prm,
+                       action, dtype, assign, o);
+  else
+    hipLaunchKernelGGL((step_wave_kernel<NG, POLICY, false>), grid, block, 0, s, L.st, L.prm,
+                       action, dtype, assign, o);
+}
+
+template <int NG>
+void launch_wpol(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
+                 const ObsOutputs& o, hipStream_t s) {
+  switch (L.prm.policy) {
+    case LBSIM_POLICY_SED: launch_w<NG, 0>(L, action, dtype, assign, o, s); break;
+    case LBSIM_POLICY_SED2: launch_w<NG, 1>(L, action, dtype, assign, o, s); break;
+    case LBSIM_POLICY_LSQ: launch_w<NG, 2>(L, action, dtype, assign, o, s); break;
+    default: launch_w<NG, 3>(L, action, dtype, assign, o, s); break;
   }
 }
 
@@ -66,6 +130,12 @@ void launch_pol(const LaunchCtx& L, const void* action, int dtype, int32_t* assi
 }
 
 }  // namespace
+
+void launch_step_wave(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
+                      const ObsOutputs& o, hipStream_t s) {
+  if (L.S <= 2) launch_wpol<1>(L, action, dtype, assign, o, s);
+  else launch_wpol<2>(L, action, dtype, assign, o, s);
+}
 
 bool launch_fused_step(const LaunchCtx& L, int group_lanes, const void* action, int dtype,
                        int32_t* assign, const ObsOutputs& o, hipStream_t s) {

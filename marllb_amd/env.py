@@ -47,11 +47,9 @@ def action_to_weights(action, action_type: str, discrete_weights, min_weight: fl
 
 def array_to_dict(obs: np.ndarray, sequence_id: int = 0) -> dict:
     """env.py:391-423: active = any(obs[s] > 0); per-server dict of the 11 named features."""
-    stats, active = {}, []
-    for sid in range(obs.shape[0]):
-        if np.any(obs[sid] > 0):
-            active.append(sid)
-            stats[sid] = {name: float(obs[sid, i]) for i, name in enumerate(FEATURE_NAMES)}
+    active = np.flatnonzero((obs > 0).any(axis=1)).tolist()
+    rows = obs.tolist()  # the float32 values as Python floats (= float(obs[sid, i]))
+    stats = {sid: dict(zip(FEATURE_NAMES, rows[sid])) for sid in active}
     return {"active_servers": active, "server_stats": stats, "sequence_id": sequence_id}
 
 
@@ -562,18 +560,25 @@ class LoadBalanceEnv:
             self.num_servers, self.action_type, self.discrete_weights, self.min_weight,
             self.max_weight, self.use_ground_truth)
 
-    # ---- single-env I/O: one device buffer [obs | raw | reward], one copy to pinned host memory
+    # ---- single-env I/O, zero-copy: the step kernels read the action from and write [obs | raw |
+    # reward] and done into pinned host memory (device-accessible, same pointers), so a step is
+    # the launches and one stream synchronisation -- no copy enqueues, no per-step allocations
     def _io_buffers(self):
         if self._io is None:
             torch = _torch()
             n = self.num_servers * NF
-            dev = torch.empty(2 * n + 2, dtype=torch.float32, device=self._vec.device)
-            host = torch.empty(2 * n + 2, dtype=torch.float32, pin_memory=True)
+            host = torch.zeros(2 * n + 2, dtype=torch.float32, pin_memory=True)
             act_dt = torch.int64 if self.action_type == "discrete" else torch.float32
-            act_h = torch.empty(self.num_servers, dtype=act_dt, pin_memory=True)
-            act_d = torch.empty(self.num_servers, dtype=act_dt, device=self._vec.device)
-            done = torch.empty(1, dtype=torch.uint8, device=self._vec.device)
-            self._io = (dev, host, act_h, act_d, done, n)
+            act_h = torch.zeros(self.num_servers, dtype=act_dt, pin_memory=True)
+            done_h = torch.zeros(8, dtype=torch.uint8, pin_memory=True)
+            out = _lib.StepOutputs()
+            base = host.data_ptr()
+            out.obs, out.raw_obs, out.reward = base, base + 4 * n, base + 8 * n
+            out.done = done_h.data_ptr()
+            stream = torch.cuda.current_stream(self._vec.device)
+            dt = _lib.DTYPE_I64 if self.action_type == "discrete" else _lib.DTYPE_F32
+            self._io = (host, host.numpy(), act_h, act_h.numpy(), done_h, out, stream,
+                        ctypes.c_void_p(stream.cuda_stream), dt, n)
         return self._io
 
     def _sim_reset(self) -> np.ndarray:
@@ -585,32 +590,22 @@ class LoadBalanceEnv:
         return obs
 
     def _sim_step(self, idx_or_w: np.ndarray):
-        """One simulator step -> (obs, raw obs, reward) with a single device->host transfer."""
-        torch = _torch()
+        """One simulator step -> (obs, raw obs, reward), zero-copy through pinned host memory."""
         v = self._vec
         if not v._reset_done:  # e.g. SHM mode whose reset came from a frame
             v.reset()
-        dev, host, act_h, act_d, done, n = self._io_buffers()
-        act_h.numpy()[:] = idx_or_w
-        act_d.copy_(act_h, non_blocking=True)
-        out = _lib.StepOutputs()
-        base = dev.data_ptr()
-        out.obs, out.raw_obs, out.reward = base, base + 4 * n, base + 8 * n
-        out.done = done.data_ptr()
-        dt = _lib.DTYPE_I64 if self.action_type == "discrete" else _lib.DTYPE_F32
-        stream = v._stream()
-        v.handle.check(v.handle.lib.lbsim_step_ex(v.handle.h, act_d.data_ptr(), dt,
-                                                  ctypes.byref(out), stream))
+        host, hview, act_h, aview, done_h, out, stream, sptr, dt, n = self._io_buffers()
+        aview[:] = idx_or_w
+        v.handle.check(v.handle.lib.lbsim_step_ex(v.handle.h, act_h.data_ptr(), dt,
+                                                  ctypes.byref(out), sptr))
         v._step_bound += 1
-        host.copy_(dev, non_blocking=True)
-        torch.cuda.current_stream(v.device).synchronize()
-        h = host.numpy()
+        stream.synchronize()
         S = self.num_servers
-        obs = h[:n].reshape(S, NF).copy()
-        raw = h[n:2 * n].reshape(S, NF).copy()
+        obs = hview[:n].reshape(S, NF).copy()
+        raw = hview[n:2 * n].reshape(S, NF).copy()
         if self._host_norm:
             obs = self._normalize_host(raw)
-        return obs, raw, float(h[2 * n])
+        return obs, raw, float(hview[2 * n])
 
     # ---- gym API
     def reset(self) -> np.ndarray:
@@ -707,11 +702,9 @@ class LoadBalanceEnv:
             reward = self._plumb.reward(obs_dict)
             next_obs = self._plumb.normalize(raw) if self.normalize_obs else raw
         else:
-            a = np.asarray(action)
-            if self.action_type == "discrete":
-                act = np.array([int(x) for x in a.reshape(-1)], dtype=np.int64)
-            else:
-                act = np.asarray(a, dtype=np.float32).reshape(-1)
+            a = np.asarray(action).reshape(-1)
+            # int(x) truncation = astype (indices past the weights already raised above)
+            act = a.astype(np.int64) if self.action_type == "discrete" else a.astype(np.float32)
             shm_res = self._shm_step(weights) if (self.use_shm and self.shm is not None) else None
             if shm_res is not None:
                 next_obs, raw, reward, _ = shm_res

@@ -317,12 +317,14 @@ def test_wider_groups_bit_exact(lanes):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
 
 
-def test_wave_kernel_bit_exact():
+@pytest.mark.parametrize("step", ["auto", "fused"])
+def test_wave_kernel_bit_exact(step):
     """LBSIM_DYN_WAVE=1 runs the one-wave-per-env dynamics (lbsim_dyn_wave.h) on every simulator
     case it applies to (S <= 4, queue capacity <= 32, every policy but ALIAS) at any batch size,
-    the 8256-env case included, both as two launches and under the fused step (whose reset
-    launch is then the wave kernel): bit-exact vs the oracle.  The setting is read once per
-    process, so the cases run in a child process."""
+    the 8256-env case included: bit-exact vs the oracle.  step = auto: a dynamics_wave_kernel
+    launch then an observe launch; fused (LBSIM_STEP_KERNEL=fused, opt-in): one step_wave_kernel
+    launch (dynamics then observe per wave).  Resets use dynamics_wave_kernel in both.  The
+    settings are read once per process, so the cases run in a child process."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -334,7 +336,8 @@ def test_wave_kernel_bit_exact():
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p",
                         "no:cacheprovider"] +
                        [os.path.join(root, "tests", "test_gpu_parity.py") + "::" + k for k in ks],
-                       cwd=root, env={**os.environ, "LBSIM_DYN_WAVE": "1"},
+                       cwd=root, env={**os.environ, "LBSIM_DYN_WAVE": "1",
+                                      **({"LBSIM_STEP_KERNEL": "fused"} if step == "fused" else {})},
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
 

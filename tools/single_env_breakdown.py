@@ -46,28 +46,35 @@ def main():
     env.reset()
     out["facade_step"] = per_step(lambda i: env.step(acts[i % 256]))
     v = env._vec
-    dev, host, act_h, act_d, done, n = env._io_buffers()
-    so = _lib.StepOutputs()
-    base = dev.data_ptr()
-    so.obs, so.raw_obs, so.reward = base, base + 4 * n, base + 8 * n
-    so.done = done.data_ptr()
-    stream = v._stream()
+    host, hview, act_h, aview, done_h, so, cur, sptr, dt, n = env._io_buffers()
     lib, h = v.handle.lib, v.handle.h
-    cur = torch.cuda.current_stream(v.device)
+    act_d = torch.zeros(S, dtype=torch.int64, device=v.device)
+    dev = torch.zeros(2 * n + 2, dtype=torch.float32, device=v.device)
+    sd = _lib.StepOutputs()  # device-resident outputs
+    base = dev.data_ptr()
+    sd.obs, sd.raw_obs, sd.reward = base, base + 4 * n, base + 8 * n
+    done_d = torch.zeros(8, dtype=torch.uint8, device=v.device)
+    sd.done = done_d.data_ptr()
+    stream = sptr
 
-    def bare(i):
-        lib.lbsim_step_ex(h, act_d.data_ptr(), _lib.DTYPE_I64, ctypes.byref(so), stream)
+    def bare(i):  # device-resident action and outputs
+        lib.lbsim_step_ex(h, act_d.data_ptr(), _lib.DTYPE_I64, ctypes.byref(sd), stream)
         cur.synchronize()
     out["step_ex_sync"] = per_step(bare)
 
     def bare_copy(i):
-        lib.lbsim_step_ex(h, act_d.data_ptr(), _lib.DTYPE_I64, ctypes.byref(so), stream)
+        lib.lbsim_step_ex(h, act_d.data_ptr(), _lib.DTYPE_I64, ctypes.byref(sd), stream)
         host.copy_(dev, non_blocking=True)
         cur.synchronize()
     out["step_ex_copy_sync"] = per_step(bare_copy)
 
+    def zero_copy(i):  # the facade's form: pinned host action and outputs
+        lib.lbsim_step_ex(h, act_h.data_ptr(), _lib.DTYPE_I64, ctypes.byref(so), stream)
+        cur.synchronize()
+    out["step_ex_zero_copy_sync"] = per_step(zero_copy)
+
     def launches_only(i):
-        lib.lbsim_step_ex(h, act_d.data_ptr(), _lib.DTYPE_I64, ctypes.byref(so), stream)
+        lib.lbsim_step_ex(h, act_d.data_ptr(), _lib.DTYPE_I64, ctypes.byref(sd), stream)
     out["step_ex_enqueue_only"] = per_step(launches_only)
 
     x = torch.zeros(1, device=v.device)
@@ -80,7 +87,7 @@ def main():
     # per-kernel HIP-event times of the bare step
     v.handle.check(lib.lbsim_profile_begin(h, 4 * 500 + 8))
     for i in range(500):
-        lib.lbsim_step_ex(h, act_d.data_ptr(), _lib.DTYPE_I64, ctypes.byref(so), stream)
+        lib.lbsim_step_ex(h, act_d.data_ptr(), _lib.DTYPE_I64, ctypes.byref(sd), stream)
     ms = (ctypes.c_double * 4)()
     cnt = (ctypes.c_int64 * 4)()
     v.handle.check(lib.lbsim_profile_end_ex(h, ms, cnt, 4))
