@@ -83,8 +83,9 @@ struct WaveBatch {
 
 constexpr int kWaveKeyStride = 34;  // key table entries per server: n = 0 .. Q + 1 (Q <= 32)
 struct WaveLds {
+  int32_t kt[4 * kWaveKeyStride];  // FAST single-choice keys of this step [server][n] (first: its
+                                   // address needs no constant, ds_read2 offsets are 8-bit)
   int2 img[32 * 4];       // ring image [pos][server] for the carried-in walk and `last`
-  int32_t kt[4 * kWaveKeyStride];  // FAST single-choice keys of this step [server][n]
   uint32_t own[4 * 128];  // insert owner of each (server, slot) in a flush: seq << 6 | lane
   uint32_t chg[4 * 4];    // written-slot masks [word][server]
 };
@@ -151,12 +152,14 @@ __device__ __forceinline__ int32_t wave_count(const uint64_t (&live)[NG], int la
 
 // The reservoir inserts of batch lanes [0, nproc): flows that completed in this step, per server in
 // arrival order (reservoir.py:64-85 with the arrival's draw word, reservoir_slot_r32).
-__device__ __forceinline__ void wave_flush(const SimParams& p, WaveSrv& V, const WaveBatch& Bt,
-                                           int nproc, int lane, uint3* const res_b, WaveLds& Ld,
-                                           uint32_t seq, uint32_t base_ms, uint32_t base_rem) {
+__device__ __forceinline__ void wave_flush(const SimParams& p, WaveSrv& V, WaveEnv& E,
+                                           const WaveBatch& Bt, int nproc, int lane,
+                                           uint3* const res_b, WaveLds& Ld, uint32_t seq,
+                                           uint32_t base_ms, uint32_t base_rem) {
   const int S = p.S;
   const int32_t dt = p.dt_us;
   const bool valid = lane < nproc && Bt.lc >= 0;
+  E.dropped += (uint32_t)__builtin_popcountll(__ballot(lane < nproc && Bt.lc < 0));  // all full
   const bool ins = valid && Bt.ltc <= dt;
   uint32_t pre = 0u, rcb = 0u;
   float scale = p.svc_scale[0];
@@ -255,18 +258,18 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
   int32_t ta = E.next_arr;
 
   // server lane s's flows queued at time t: the popcounts of the four ring-lane halves (scalar),
-  // packed as 16-bit fields and unpacked by one shift per lane
-  const uint32_t cnt_sh = (uint32_t)(lane & 3) * 16u;
+  // packed as bytes of one SGPR (counts <= 32) and unpacked by one v_bfe per lane
+  const uint32_t cnt_sh = (uint32_t)(lane & 3) * 8u;
   auto count_at = [&](int32_t t) -> int32_t {
     const uint64_t m0 = __ballot(R.tc[0] > t);
-    uint64_t packed = (uint64_t)__builtin_popcount((uint32_t)m0) |
-                      ((uint64_t)__builtin_popcount((uint32_t)(m0 >> 32)) << 16);
+    uint32_t packed = (uint32_t)__builtin_popcount((uint32_t)m0) +
+                      ((uint32_t)__builtin_popcount((uint32_t)(m0 >> 32)) << 8);
     if constexpr (NG > 1) {
       const uint64_t m1 = __ballot(R.tc[NG - 1] > t);
-      packed |= ((uint64_t)__builtin_popcount((uint32_t)m1) << 32) |
-                ((uint64_t)__builtin_popcount((uint32_t)(m1 >> 32)) << 48);
+      packed += ((uint32_t)__builtin_popcount((uint32_t)m1) << 16) +
+                ((uint32_t)__builtin_popcount((uint32_t)(m1 >> 32)) << 24);
     }
-    return (int32_t)((uint32_t)(packed >> cnt_sh) & 0xFFFFu);
+    return (int32_t)__builtin_amdgcn_ubfe(packed, cnt_sh, 8u);
   };
   const uint32_t smask = (1u << S) - 1u;  // server lanes
   // push lane of server lane s: ring register (s >> 1) x 64 + lane 32 (s & 1) + write position
@@ -305,11 +308,12 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
       int c = -1;
       if constexpr (TAB) {
         // finite scores: the eligible minimum, h among equal minima, else the lowest such server
+        // (every server full: no eligible tie, and the find-first-set of 0 is -1: dropped)
         const int32_t mk = __builtin_amdgcn_readfirstlane(group_min_i32<4>(key));
-        const int h = (int)__umulhi(u2, (uint32_t)S);
-        const uint32_t tie = (uint32_t)__ballot(key == mk) & smask;
-        c = ((tie >> h) & 1u) ? h : __builtin_ctz(tie);
-        c = mk == 0x7FFFFFFF ? -1 : c;
+        const uint32_t hbit = 1u << (int)__umulhi(u2, (uint32_t)S);
+        const uint32_t tie = (uint32_t)__ballot(key == mk) & (mk != 0x7FFFFFFF ? smask : 0u);
+        const uint32_t sel = (tie & hbit) ? hbit : tie;
+        c = sel ? __builtin_ctz(sel) : -1;
       } else if constexpr (two_choice) {
         const uint32_t em = (uint32_t)__ballot(n < Q) & smask;
         const int h1 = two_choice_h1(u2, S);
@@ -354,7 +358,6 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
       V.tail = me ? tc : V.tail;
       const int32_t pl1 = pl + 1 == pl_wrap ? lane * 32 : pl + 1;
       pl = me ? pl1 : pl;
-      E.dropped += c < 0 ? 1u : 0u;
       Bt.lc = lg ? c : Bt.lc;
       Bt.ltc = lg ? tc : Bt.ltc;
       // ---- the next arrival: the pushed flow is still queued at ta_n if tc > ta_n
@@ -363,7 +366,7 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
       key = adj ? k1 : k0;
       score = adj ? sc1 : sc0;
     }
-    wave_flush(p, V, Bt, bi, lane, res_b, Ld, seq++, base_ms, base_rem);
+    wave_flush(p, V, E, Bt, bi, lane, res_b, Ld, seq++, base_ms, base_rem);
     ta = rdl(Bt.ta, bi);
     if (ta >= dt) break;
     base += 63u;

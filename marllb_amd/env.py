@@ -578,7 +578,8 @@ class LoadBalanceEnv:
             stream = torch.cuda.current_stream(self._vec.device)
             dt = _lib.DTYPE_I64 if self.action_type == "discrete" else _lib.DTYPE_F32
             self._io = (host, host.numpy(), act_h, act_h.numpy(), done_h, out, stream,
-                        ctypes.c_void_p(stream.cuda_stream), dt, n)
+                        ctypes.c_void_p(stream.cuda_stream), dt, n,
+                        ctypes.c_void_p(act_h.data_ptr()), ctypes.byref(out))
         return self._io
 
     def _sim_reset(self) -> np.ndarray:
@@ -594,10 +595,13 @@ class LoadBalanceEnv:
         v = self._vec
         if not v._reset_done:  # e.g. SHM mode whose reset came from a frame
             v.reset()
-        host, hview, act_h, aview, done_h, out, stream, sptr, dt, n = self._io_buffers()
+        io = self._io if self._io is not None else self._io_buffers()
+        hview, aview, stream, sptr, dt, n, aptr, outref = (io[1], io[3], io[6], io[7], io[8],
+                                                           io[9], io[10], io[11])
         aview[:] = idx_or_w
-        v.handle.check(v.handle.lib.lbsim_step_ex(v.handle.h, act_h.data_ptr(), dt,
-                                                  ctypes.byref(out), sptr))
+        rc = v.handle.lib.lbsim_step_ex(v.handle.h, aptr, dt, outref, sptr)
+        if rc != _lib.OK:
+            v.handle.check(rc)
         v._step_bound += 1
         stream.synchronize()
         S = self.num_servers

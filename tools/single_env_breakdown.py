@@ -46,7 +46,7 @@ def main():
     env.reset()
     out["facade_step"] = per_step(lambda i: env.step(acts[i % 256]))
     v = env._vec
-    host, hview, act_h, aview, done_h, so, cur, sptr, dt, n = env._io_buffers()
+    host, hview, act_h, aview, done_h, so, cur, sptr, dt, n = env._io_buffers()[:10]
     lib, h = v.handle.lib, v.handle.h
     act_d = torch.zeros(S, dtype=torch.int64, device=v.device)
     dev = torch.zeros(2 * n + 2, dtype=torch.float32, device=v.device)
