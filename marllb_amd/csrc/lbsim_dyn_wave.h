@@ -283,8 +283,9 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
   for (;;) {      // batches
     // arrivals bi .. lim - 1 of this batch come before dt (times increase with the lane); lane 63
     // opens the next batch
+    // (lim > bi: the batch starts at an arrival before dt)
     const int lim = __builtin_ctzll(__ballot(Bt.ta >= dt) | (1ull << 63));
-    for (; bi < lim; ++bi) {
+    do {
       const int32_t ta = rdl(Bt.ta, bi);
       const float work = rdl(Bt.wk, bi);
       const uint32_t u2 = rdl(Bt.u2, bi);
@@ -365,7 +366,7 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
       n = adj ? n_n + 1 : n_n;
       key = adj ? k1 : k0;
       score = adj ? sc1 : sc0;
-    }
+    } while (++bi < lim);
     wave_flush(p, V, E, Bt, bi, lane, res_b, Ld, seq++, base_ms, base_rem);
     ta = rdl(Bt.ta, bi);
     if (ta >= dt) break;

@@ -25,4 +25,5 @@ for a in "--batch 4096" "--trace poisson_for_loop_rate_500 --servers 8" "--workl
 done
 timeout -k 10 300 python bench.py --no-cpu-baseline --no-graph --async-groups 2 --late-episode 1000,5000 > $O/async_late.json 2>> $O/workloads.err || exit 15
 timeout -k 10 300 python tools/single_env_latency.py --steps 2000 > $O/single_env_latency.json 2>> $O/workloads.err || exit 16
+timeout -k 10 300 python tools/single_env_breakdown.py --steps 2000 > $O/single_env_breakdown.json 2>> $O/workloads.err || exit 18
 bash tools/gpu_sweep.sh $TAG --no-graph || exit 17
