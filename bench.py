@@ -541,12 +541,14 @@ def main():
         # lbsim_profile times each class
         dyn = ("dynamics_kernel", "dynamics_group_kernel",
                "dynamics_wave_kernel")[lib.lbsim_dynamics_kernel(handle.h)]
-        names = {0: dyn, 1: "observe_kernel", 4: "fused_step_kernel"}
+        fused = "step_wave_kernel" if dyn == "dynamics_wave_kernel" else "fused_step_kernel"
+        names = {0: dyn, 1: "observe_kernel", 4: fused}
         avg = {names[i]: ms[i] / cnt[i] for i in names if cnt[i] > 0}
         rate = tr.rate if tr is not None else ARRIVAL_RATE
         slots, inflight = step_accounting(handle, lib, one_step, args.steps, replay)
         abytes = algorithmic_bytes(S, slots / B, inflight / B)
         abytes[dyn] = abytes.pop("dynamics_kernel")
+        abytes[fused] = abytes.pop("fused_step_kernel")
         per_kernel = {}
         for k in avg:
             ab_k = abytes[k] * B

@@ -305,12 +305,20 @@ int step_kernel_of(const lbsim_t* h) {
   return h->cfg.step_kernel != LBSIM_STEP_AUTO ? h->cfg.step_kernel : env;
 }
 
-// The one-launch wave step (step_wave_kernel): one wave per env and FUSED asked for.  AUTO is the
-// two launches here too: the one-launch form measured slower (4096 x 4: 0.141 ms against 0.066 +
-// 0.019 ms, profiles/r03w/ab_step_wave_fused.txt -- the observe phase needs ~190 VGPRs inlined,
-// and out of line its call frames go through scratch).
+// The one-launch wave step (step_wave_kernel, 2 waves per SIMD): one wave per env, FUSED asked
+// for, or AUTO on batches of at most 2 envs per SIMD (LBSIM_STEP_WAVE_MAX_B overrides), where one
+// launch instead of two pays (profiles/r03w/ab_step_wave_fused.txt); larger AUTO batches take the
+// two launches (their 4 waves per SIMD need the 128-VGPR kernels).
 bool use_step_wave(const lbsim_t* h) {
-  return step_kernel_of(h) == LBSIM_STEP_FUSED && dyn_wave_ok(ctx(h));
+  static const int64_t max_b = [] {
+    const char* e = std::getenv("LBSIM_STEP_WAVE_MAX_B");
+    return e ? (int64_t)std::atoll(e) : (int64_t)-1;
+  }();
+  const LaunchCtx L = ctx(h);
+  if (!dyn_wave_ok(L)) return false;
+  const int k = step_kernel_of(h);
+  if (k == LBSIM_STEP_FUSED) return true;
+  return k == LBSIM_STEP_AUTO && (int64_t)L.B <= (max_b >= 0 ? max_b : 2 * (int64_t)L.simds);
 }
 
 // The fused step for this handle: its config (LBSIM_STEP_KERNEL=split|fused overrides AUTO) and

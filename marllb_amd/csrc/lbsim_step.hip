@@ -46,25 +46,11 @@ __global__ void __launch_bounds__(64)
 // (dyn_wave_env) and then observes it (observe_env_wave: S <= 4 is one chunk, one wave), so the
 // step is ONE launch and each env's observation runs as soon as its own event loop ends, while
 // slower envs still simulate.  Same routines, same order: the same bits as the two launches.
-// The two phases as separate (not inlined) functions: each gets the register file to itself
-// (inlined, the allocator kept both phases' registers live together and spilled at 128 VGPRs).
+// 2 waves per SIMD: the observe phase inlined after the event loop needs ~190 VGPRs (capped at
+// 128 it spilled 64; out of line its call frames went through 1 KB of scratch per lane and the
+// kernel ran 0.141 ms at 4096 x 4).  So it serves batches of at most 2 envs per SIMD (use_step_wave).
 template <int NG, int POLICY, bool TRACE>
-__device__ __attribute__((noinline)) bool step_wave_dyn(const DevState& st, const SimParams& p,
-                                                        const void* action, int action_dtype,
-                                                        int32_t* assign_out, uint32_t b,
-                                                        int lane, WaveLds& Ld) {
-  return dyn_wave_env<NG, kModeStep, POLICY, TRACE>(st, p, action, action_dtype, assign_out,
-                                                    nullptr, b, lane, Ld);
-}
-__device__ __attribute__((noinline)) void step_wave_obs(const DevState& st, const SimParams& p,
-                                                        const ObsOutputs& out, size_t b,
-                                                        ObsScratch& sc, float* s_obs,
-                                                        float* s_act, int lane) {
-  observe_env_wave<kObsChunk>(st, p, out, b, sc, s_obs, s_act, lane);
-}
-
-template <int NG, int POLICY, bool TRACE>
-__global__ void __launch_bounds__(64, 4)
+__global__ void __launch_bounds__(64, 2)
     step_wave_kernel(DevState st, SimParams p, const void* action, int action_dtype,
                      int32_t* assign_out, ObsOutputs out) {
   __shared__ union {
@@ -74,11 +60,11 @@ __global__ void __launch_bounds__(64, 4)
   __shared__ float s_obs[kObsChunk * NF];
   __shared__ float s_act[kObsChunk];
   const int lane = (int)threadIdx.x;
-  if (!step_wave_dyn<NG, POLICY, TRACE>(st, p, action, action_dtype, assign_out, blockIdx.x, lane,
-                                        L.dyn))
+  if (!dyn_wave_env<NG, kModeStep, POLICY, TRACE>(st, p, action, action_dtype, assign_out, nullptr,
+                                                  blockIdx.x, lane, L.dyn))
     return;
   __syncthreads();  // state stores complete and visible to this workgroup; LDS reused below
-  step_wave_obs(st, p, out, blockIdx.x, L.obs, s_obs, s_act, lane);
+  observe_env_wave<kObsChunk>(st, p, out, blockIdx.x, L.obs, s_obs, s_act, lane);
 }
 
 template <int NG, int POLICY>
