@@ -714,18 +714,21 @@ class LoadBalanceEnv:
                 next_obs, raw, reward, _ = shm_res
             else:
                 next_obs, raw, reward = self._sim_step(act)
-            obs_dict = self._array_to_dict(raw)
+            obs_dict = None  # the per-server dict (env.py:391-423) is built when render asks
         self._last_raw = raw
         # the reference sets last_observation only in SHM mode (env.py:201,249); problem-05's
         # get_state() relies on it staying None in simulation (multi_agent_env.py:249-254)
         self._last_obs_dict = obs_dict
+        self._last_obs_step = self.current_step
         self.episode_rewards.append(reward)
         self.episode_return += reward
         done = self.current_step >= self.max_steps
+        active = (obs_dict["active_servers"] if obs_dict is not None
+                  else np.flatnonzero((raw > 0).any(axis=1)).tolist())  # env.py:410-413
         info = {
             "step": self.current_step,
             "weights": weights.tolist(),
-            "active_servers": obs_dict.get("active_servers", list(range(self.num_servers))),
+            "active_servers": active,
             "episode_return": self.episode_return,
         }
         if done:
@@ -738,6 +741,8 @@ class LoadBalanceEnv:
             print(f"Step: {self.current_step}/{self.max_steps}")
             print(f"Episode Return: {self.episode_return:.4f}")
             obs_dict = self.last_observation or getattr(self, "_last_obs_dict", None)
+            if obs_dict is None and getattr(self, "_last_raw", None) is not None:
+                obs_dict = array_to_dict(self._last_raw, getattr(self, "_last_obs_step", 0))
             if obs_dict:
                 active = obs_dict.get("active_servers", [])
                 stats = obs_dict.get("server_stats", {})
