@@ -204,7 +204,7 @@ __device__ __forceinline__ void wave_flush(const SimParams& p, WaveSrv& V, WaveE
 // iteration fetches the keys for both outcomes of its push (n and n + 1 at the next arrival) in
 // one ds_read2 before it chooses, and the choice -> choice chain is a select, a DPP minimum and
 // a ballot.  SED2 / LSQ2 and non-finite SED compute their scores in the loop.
-template <int NG, int POLICY, bool TRACE, bool FAST>
+template <int NG, int POLICY, bool TRACE, bool FAST, bool VC>
 __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimParams& p,
                                                 WaveEnv& E, WaveSrv& V, WaveRing<NG>& R,
                                                 int lane, uint3* const res_b, WaveLds& Ld,
@@ -257,19 +257,33 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
   int bi = 0;  // batch lane of the current arrival
   int32_t ta = E.next_arr;
 
-  // server lane s's flows queued at time t: the popcounts of the four ring-lane halves (scalar),
-  // packed as bytes of one SGPR (counts <= 32) and unpacked by one v_bfe per lane
+  // server lane s's flows queued at time t, from one ballot per ring register.  VC (the one-launch
+  // step, <= 2 envs per SIMD): its half selected per lane and counted by VALU -- the shorter chain,
+  // a lone wave's step 2.5 us faster; else the four halves' popcounts by the scalar unit, packed as
+  // bytes of one SGPR and unpacked by one v_bfe -- fewer VALU, 2.5 % faster at 4 envs per SIMD
+  // (profiles/r03w/ab_wave_counts.txt)
+  const bool odd = (lane & 1) != 0, hi_reg = (lane & 2) != 0;
   const uint32_t cnt_sh = (uint32_t)(lane & 3) * 8u;
   auto count_at = [&](int32_t t) -> int32_t {
     const uint64_t m0 = __ballot(R.tc[0] > t);
-    uint32_t packed = (uint32_t)__builtin_popcount((uint32_t)m0) +
-                      ((uint32_t)__builtin_popcount((uint32_t)(m0 >> 32)) << 8);
-    if constexpr (NG > 1) {
-      const uint64_t m1 = __ballot(R.tc[NG - 1] > t);
-      packed += ((uint32_t)__builtin_popcount((uint32_t)m1) << 16) +
-                ((uint32_t)__builtin_popcount((uint32_t)(m1 >> 32)) << 24);
+    if constexpr (VC) {
+      uint32_t w = odd ? (uint32_t)(m0 >> 32) : (uint32_t)m0;
+      if constexpr (NG > 1) {
+        const uint64_t m1 = __ballot(R.tc[NG - 1] > t);
+        const uint32_t w1 = odd ? (uint32_t)(m1 >> 32) : (uint32_t)m1;
+        w = hi_reg ? w1 : w;
+      }
+      return (int32_t)__builtin_popcount(w);
+    } else {
+      uint32_t packed = (uint32_t)__builtin_popcount((uint32_t)m0) +
+                        ((uint32_t)__builtin_popcount((uint32_t)(m0 >> 32)) << 8);
+      if constexpr (NG > 1) {
+        const uint64_t m1 = __ballot(R.tc[NG - 1] > t);
+        packed += ((uint32_t)__builtin_popcount((uint32_t)m1) << 16) +
+                  ((uint32_t)__builtin_popcount((uint32_t)(m1 >> 32)) << 24);
+      }
+      return (int32_t)__builtin_amdgcn_ubfe(packed, cnt_sh, 8u);
     }
-    return (int32_t)__builtin_amdgcn_ubfe(packed, cnt_sh, 8u);
   };
   const uint32_t smask = (1u << S) - 1u;  // server lanes
   // push lane of server lane s: ring register (s >> 1) x 64 + lane 32 (s & 1) + write position
@@ -383,7 +397,7 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
   E.u3 = rdl(Bt.u3, bi);
 }
 
-template <int NG, int POLICY, bool TRACE>
+template <int NG, int POLICY, bool TRACE, bool VC>
 __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParams& p, WaveEnv& E,
                                               WaveSrv& V, WaveRing<NG>& R, int lane,
                                               uint3* const res_b, WaveLds& Ld, uint32_t& seq,
@@ -438,10 +452,10 @@ __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParam
   // ---- 2. the arrivals (SED / SED2 scores are finite unless some den is 0 / inf / NaN)
   const bool finite = lsq || !V.act || (fabs(V.den) >= 1e-30 && fabs(V.den) <= 1e300);
   if (__all(finite))
-    wave_event_loop<NG, POLICY, TRACE, true>(st, p, E, V, R, lane, res_b, Ld, seq, base_ms,
+    wave_event_loop<NG, POLICY, TRACE, true, VC>(st, p, E, V, R, lane, res_b, Ld, seq, base_ms,
                                              base_rem);
   else
-    wave_event_loop<NG, POLICY, TRACE, false>(st, p, E, V, R, lane, res_b, Ld, seq, base_ms,
+    wave_event_loop<NG, POLICY, TRACE, false, VC>(st, p, E, V, R, lane, res_b, Ld, seq, base_ms,
                                               base_rem);
 
   // ---- 3. completions up to dt; the server's count, head and last completion
@@ -480,7 +494,7 @@ __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParam
 
 // One dynamics launch's work for env b by one wave: state in, the step (or reset + warm-up),
 // state out.  Returns false (having done nothing) for an env outside the batch or the reset mask.
-template <int NG, int MODE, int POLICY, bool TRACE>
+template <int NG, int MODE, int POLICY, bool TRACE, bool VC = false>
 __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams& p,
                                              const void* action, int action_dtype,
                                              int32_t* assign_out, const uint8_t* reset_mask,
@@ -544,7 +558,7 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
     V.rcnt = 0u;
     wave_sync();
     for (int k = 0; k < p.warmup_steps; ++k)
-      sim_step_wave<NG, POLICY, TRACE>(st, p, E, V, R, lane, res_b, Ld, seq, 1.0f);
+      sim_step_wave<NG, POLICY, TRACE, VC>(st, p, E, V, R, lane, res_b, Ld, seq, 1.0f);
     if (lane == 0) {
       st.ep_step[b] = 0;
       st.ep_return[b] = 0.0;
@@ -597,7 +611,7 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
       V.tail = (V.act && V.cnt0 > 0) ? tl : 0;
     }
     wave_sync();
-    sim_step_wave<NG, POLICY, TRACE>(st, p, E, V, R, lane, res_b, Ld, seq, w_own);
+    sim_step_wave<NG, POLICY, TRACE, VC>(st, p, E, V, R, lane, res_b, Ld, seq, w_own);
   }
 
   // ---- state out: the queued flows, the server fields, the env words

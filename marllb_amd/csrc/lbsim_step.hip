@@ -60,8 +60,8 @@ __global__ void __launch_bounds__(64, 2)
   __shared__ float s_obs[kObsChunk * NF];
   __shared__ float s_act[kObsChunk];
   const int lane = (int)threadIdx.x;
-  if (!dyn_wave_env<NG, kModeStep, POLICY, TRACE>(st, p, action, action_dtype, assign_out, nullptr,
-                                                  blockIdx.x, lane, L.dyn))
+  if (!dyn_wave_env<NG, kModeStep, POLICY, TRACE, true>(st, p, action, action_dtype, assign_out,
+                                                        nullptr, blockIdx.x, lane, L.dyn))
     return;
   __syncthreads();  // state stores complete and visible to this workgroup; LDS reused below
   observe_env_wave<kObsChunk>(st, p, out, blockIdx.x, L.obs, s_obs, s_act, lane);
