@@ -88,11 +88,12 @@ def main():
     v.handle.check(lib.lbsim_profile_begin(h, 4 * 500 + 8))
     for i in range(500):
         lib.lbsim_step_ex(h, act_d.data_ptr(), _lib.DTYPE_I64, ctypes.byref(sd), stream)
-    ms = (ctypes.c_double * 4)()
-    cnt = (ctypes.c_int64 * 4)()
-    v.handle.check(lib.lbsim_profile_end_ex(h, ms, cnt, 4))
+    ms = (ctypes.c_double * 5)()
+    cnt = (ctypes.c_int64 * 5)()
+    v.handle.check(lib.lbsim_profile_end_ex(h, ms, cnt, 5))
     out["kernel_us"] = {name: (ms[i] / max(cnt[i], 1) * 1e3) for i, name in
-                        enumerate(("dynamics", "observe", "dynamics_reset", "observe_reset"))}
+                        enumerate(("dynamics", "observe", "dynamics_reset", "observe_reset",
+                                   "one_launch_step")) if cnt[i] > 0}
     print(json.dumps(out), flush=True)
 
 
