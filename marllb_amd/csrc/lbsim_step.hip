@@ -17,6 +17,12 @@
 #include "lbsim_dyn_group.h"
 #include "lbsim_dyn_wave.h"
 
+// Waves per SIMD step_wave_kernel is compiled for (an A/B build knob: 4 caps it at 128 VGPRs and
+// spills, measured slower, profiles/r03w/ab_step_wave_fused.txt).
+#ifndef LBSIM_STEP_WAVE_OCC
+#define LBSIM_STEP_WAVE_OCC 2
+#endif
+
 namespace lbk {
 namespace {
 
@@ -50,7 +56,7 @@ __global__ void __launch_bounds__(64)
 // 128 it spilled 64; out of line its call frames went through 1 KB of scratch per lane and the
 // kernel ran 0.141 ms at 4096 x 4).  So it serves batches of at most 2 envs per SIMD (use_step_wave).
 template <int NG, int POLICY, bool TRACE>
-__global__ void __launch_bounds__(64, 2)
+__global__ void __launch_bounds__(64, LBSIM_STEP_WAVE_OCC)
     step_wave_kernel(DevState st, SimParams p, const void* action, int action_dtype,
                      int32_t* assign_out, ObsOutputs out) {
   __shared__ union {
