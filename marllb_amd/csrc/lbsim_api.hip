@@ -315,7 +315,7 @@ bool use_step_wave(const lbsim_t* h) {
     return e ? (int64_t)std::atoll(e) : (int64_t)-1;
   }();
   const LaunchCtx L = ctx(h);
-  if (!dyn_wave_ok(L)) return false;
+  if (!dyn_wave_ok(L) || L.S > kObsChunk) return false;  // one observe chunk per wave: S <= 4
   const int k = step_kernel_of(h);
   if (k == LBSIM_STEP_FUSED) return true;
   return k == LBSIM_STEP_AUTO && (int64_t)L.B <= (max_b >= 0 ? max_b : 2 * (int64_t)L.simds);

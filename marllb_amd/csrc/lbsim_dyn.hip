@@ -113,7 +113,8 @@ void launch_dynamics_t(const LaunchCtx& L, const void* action, int dtype, int32_
                        const uint8_t* mask, hipStream_t stream) {
   if (dyn_wave_ok(L)) {
     if (L.S <= 2) launch_dyn_wave_policy<1>(L, action, dtype, assign, mask, stream);
-    else launch_dyn_wave_policy<2>(L, action, dtype, assign, mask, stream);
+    else if (L.S <= 4) launch_dyn_wave_policy<2>(L, action, dtype, assign, mask, stream);
+    else launch_dyn_wave_policy<4>(L, action, dtype, assign, mask, stream);
     return;
   }
   switch (dyn_group_lanes(L)) {

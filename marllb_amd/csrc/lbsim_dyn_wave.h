@@ -30,9 +30,9 @@
 //     happen in arrival order = FIFO completion order, after the carried-in flows, exactly as
 //     the oracle's pops make them.
 // Same event sequence, same arithmetic, same state layout as the other two
-// mappings: interchangeable between launches, bit-identical to the oracle.  S <= 4, Q <= 32 and the
-// SED / SED2 / LSQ / LSQ2 policies (ALIAS and larger shapes use the group kernel: dyn_wave_ok in
-// lbsim_internal.h).
+// mappings: interchangeable between launches, bit-identical to the oracle.  S <= 8 (NG = 1, 2, 4
+// ring registers), Q <= 32 and the SED / SED2 / LSQ / LSQ2 policies (ALIAS and larger shapes use
+// the group kernel: dyn_wave_ok in lbsim_internal.h).
 #pragma once
 
 #include "lbsim_dyn_group.h"
@@ -82,13 +82,18 @@ struct WaveBatch {
 };
 
 constexpr int kWaveKeyStride = 34;  // key table entries per server: n = 0 .. Q + 1 (Q <= 32)
+constexpr int kWaveMaxS = 8;        // servers of the wave kernel (NG = 4 ring registers)
 struct WaveLds {
-  int32_t kt[4 * kWaveKeyStride];  // FAST single-choice keys of this step [server][n] (first: its
-                                   // address needs no constant, ds_read2 offsets are 8-bit)
-  int2 img[32 * 4];       // ring image [pos][server] for the carried-in walk and `last`
-  uint32_t own[4 * 128];  // insert owner of each (server, slot) in a flush: seq << 6 | lane
-  uint32_t chg[4 * 4];    // written-slot masks [word][server]
+  int32_t kt[kWaveMaxS * kWaveKeyStride];  // FAST single-choice keys of this step [server][n]
+                                           // (first: no constant in its address, ds_read2
+                                           // offsets are 8-bit)
+  int2 img[32 * kWaveMaxS];       // ring image [pos][server] for the carried-in walk and `last`
+  uint32_t own[kWaveMaxS * 128];  // insert owner of each (server, slot) in a flush: seq << 6 | lane
+  uint32_t chg[4 * kWaveMaxS];    // written-slot masks [word][server]
 };
+// Server lanes a reduction / key table covers: 4 for NG <= 2 (S <= 4), 8 for NG = 4 (S <= 8).
+template <int NG>
+constexpr int kWaveLanesS = NG <= 2 ? 4 : 8;
 
 __device__ __forceinline__ int32_t rdl(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ uint32_t rdl(uint32_t v, int l) {
@@ -143,9 +148,10 @@ template <int NG>
 __device__ __forceinline__ int32_t wave_count(const uint64_t (&live)[NG], int lane) {
   const bool odd = lane & 1;
   uint32_t w = odd ? (uint32_t)(live[0] >> 32) : (uint32_t)live[0];
-  if constexpr (NG > 1) {
-    const uint32_t w1 = odd ? (uint32_t)(live[NG - 1] >> 32) : (uint32_t)live[NG - 1];
-    w = (lane & 2) ? w1 : w;
+#pragma unroll
+  for (int g = 1; g < NG; ++g) {
+    const uint32_t wg = odd ? (uint32_t)(live[g] >> 32) : (uint32_t)live[g];
+    w = ((lane >> 1) & (NG - 1)) == g ? wg : w;
   }
   return __builtin_popcount(w);
 }
@@ -164,7 +170,7 @@ __device__ __forceinline__ void wave_flush(const SimParams& p, WaveSrv& V, WaveE
   uint32_t pre = 0u, rcb = 0u;
   float scale = p.svc_scale[0];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
+  for (int s = 0; s < kWaveMaxS; ++s) {
     if (s < S) {
       const bool mine = Bt.lc == s;
       const uint64_t m = __ballot(ins && mine);
@@ -186,7 +192,7 @@ __device__ __forceinline__ void wave_flush(const SimParams& p, WaveSrv& V, WaveE
   const uint32_t me_tag = (seq << 6) | (uint32_t)lane;
   if (slot >= 0) {
     atomicMax(&Ld.own[key], me_tag);  // the last insert into a slot is the one that stays
-    atomicOr(&Ld.chg[((uint32_t)slot >> 5) * 4u + (uint32_t)Bt.lc], 1u << (slot & 31));
+    atomicOr(&Ld.chg[((uint32_t)slot >> 5) * kWaveMaxS + (uint32_t)Bt.lc], 1u << (slot & 31));
   }
   wave_sync();
   if (slot >= 0 && Ld.own[key] == me_tag) {
@@ -232,15 +238,17 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
       return (float)q;
     }
   };
-  const int s4 = lane & 3;  // the server whose queue count this lane holds
+  constexpr int LS = kWaveLanesS<NG>;  // server lanes of the reductions
+  constexpr int LPS = 64 / LS;         // key-table lanes per server
+  const int s4 = lane & (LS - 1);  // the server whose queue count this lane holds
   int32_t* const kt_s = Ld.kt + s4 * KT;
   if constexpr (TAB) {
-    // the step's key table: lanes 16 s .. 16 s + 15 fill server s's entries n = 0 .. Q + 1
-    const int ts = lane >> 4;
+    // the step's key table: lanes LPS s .. LPS s + LPS - 1 fill server s's entries n = 0 .. Q + 1
+    const int ts = lane / LPS;
     const double den = __shfl(V.den, ts, 64), rcp = __shfl(V.rcp, ts, 64);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int nn = (lane & 15) + 16 * k;
+    for (int k = 0; k < (KT + LPS - 1) / LPS; ++k) {
+      const int nn = (lane & (LPS - 1)) + LPS * k;
       if (nn < Q + 2)  // servers past S: never eligible
         Ld.kt[ts * KT + nn] = (nn < Q && ts < S) ? f32_key(score_of(nn, den, rcp)) : 0x7FFFFFFF;
     }
@@ -262,25 +270,25 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
   // a lone wave's step 2.5 us faster; else the four halves' popcounts by the scalar unit, packed as
   // bytes of one SGPR and unpacked by one v_bfe -- fewer VALU, 2.5 % faster at 4 envs per SIMD
   // (profiles/r03w/ab_wave_counts.txt)
-  const bool odd = (lane & 1) != 0, hi_reg = (lane & 2) != 0;
   const uint32_t cnt_sh = (uint32_t)(lane & 3) * 8u;
   auto count_at = [&](int32_t t) -> int32_t {
-    const uint64_t m0 = __ballot(R.tc[0] > t);
+    uint64_t m[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) m[g] = __ballot(R.tc[g] > t);
     if constexpr (VC) {
-      uint32_t w = odd ? (uint32_t)(m0 >> 32) : (uint32_t)m0;
-      if constexpr (NG > 1) {
-        const uint64_t m1 = __ballot(R.tc[NG - 1] > t);
-        const uint32_t w1 = odd ? (uint32_t)(m1 >> 32) : (uint32_t)m1;
-        w = hi_reg ? w1 : w;
-      }
-      return (int32_t)__builtin_popcount(w);
+      return wave_count<NG>(m, lane);
     } else {
-      uint32_t packed = (uint32_t)__builtin_popcount((uint32_t)m0) +
-                        ((uint32_t)__builtin_popcount((uint32_t)(m0 >> 32)) << 8);
-      if constexpr (NG > 1) {
-        const uint64_t m1 = __ballot(R.tc[NG - 1] > t);
-        packed += ((uint32_t)__builtin_popcount((uint32_t)m1) << 16) +
-                  ((uint32_t)__builtin_popcount((uint32_t)(m1 >> 32)) << 24);
+      uint32_t packed = (uint32_t)__builtin_popcount((uint32_t)m[0]) +
+                        ((uint32_t)__builtin_popcount((uint32_t)(m[0] >> 32)) << 8);
+      if constexpr (NG > 1)
+        packed += ((uint32_t)__builtin_popcount((uint32_t)m[1]) << 16) +
+                  ((uint32_t)__builtin_popcount((uint32_t)(m[1] >> 32)) << 24);
+      if constexpr (NG > 2) {  // servers 4..7 in a second word
+        const uint32_t packed2 = (uint32_t)__builtin_popcount((uint32_t)m[2]) +
+                                 ((uint32_t)__builtin_popcount((uint32_t)(m[2] >> 32)) << 8) +
+                                 ((uint32_t)__builtin_popcount((uint32_t)m[3]) << 16) +
+                                 ((uint32_t)__builtin_popcount((uint32_t)(m[3] >> 32)) << 24);
+        packed = (lane & 4) ? packed2 : packed;
       }
       return (int32_t)__builtin_amdgcn_ubfe(packed, cnt_sh, 8u);
     }
@@ -324,7 +332,7 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
       if constexpr (TAB) {
         // finite scores: the eligible minimum, h among equal minima, else the lowest such server
         // (every server full: no eligible tie, and the find-first-set of 0 is -1: dropped)
-        const int32_t mk = __builtin_amdgcn_readfirstlane(group_min_i32<4>(key));
+        const int32_t mk = __builtin_amdgcn_readfirstlane(group_min_i32<LS>(key));
         const uint32_t hbit = 1u << (int)__umulhi(u2, (uint32_t)S);
         const uint32_t tie = (uint32_t)__ballot(key == mk) & (mk != 0x7FFFFFFF ? smask : 0u);
         const uint32_t sel = (tie & hbit) ? hbit : tie;
@@ -341,11 +349,11 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
         const uint32_t em = (uint32_t)__ballot(n < Q) & smask;
         const bool num = elig && score == score;
         const float m = key_f32(__builtin_amdgcn_readfirstlane(
-            group_min_i32<4>(num ? f32_key(score) : 0x7f800000)));
+            group_min_i32<LS>(num ? f32_key(score) : 0x7f800000)));
         const int h = (int)__umulhi(u2, (uint32_t)S);
         const int c0 = ((em >> h) & 1u) ? h : (em ? __builtin_ctz(em) : -1);
-        const uint32_t tie = (uint32_t)__ballot(num && score == m) & 0xFu;
-        const uint32_t nan = (uint32_t)__ballot(score != score) & 0xFu;
+        const uint32_t tie = (uint32_t)__ballot(num && score == m) & ((1u << LS) - 1u);
+        const uint32_t nan = (uint32_t)__ballot(score != score) & ((1u << LS) - 1u);
         c = c0 < 0 ? -1 : ((((tie | nan) >> c0) & 1u) ? c0 : (tie ? __builtin_ctz(tie) : -1));
       }
       const bool lg = lane == bi;  // this arrival's batch lane (the insert log)
@@ -360,7 +368,8 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
       const int T = rdl(pl, c);  // ring register x 64 + lane of the push
       if (rdl(n, c) == Q - 1) {  // rare: this push fills the ring -- keep the t_complete it
         int32_t old = rdl(R.tc[0], T & 63);  // overwrites (the last completion)
-        if constexpr (NG > 1) old = T >= 64 ? rdl(R.tc[NG - 1], T & 63) : old;
+#pragma unroll
+        for (int g = 1; g < NG; ++g) old = (T >> 6) == g ? rdl(R.tc[g], T & 63) : old;
         V.saved = lane == c ? old : V.saved;
       }
 #pragma unroll
@@ -420,7 +429,7 @@ __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParam
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
     const int srv = 2 * g + (lane >> 5);
-    if (srv < S && rpos < Q) Ld.img[rpos * 4 + srv] = make_int2(R.tc[g], R.ta[g]);
+    if (srv < S && rpos < Q) Ld.img[rpos * kWaveMaxS + srv] = make_int2(R.tc[g], R.ta[g]);
   }
   wave_sync();
   if (V.act && V.cnt0 > 0) {
@@ -429,7 +438,7 @@ __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParam
     int32_t prev = V.last;
     uint32_t rc = V.rcnt;
     for (int i = 0; i < V.cnt0; ++i) {
-      const int2 e = Ld.img[pos * 4 + lane];
+      const int2 e = Ld.img[pos * kWaveMaxS + lane];
       if (e.x > dt) break;
       const u32x4 d = philox4x32_10(
           u32x4{rc >> 1, E.gid, E.episode, (kStreamReservoir << 24) | (uint32_t)lane}, p.key0,
@@ -439,7 +448,7 @@ __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParam
         res_b[(uint32_t)lane * K + (uint32_t)slot] =
             make_uint3((uint32_t)(e.x - e.y), (uint32_t)(e.x - (e.y > prev ? e.y : prev)),
                        base_ms + (base_rem + (uint32_t)e.x) / 1000u);
-        atomicOr(Ld.chg + ((uint32_t)slot >> 5) * 4u + (uint32_t)lane, 1u << (slot & 31));
+        atomicOr(Ld.chg + ((uint32_t)slot >> 5) * kWaveMaxS + (uint32_t)lane, 1u << (slot & 31));
       }
       prev = e.x;
       rc = count_inc(rc);
@@ -466,7 +475,7 @@ __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParam
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
     const int srv = 2 * g + (lane >> 5);
-    if (srv < S && rpos < Q) Ld.img[rpos * 4 + srv].x = R.tc[g];
+    if (srv < S && rpos < Q) Ld.img[rpos * kWaveMaxS + srv].x = R.tc[g];
   }
   wave_sync();
   if (V.act && V.cnt0 + V.pushed > n) {  // a flow completed this step: the newest one
@@ -475,7 +484,7 @@ __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParam
     } else {
       int pl = V.wp - n - 1;
       pl = pl < 0 ? pl + Q : pl;
-      V.last = Ld.img[pl * 4 + lane].x;
+      V.last = Ld.img[pl * kWaveMaxS + lane].x;
     }
   }
   wave_sync();
@@ -511,14 +520,14 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
   V.act = lane < S;
   V.scale = p.svc_scale[0];
 #pragma unroll
-  for (int k = 1; k < 4; ++k) V.scale = (k == lane) ? p.svc_scale[k] : V.scale;
+  for (int k = 1; k < kWaveMaxS; ++k) V.scale = (k == lane) ? p.svc_scale[k] : V.scale;
   V.den = 1.0;
   V.rcp = 1.0;
   V.assigned = 0;
   V.saved = 0;
-  if (lane < 16) Ld.chg[lane] = 0u;
+  if (lane < 4 * kWaveMaxS) Ld.chg[lane] = 0u;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) Ld.own[i * 64 + lane] = 0u;
+  for (int i = 0; i < kWaveMaxS * 128 / 64; ++i) Ld.own[i * 64 + lane] = 0u;
   uint32_t seq = 1u;
   WaveRing<NG> R;
 #pragma unroll
@@ -605,9 +614,12 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
     {  // tail = t_complete of the last queued flow, from the ring lanes (no dependent load)
       const int tp = V.wp == 0 ? Q - 1 : V.wp - 1;
       const int src = (lane & 1) * 32 + (tp & 31);
-      const int32_t t0 = __shfl(R.tc[0], src, 64);
-      const int32_t t1 = __shfl(R.tc[NG - 1], src, 64);
-      const int32_t tl = (lane & 2) ? t1 : t0;
+      int32_t tl = __shfl(R.tc[0], src, 64);
+#pragma unroll
+      for (int g = 1; g < NG; ++g) {
+        const int32_t tg = __shfl(R.tc[g], src, 64);
+        tl = ((lane >> 1) & (NG - 1)) == g ? tg : tl;
+      }
       V.tail = (V.act && V.cnt0 > 0) ? tl : 0;
     }
     wave_sync();
@@ -630,7 +642,8 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
     st.last_tc[sb] = V.last;
     st.res_count[sb] = V.rcnt;
     *reinterpret_cast<uint4*>(st.chg + (size_t)sb * 4) =
-        make_uint4(Ld.chg[lane], Ld.chg[4 + lane], Ld.chg[8 + lane], Ld.chg[12 + lane]);
+        make_uint4(Ld.chg[lane], Ld.chg[kWaveMaxS + lane], Ld.chg[2 * kWaveMaxS + lane],
+                   Ld.chg[3 * kWaveMaxS + lane]);
     if (MODE != kModeReset && assign_out != nullptr) assign_out[sb] = V.assigned;
   }
   if (lane == 0) {

@@ -50,11 +50,12 @@ inline int dyn_group_lanes(const LaunchCtx& L) {
   return g;
 }
 
-// One wave per env (lbsim_dyn_wave.h): S <= 4, Q <= 32, SED / SED2 / LSQ / LSQ2, the default
+// One wave per env (lbsim_dyn_wave.h): S <= 8, Q <= 32, SED / SED2 / LSQ / LSQ2, the default
 // mapping, and a batch small enough that one env's event-loop chain, not issue throughput, sets
-// the step time: at most 4 waves (envs) per SIMD, B <= 4096 on 256 CUs.  Measured S = 4 dynamics,
-// wave vs server-per-lane groups (profiles/r03w/wave_sweep.txt): 1024 envs 0.041 vs 0.084 ms,
-// 4096 0.066 vs 0.090, 8192 0.108 vs 0.095 (8 waves per SIMD: issue-bound, the groups win).
+// the step time: at most 4 waves (envs) per SIMD for S <= 4 (B <= 4096 on 256 CUs), 2 for S <= 8.
+// Measured dynamics, wave vs server-per-lane groups (profiles/r03w/wave_sweep*.txt): S = 4 1024
+// envs 0.041 vs 0.084 ms, 4096 0.066 vs 0.090, 8192 0.108 vs 0.095 (8 waves per SIMD:
+// issue-bound, the groups win); S = 8 2048 envs 0.058 vs 0.078, 4096 0.087 vs 0.083.
 // LBSIM_DYN_WAVE_MAX_B overrides the limit; LBSIM_DYN_WAVE = 0 disables the kernel, 1 uses it at
 // every batch size it applies to; a forced LBSIM_DYN_GROUP_LANES width wins over both.
 inline bool dyn_wave_ok(const LaunchCtx& L) {
@@ -68,8 +69,9 @@ inline bool dyn_wave_ok(const LaunchCtx& L) {
   }();
   static const bool forced_lanes = std::getenv("LBSIM_DYN_GROUP_LANES") != nullptr;
   if (mode == 0 || forced_lanes || L.dyn_mapping == LBSIM_DYN_ENV_PER_LANE) return false;
-  if (L.S > 4 || L.prm.Q > 32 || L.prm.policy == LBSIM_POLICY_ALIAS) return false;
-  return mode == 1 || (int64_t)L.B <= (max_b >= 0 ? max_b : 4 * (int64_t)L.simds);
+  if (L.S > 8 || L.prm.Q > 32 || L.prm.policy == LBSIM_POLICY_ALIAS) return false;
+  const int64_t per_simd = L.S <= 4 ? 4 : 2;  // S = 8: 2048 envs 0.058 vs 0.078 ms, 4096 0.087 vs 0.083
+  return mode == 1 || (int64_t)L.B <= (max_b >= 0 ? max_b : per_simd * (int64_t)L.simds);
 }
 
 // Dynamics of one step (mode kModeStep) or of a reset with warm-up (kModeReset).

@@ -320,7 +320,7 @@ def test_wider_groups_bit_exact(lanes):
 @pytest.mark.parametrize("step", ["auto", "fused"])
 def test_wave_kernel_bit_exact(step):
     """LBSIM_DYN_WAVE=1 runs the one-wave-per-env dynamics (lbsim_dyn_wave.h) on every simulator
-    case it applies to (S <= 4, queue capacity <= 32, every policy but ALIAS) at any batch size,
+    case it applies to (S <= 8, queue capacity <= 32, every policy but ALIAS) at any batch size,
     the 8256-env case included: bit-exact vs the oracle.  step = auto: a dynamics_wave_kernel
     launch then an observe launch; fused (LBSIM_STEP_KERNEL=fused, opt-in): one step_wave_kernel
     launch (dynamics then observe per wave).  Resets use dynamics_wave_kernel in both.  The
@@ -330,7 +330,7 @@ def test_wave_kernel_bit_exact(step):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     ks = [f"test_simulator_bit_exact_vs_oracle[{c}-{m}]" for c in range(len(CONFIGS))
           for m in ("server", "server-fused")
-          if CONFIGS[c]["S"] <= 4 and CONFIGS[c]["kw"].get("queue_capacity", 32) <= 32
+          if CONFIGS[c]["S"] <= 8 and CONFIGS[c]["kw"].get("queue_capacity", 32) <= 32
           and CONFIGS[c]["kw"].get("assign_policy") != "alias"]
     assert len(ks) >= 20
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p",
@@ -449,12 +449,14 @@ def test_full_size_trace_replay_c3(lib, oracle_mod):
 
 
 def test_dynamics_kernel_dispatch(lib):
-    """lbsim_dynamics_kernel names the kernel the launches use: one wave per env for small S <= 4
+    """lbsim_dynamics_kernel names the kernel the launches use: one wave per env for small S <= 8
     batches (at most 4 envs per SIMD, queue capacity <= 32, not ALIAS), server-per-lane groups
     otherwise, one lane per env when asked for."""
     from marllb_amd.env import VecLoadBalanceEnv
     cases = [(dict(num_envs=257, num_servers=4), 2), (dict(num_envs=1, num_servers=4), 2),
-             (dict(num_envs=8256, num_servers=4), 1), (dict(num_envs=64, num_servers=8), 1),
+             (dict(num_envs=8256, num_servers=4), 1), (dict(num_envs=64, num_servers=8), 2),
+             (dict(num_envs=4096, num_servers=4), 2), (dict(num_envs=4096, num_servers=8), 1),
+             (dict(num_envs=64, num_servers=16), 1),
              (dict(num_envs=64, num_servers=4, assign_policy="alias"), 1),
              (dict(num_envs=64, num_servers=4, queue_capacity=64), 1),
              (dict(num_envs=64, num_servers=4, dyn_mapping="env"), 0)]
