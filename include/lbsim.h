@@ -86,8 +86,8 @@ enum lbsim_dyn_mapping {
   LBSIM_DYN_SERVER_PER_LANE = 2  /* a group of G lanes = one env, one lane per server: G =     */
                                  /* pow2 >= S, except S <= 4 on small batches (B*4/64 <= half */
                                  /* the device's SIMDs), which get G = 8 (twice the waves);    */
-                                 /* S <= 4 batches of at most 4 envs per SIMD (Q <= 32, no     */
-                                 /* ALIAS) run one WAVE per env instead         */
+                                 /* S <= 8 batches of at most 4 (S <= 4) or 2 envs per SIMD   */
+                                 /* (Q <= 32, no ALIAS) run one WAVE per env    */
 };
 
 /* The dynamics kernel a handle's launches use (lbsim_dynamics_kernel). */

@@ -7,16 +7,17 @@
 // LDS round trip for the next queue head and one for the next drawn arrival, two DPP reductions,
 // the reservoir insert and the draw-ahead refill every G iterations.  Here the whole env is one
 // wave and its state is laid out so that an arrival is a short straight-line block:
-//   * ring lanes: servers 2g and 2g + 1 own the two 32-lane halves of ring register g (NG = 1 or
-//     2 registers each of {t_complete, t_arrival}); ring position pos of server s is register
+//   * ring lanes: servers 2g and 2g + 1 own the two 32-lane halves of ring register g (NG = 1, 2
+//     or 4 registers each of {t_complete, t_arrival}); ring position pos of server s is register
 //     s >> 1, lane 32 (s & 1) + pos, so the HBM ring loads and stores lane for
 //     lane.  With FIFO service and arrival times that never decrease, a slot's flow is queued at
 //     time t iff its t_complete > t (free slots hold kDead): the pops before an arrival at ta are
 //     implicit, and a server's flow count at ta is the popcount of its half of one ballot per
 //     register (the oracle's pop_until, lbsim_oracle.c sim_step, however many complete);
 //   * the counts for the NEXT arrival are taken while the current one is chosen (its time is
-//     known: arrivals are drawn ahead), so the chain from one choice to the next is the pushed
-//     flow's +1 on its server, the SED score (3 f64 ops), one DPP minimum and a ballot of the ties;
+//     known: arrivals are drawn ahead), and with them the keys of both outcomes of the push from a
+//     per-step LDS key table (wave_event_loop), so the chain from one choice to the next is a
+//     select, one DPP minimum, a ballot of the ties and a find-first-set;
 //   * server lanes: lane s < S holds server s's fields (write position, tail, Algorithm R count,
 //     SED denominator); the push is a select in ring lane 32 (c & 1) + wp_c and one in lane c;
 //   * arrivals: 64 at a time (lane j: arrival base + j, its Philox block, gap and work or its
