@@ -305,10 +305,10 @@ int step_kernel_of(const lbsim_t* h) {
   return h->cfg.step_kernel != LBSIM_STEP_AUTO ? h->cfg.step_kernel : env;
 }
 
-// The one-launch wave step (step_wave_kernel, 2 waves per SIMD): one wave per env, FUSED asked
-// for, or AUTO on batches of at most 2 envs per SIMD (LBSIM_STEP_WAVE_MAX_B overrides), where one
-// launch instead of two pays (profiles/r03w/ab_step_wave_fused.txt); larger AUTO batches take the
-// two launches (their 4 waves per SIMD need the 128-VGPR kernels).
+// The one-launch wave step (step_wave_kernel): one wave per env and S <= 4, FUSED asked for, or
+// AUTO on batches of at most 4 envs per SIMD (every S <= 4 wave batch; LBSIM_STEP_WAVE_MAX_B
+// overrides), where one launch instead of two pays: 2048 x 4 0.0711 -> 0.0620 ms per step, 4096 x 4
+// +2.5 % (profiles/r03w/ab_step_wave_fused.txt).
 bool use_step_wave(const lbsim_t* h) {
   static const int64_t max_b = [] {
     const char* e = std::getenv("LBSIM_STEP_WAVE_MAX_B");
@@ -318,7 +318,7 @@ bool use_step_wave(const lbsim_t* h) {
   if (!dyn_wave_ok(L) || L.S > kObsChunk) return false;  // one observe chunk per wave: S <= 4
   const int k = step_kernel_of(h);
   if (k == LBSIM_STEP_FUSED) return true;
-  return k == LBSIM_STEP_AUTO && (int64_t)L.B <= (max_b >= 0 ? max_b : 2 * (int64_t)L.simds);
+  return k == LBSIM_STEP_AUTO && (int64_t)L.B <= (max_b >= 0 ? max_b : 4 * (int64_t)L.simds);
 }
 
 // The fused step for this handle: its config (LBSIM_STEP_KERNEL=split|fused overrides AUTO) and

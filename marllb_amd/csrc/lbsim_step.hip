@@ -17,11 +17,6 @@
 #include "lbsim_dyn_group.h"
 #include "lbsim_dyn_wave.h"
 
-// Waves per SIMD step_wave_kernel is compiled for (an A/B build knob: 4 caps it at 128 VGPRs and
-// spills, measured slower, profiles/r03w/ab_step_wave_fused.txt).
-#ifndef LBSIM_STEP_WAVE_OCC
-#define LBSIM_STEP_WAVE_OCC 2
-#endif
 
 namespace lbk {
 namespace {
@@ -52,11 +47,13 @@ __global__ void __launch_bounds__(64)
 // (dyn_wave_env) and then observes it (observe_env_wave: S <= 4 is one chunk, one wave), so the
 // step is ONE launch and each env's observation runs as soon as its own event loop ends, while
 // slower envs still simulate.  Same routines, same order: the same bits as the two launches.
-// 2 waves per SIMD: the observe phase inlined after the event loop needs ~190 VGPRs (capped at
-// 128 it spilled 64; out of line its call frames went through 1 KB of scratch per lane and the
-// kernel ran 0.141 ms at 4096 x 4).  So it serves batches of at most 2 envs per SIMD (use_step_wave).
-template <int NG, int POLICY, bool TRACE>
-__global__ void __launch_bounds__(64, LBSIM_STEP_WAVE_OCC)
+// OCC waves per SIMD.  2: the observe phase inlined after the event loop takes ~190 VGPRs, for
+// batches of at most 2 envs per SIMD, with the VALU queue counts (the shorter chain).  4: capped at
+// 128 VGPRs (it spills, yet beats the two launches at 4096 x 4: 45.0-45.6 vs 43.4-44.2 M, same
+// box), for 2-4 envs per SIMD, with the scalar counts (profiles/r03w/ab_step_wave_fused.txt).  Out
+// of line, the observe phase's call frames went through 1 KB of scratch per lane (0.141 ms).
+template <int NG, int POLICY, bool TRACE, int OCC>
+__global__ void __launch_bounds__(64, OCC)
     step_wave_kernel(DevState st, SimParams p, const void* action, int action_dtype,
                      int32_t* assign_out, ObsOutputs out) {
   __shared__ union {
@@ -66,23 +63,31 @@ __global__ void __launch_bounds__(64, LBSIM_STEP_WAVE_OCC)
   __shared__ float s_obs[kObsChunk * NF];
   __shared__ float s_act[kObsChunk];
   const int lane = (int)threadIdx.x;
-  if (!dyn_wave_env<NG, kModeStep, POLICY, TRACE, true>(st, p, action, action_dtype, assign_out,
-                                                        nullptr, blockIdx.x, lane, L.dyn))
+  if (!dyn_wave_env<NG, kModeStep, POLICY, TRACE, OCC == 2>(st, p, action, action_dtype,
+                                                            assign_out, nullptr, blockIdx.x, lane,
+                                                            L.dyn))
     return;
   __syncthreads();  // state stores complete and visible to this workgroup; LDS reused below
   observe_env_wave<kObsChunk>(st, p, out, blockIdx.x, L.obs, s_obs, s_act, lane);
 }
 
+template <int NG, int POLICY, int OCC>
+void launch_wo(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
+               const ObsOutputs& o, hipStream_t s) {
+  const dim3 block(64), grid((unsigned)L.B);
+  if (L.prm.trace)
+    hipLaunchKernelGGL((step_wave_kernel<NG, POLICY, true, OCC>), grid, block, 0, s, L.st, L.prm,
+                       action, dtype, assign, o);
+  else
+    hipLaunchKernelGGL((step_wave_kernel<NG, POLICY, false, OCC>), grid, block, 0, s, L.st,
+                       L.prm, action, dtype, assign, o);
+}
+
 template <int NG, int POLICY>
 void launch_w(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
               const ObsOutputs& o, hipStream_t s) {
-  const dim3 block(64), grid((unsigned)L.B);
-  if (L.prm.trace)
-    hipLaunchKernelGGL((step_wave_kernel<NG, POLICY, true>), grid, block, 0, s, L.st, L.prm,
-                       action, dtype, assign, o);
-  else
-    hipLaunchKernelGGL((step_wave_kernel<NG, POLICY, false>), grid, block, 0, s, L.st, L.prm,
-                       action, dtype, assign, o);
+  if ((int64_t)L.B <= 2 * (int64_t)L.simds) launch_wo<NG, POLICY, 2>(L, action, dtype, assign, o, s);
+  else launch_wo<NG, POLICY, 4>(L, action, dtype, assign, o, s);
 }
 
 template <int NG>
