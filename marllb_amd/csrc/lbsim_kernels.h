@@ -2030,9 +2030,13 @@ __device__ __forceinline__ void observe_env_wave(const DevState& st, const SimPa
                                                  const ObsOutputs& out, size_t b, ObsScratch& sc,
                                                  float* s_obs, float* s_act, int lane) {
   const int S = p.S;
-  for (int s0 = 0; s0 < S; s0 += kObsChunk)
-    observe_chunk<true, true>(st, p, b, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk, sc, s_obs,
-                              lane);
+  if constexpr (MAXS <= kObsChunk) {  // one chunk: straight-line code, no loop-carried s0
+    observe_chunk<true, true>(st, p, b, 0, S, sc, s_obs, lane);
+  } else {
+    for (int s0 = 0; s0 < S; s0 += kObsChunk)
+      observe_chunk<true, true>(st, p, b, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk, sc, s_obs,
+                                lane);
+  }
   observe_outputs<MAXS, kModeStep, true>(st, p, out, b, s_obs, s_act, lane, 64);
   wave_sync();  // s_obs / s_act reused by the next env
 }
