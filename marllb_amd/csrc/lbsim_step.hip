@@ -47,11 +47,11 @@ __global__ void __launch_bounds__(64)
 // (dyn_wave_env) and then observes it (observe_env_wave: S <= 4 is one chunk, one wave), so the
 // step is ONE launch and each env's observation runs as soon as its own event loop ends, while
 // slower envs still simulate.  Same routines, same order: the same bits as the two launches.
-// OCC waves per SIMD.  2: the observe phase inlined after the event loop takes ~190 VGPRs, for
-// batches of at most 2 envs per SIMD, with the VALU queue counts (the shorter chain).  4: capped at
-// 128 VGPRs (it spills, yet beats the two launches at 4096 x 4: 45.0-45.6 vs 43.4-44.2 M, same
-// box), for 2-4 envs per SIMD, with the scalar counts (profiles/r03w/ab_step_wave_fused.txt).  Out
-// of line, the observe phase's call frames went through 1 KB of scratch per lane (0.141 ms).
+// OCC waves per SIMD.  2: batches of at most 2 envs per SIMD, with the VALU queue counts (the
+// shorter chain).  4: 2-4 envs per SIMD, with the scalar counts (profiles/r03w/ab_step_wave_fused.txt).
+// Both take 118-120 VGPRs with no spill since the one-chunk observe is straight-line code (the
+// chunk loop took 194 and spilled 64 under the 128 cap: profiles/r03o/).  Out of line, the observe
+// phase's call frames went through 1 KB of scratch per lane (0.141 ms).
 template <int NG, int POLICY, bool TRACE, int OCC>
 __global__ void __launch_bounds__(64, OCC)
     step_wave_kernel(DevState st, SimParams p, const void* action, int action_dtype,
