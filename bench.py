@@ -52,14 +52,16 @@ def algorithmic_bytes(S: int, slots_per_env: float, inflight_per_env: float):
     return {"observe_kernel": obs, "dynamics_kernel": dyn, "fused_step_kernel": obs + dyn}
 
 
-def valu_roofline(B: int, S: int, avg: dict):
+def valu_roofline(B: int, S: int, avg: dict, sigs: dict):
     """The VALU side of each simulator kernel, from profiles/pmc_valu.json
     (tools/pmc_valu.py over rocprofv3 SQ counter passes of this workload, VALU issue costs measured
     by tools/ubench_valu.hip): VALU instructions per env-step and per class, the SIMD issue cycles
     they cost at the measured rates, and that issue time against this run's HIP-event kernel time
     (frac = issue_bound_ms / avg_launch_ms: 1.0 = the SIMDs never stop issuing VALU), plus the
-    share of wave cycles parked on s_waitcnt / barriers (SQ_WAIT_ANY).  None when the committed
-    counters are for another shape."""
+    share of wave cycles parked on s_waitcnt / barriers (SQ_WAIT_ANY).  Counters are matched to
+    the kernels that ran by their full template signature (sigs: lbsim_launch_names); a kernel
+    whose signature the file does not hold gets {"pmc_kernel": None, "stale_reason": ...}, never
+    another instantiation's counters.  None when the committed counters are for another shape."""
     path = os.path.join(ROOT, "profiles", "pmc_valu.json")
     if not os.path.exists(path):
         return None
@@ -68,9 +70,13 @@ def valu_roofline(B: int, S: int, avg: dict):
         return None
     out = {"source": "profiles/pmc_valu.json", "simds": t["simds"], "clock_hz": t["clock_hz"],
            "issue_costs_simd_cyc": t["ubench_simd_cyc_per_inst"]}
-    for full, rec in t["kernels"].items():
-        name = next((n for n in avg if full.startswith(n)), None)
-        if name is None:
+    for name in avg:
+        full = sigs.get(name)
+        rec = t["kernels"].get(full) if full else None
+        if rec is None:
+            out[name] = {"pmc_kernel": None, "ran": full,
+                         "stale_reason": f"profiles/pmc_valu.json has no counters for {full!r} "
+                                         f"(it holds {sorted(t['kernels'])})"}
             continue
         out[name] = {"pmc_kernel": full, "valu_per_env_step": rec["valu_per_env_step"],
                      "classes_per_env_step": rec["classes_per_env_step"],
@@ -159,6 +165,11 @@ def parse():
                          "stepped on its own HIP stream with no join between groups per step "
                          "(EnvPool-style async groups).  Off by default; reported beside `value`, "
                          "never as it")
+    ap.add_argument("--prewarm-ms", type=float, default=200.0,
+                    help="before the measured env is created, step a scratch env of the same "
+                         "shape for at least this long (GPU clocks and caches ramp up); the "
+                         "measured env's trajectory, warm-up and timed steps are unchanged.  "
+                         "Reported as prewarm_ms; 0 disables")
     ap.add_argument("--late-episode", default="",
                     help="rollout workload at N=1: after the headline measurement, keep stepping the "
                          "same envs and also time --steps steps from these episode steps (comma "
@@ -392,6 +403,44 @@ def late_episode(args, env, handle, lib, one_step, rate, B, S, done_steps):
     return res
 
 
+def prewarm_scratch(args, dev, B, S, common):
+    """Step a scratch env of the measured shape (its own seed, destroyed afterwards) for at least
+    --prewarm-ms of wall time, so the timed region does not start on an idle GPU's clocks.  The
+    measured env is created after it: its trajectory, W warm-up and K timed steps are exactly
+    those of a run without the pre-warm (the slots written per step depend on the episode
+    phase, so pre-warming on the measured env itself would change the timed work)."""
+    import torch
+    from marllb_amd.env import VecLoadBalanceEnv
+    if args.prewarm_ms <= 0:
+        return None
+    kw = dict(common, seed=args.seed ^ 0x5A5A5A5A)
+    if args.workload == "sac-gru":
+        kw["action_type"] = "continuous"
+    env = VecLoadBalanceEnv(B, S, max_steps=10000, **kw)
+    env.reset()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(args.seed + 7)
+    continuous = args.workload == "sac-gru"
+    n, t0 = 0, time.perf_counter()
+    while True:
+        if continuous:
+            a = torch.rand((B, S), device=dev, generator=gen) * 2.0
+        else:
+            a = torch.randint(0, 3, (B, S), device=dev, dtype=torch.int64, generator=gen)
+        env.step(a)
+        n += 1
+        if n % 8 == 0:
+            torch.cuda.synchronize()
+            if (time.perf_counter() - t0) * 1e3 >= args.prewarm_ms:
+                break
+    el = (time.perf_counter() - t0) * 1e3
+    env.close()
+    torch.cuda.synchronize()
+    return {"prewarm_ms": el, "steps": n,
+            "form": "a scratch env of the same shape (own seed), created, stepped and destroyed "
+                    "before the measured env exists; not part of W or K"}
+
+
 def spawn_ranks(args) -> int:
     """`bench.py --gpus N` without torchrun: start N rank processes of this script (one per GPU,
     the torchrun environment contract: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), before this
@@ -462,6 +511,7 @@ def main():
         tr = trace.builtin(args.trace)
     common = dict(device=dev, seed=args.seed, env_id_offset=shard.env_id_offset, autoreset=True,
                   assign_policy=args.policy, trace=tr, dyn_mapping=args.dyn_mapping)
+    prewarm = prewarm_scratch(args, dev, B, S, common)
     torch.manual_seed(args.seed)  # network init (random weights of the reference architecture)
     if args.workload == "rollout":
         env = VecLoadBalanceEnv(B, S, max_steps=10000, **common)
@@ -555,16 +605,28 @@ def main():
             ach = ab_k / (avg[k] * 1e-3) / 1e9
             per_kernel[k] = {"avg_launch_ms": avg[k], "algorithmic_bytes_per_launch": ab_k,
                              "achieved_GBps": ach, "frac": ach / HBM_PEAK_GBS}
+        # the template signature of each kernel the step launched (lbsim_launch_names), the key
+        # of the committed PMC counter files
+        ran = _lib.launch_names(handle, 0)
+        sigs = {names[c]: sig for c, sig in ran.items() if c in names}
+        for k in per_kernel:
+            per_kernel[k]["signature"] = sigs.get(k)
         dom = max(avg, key=avg.get)
         ab = abytes[dom] * B
         achieved = ab / (avg[dom] * 1e-3) / 1e9
-        valu = valu_roofline(B, S, avg)
-        traffic = None
+        valu = valu_roofline(B, S, avg, sigs)
+        traffic, traffic_note = None, None
         tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tfile):
             t = json.load(open(tfile))
-            if t.get("batch") == B and t.get("servers") == S and dom in t.get("bytes_per_launch", {}):
-                traffic = t["bytes_per_launch"][dom]
+            held = t.get("bytes_per_launch", {})
+            if t.get("batch") != B or t.get("servers") != S:
+                traffic_note = f"profiles/pmc_traffic.json is for {t.get('batch')} x {t.get('servers')}"
+            elif sigs.get(dom) in held:
+                traffic = held[sigs[dom]]
+            else:
+                traffic_note = (f"profiles/pmc_traffic.json has no counters for {sigs.get(dom)!r} "
+                                f"(it holds {sorted(held)})")
         out = {
             "metric": METRIC, "value": value, "unit": "env-steps/s",
             "n_gpus": dist.get_world_size() if world > 1 else 1,
@@ -588,7 +650,9 @@ def main():
                        "parallelism": f"env-shard x{world}", "dyn_mapping": args.dyn_mapping},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic, "algorithmic_bytes_per_launch": ab,
+                         "traffic": traffic, "traffic_source": "profiles/pmc_traffic.json"
+                         if traffic is not None else None, "stale_reason": traffic_note,
+                         "signature": sigs.get(dom), "algorithmic_bytes_per_launch": ab,
                          "avg_launch_ms": avg[dom],
                          "kernel_avg_ms": avg, "kernels": per_kernel, "valu": valu,
                          "accounting": {"reservoir_slots_written_per_env_step": slots / B,
@@ -597,6 +661,7 @@ def main():
                                                  "replay of the timed steps" if replay else
                                                  "lbsim_step_stats over as many further steps"}},
         }
+        out["prewarm"] = prewarm
         if args.workload != "rollout":
             out["config"]["workload"] = {
                 "sac-gru": f"problem-04 SAC-GRU actor (GRU {S * 11}->128, fc 128->256, heads "

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define LBSIM_ABI_VERSION 4
+#define LBSIM_ABI_VERSION 5
 #define LBSIM_MAX_SERVERS 64   /* S <= 64: BASELINE configs[4] read literally is 4 agents x 16 */
                                /* servers = 64 (S > 16: server-per-lane dynamics only)       */
 #define LBSIM_RESERVOIR_K 128  /* reservoir.py:31 capacity=128, reservoir.h:24               */
@@ -100,9 +100,11 @@ enum lbsim_dyn_kernel {
 /* How lbsim_step runs; every choice produces the same bits.  FUSED: one launch per step whose
  * workgroups simulate their envs and then observe them: step_wave_kernel for
  * one-wave-per-env handles, fused_step_kernel for server-per-lane groups of <= 16 lanes (else
- * SPLIT); SPLIT: a dynamics launch and an observe launch.  AUTO = SPLIT (both fused forms
- * measured slower).  The environment variable LBSIM_STEP_KERNEL=split|fused
- * overrides AUTO. */
+ * SPLIT); SPLIT: a dynamics launch and an observe launch.  AUTO: the one-launch step_wave_kernel
+ * for one-wave-per-env handles with S <= 4 and at most 4 envs per SIMD (the single-env facade
+ * and BASELINE configs[1]'s 4096 x 4 on 256 CUs; LBSIM_STEP_WAVE_MAX_B overrides the limit),
+ * else SPLIT (the server-per-lane fused form measured slower).  The environment
+ * variable LBSIM_STEP_KERNEL=split|fused overrides AUTO. */
 enum lbsim_step_kernel { LBSIM_STEP_AUTO = 0, LBSIM_STEP_SPLIT = 1, LBSIM_STEP_FUSED = 2 };
 
 /*
@@ -404,9 +406,20 @@ int lbsim_vpp_features(const float* tv, const float* ts, int64_t res_per_ts, int
  * kernel.  Used by bench.py.
  */
 #define LBSIM_PROFILE_CLASSES 5
+/* (lbsim_profile_end reports the first 4 classes only: a handle whose steps are one launch --
+ * step_wave_kernel under AUTO, or FUSED -- times them in class 4, so its callers need
+ * lbsim_profile_end_ex(..., 5).) */
 int lbsim_profile_begin(lbsim_t* h, int max_launches);
 int lbsim_profile_end(lbsim_t* h, double* ms_out, int64_t* count_out);
 int lbsim_profile_end_ex(lbsim_t* h, double* ms_out, int64_t* count_out, int n_classes);
+
+/* The kernels the last lbsim_step_ex (which = 0) or lbsim_reset_ex (which = 1) of this handle
+ * launched, in launch order, as "class=name;class=name" (class as in the profiler above; name the
+ * kernel's template signature as rocprofv3 reports it, e.g. "0=dynamics_group_kernel<4, 0, 0,
+ * false, 1>;1=observe_kernel<4, 0, false>").  bench.py keys its committed PMC counter files by
+ * these names.  LBSIM_ESHAPE if buf_len is too short.  Measurement labels; no reference
+ * counterpart. */
+int lbsim_launch_names(lbsim_t* h, int which, char* buf, size_t buf_len);
 
 /* Snapshot: total bytes of the device state, and copies to/from a HOST buffer of that size.
  * Layout: DESIGN.md §4 (used by the parity tests to compare every state word with oracle/). */

@@ -167,6 +167,7 @@ _SIGNATURES = {
     "lbsim_profile_begin": (ctypes.c_int, [_P, ctypes.c_int]),
     "lbsim_profile_end": (ctypes.c_int, [_P, _P, _P]),
     "lbsim_profile_end_ex": (ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
+    "lbsim_launch_names": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),
     "lbsim_state_size": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_size_t)]),
     "lbsim_get_state": (ctypes.c_int, [_P, _P, ctypes.c_size_t]),
     "lbsim_set_state": (ctypes.c_int, [_P, _P, ctypes.c_size_t]),
@@ -201,6 +202,19 @@ def load() -> ctypes.CDLL:
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def launch_names(handle, which: int = 0) -> dict:
+    """{profile class: kernel signature} of the last step (which=0) / reset (1) of a Handle
+    (lbsim_launch_names), e.g. {0: 'dynamics_group_kernel<4, 0, 0, false, 1>', 1: ...}."""
+    buf = ctypes.create_string_buffer(4096)
+    check(load().lbsim_launch_names(handle.h, which, buf, len(buf)), handle.h)
+    out = {}
+    for item in buf.value.decode().split(";"):
+        if item:
+            cls, name = item.split("=", 1)
+            out[int(cls)] = name
+    return out
 
 
 def default_config() -> LbsimConfig:

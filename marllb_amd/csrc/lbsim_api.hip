@@ -5,6 +5,8 @@
 // happens inside lbsim_reset / lbsim_step, so a caller may capture them into a hipGraph.
 #include <hip/hip_runtime.h>
 
+#include <cxxabi.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
@@ -22,6 +24,25 @@
 #include "lbsim_vpp.h"
 
 using namespace lbk;
+
+// The launch log of LBSIM_LAUNCH (lbsim_internal.h): (profile class, host stub) of each kernel
+// the API call in progress launched.  The calls that launch simulator kernels set the class
+// before each launch; a scoped LaunchLog copies the log into the handle when the call returns.
+namespace {
+constexpr int kLogMax = 8;
+thread_local const void* g_log_fn[kLogMax];
+thread_local int g_log_cls[kLogMax];
+thread_local int g_log_n = 0;
+thread_local int g_log_class = -1;
+}  // namespace
+
+void lbk::note_launch(const void* host_fn) {
+  if (g_log_n < kLogMax) {
+    g_log_fn[g_log_n] = host_fn;
+    g_log_cls[g_log_n] = g_log_class;
+    ++g_log_n;
+  }
+}
 
 struct Profiler {
   bool on = false;
@@ -49,6 +70,8 @@ struct lbsim {
   unsigned long long* stats_buf = nullptr;  // lbsim_step_stats sums (2 x u64)
   bool initialised;  // a full reset has been issued
   std::string err;
+  // (class, host stub) of the kernels the last lbsim_step_ex / lbsim_reset_ex launched
+  std::vector<std::pair<int, const void*>> launched[2];
 };
 
 namespace {
@@ -237,6 +260,7 @@ struct ProfScope {
   hipStream_t s;
   bool rec = false;
   ProfScope(lbsim_t* h_, hipStream_t s_, int cls) : h(h_), s(s_) {
+    g_log_class = cls;  // the launch log's class of the kernel launched in this scope
     Profiler& p = h->prof;
     if (!p.on) return;
     if (p.chain_ev >= 0 && p.used + 1 <= p.cap) {
@@ -258,6 +282,45 @@ struct ProfScope {
     ++p.used;
   }
 };
+
+// Scope of one lbsim_step_ex (which = 0) / lbsim_reset_ex (1): the launch log starts empty and
+// is kept in the handle when the call returns (lbsim_launch_names).
+struct LaunchLog {
+  lbsim_t* h;
+  int which;
+  LaunchLog(lbsim_t* h_, int w) : h(h_), which(w) { g_log_n = 0; }
+  ~LaunchLog() {
+    auto& v = h->launched[which];
+    v.clear();
+    for (int i = 0; i < g_log_n; ++i) v.emplace_back(g_log_cls[i], g_log_fn[i]);
+    g_log_n = 0;
+    g_log_class = -1;
+  }
+};
+
+// "void lbk::observe_kernel<4, 0, false>(lbk::DevState, ...)" -> "observe_kernel<4, 0, false>":
+// the form tools/pmc_traffic.py and tools/pmc_valu.py key their counter files by.
+std::string short_kernel_name(const char* raw) {
+  std::string s = raw ? raw : "?";
+  int st = 0;
+  if (char* d = abi::__cxa_demangle(s.c_str(), nullptr, nullptr, &st)) {
+    if (st == 0) s = d;
+    free(d);
+  }
+  int depth = 0;  // cut the parameter list: the first '(' outside template brackets
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '<') ++depth;
+    else if (s[i] == '>') --depth;
+    else if (s[i] == '(' && depth == 0 && s.compare(i, 21, "(anonymous namespace)") != 0) {
+      s.resize(i);
+      break;
+    }
+  }
+  for (const char* pre : {"void ", "lbk::", "(anonymous namespace)::"}) {
+    for (size_t at; (at = s.find(pre)) != std::string::npos;) s.erase(at, strlen(pre));
+  }
+  return s;
+}
 
 LaunchCtx ctx(const lbsim_t* h) {
   return LaunchCtx{h->st, h->prm, h->B, h->S, h->simds, h->cfg.dyn_mapping};
@@ -501,6 +564,7 @@ int lbsim_reset_ex(lbsim_t* h, const uint8_t* env_mask, const lbsim_step_outputs
   if (h->prm.trace && h->prm.trace_rows == 0)
     return fail(h, LBSIM_EINVAL, "arrival_source TRACE: call lbsim_set_trace before lbsim_reset");
   DeviceGuard g(h->device);
+  LaunchLog log(h, 1);
   const hipStream_t s = (hipStream_t)stream;
   int rc = launch_dynamics(h, nullptr, 0, nullptr, env_mask, kModeReset, s);
   if (rc != LBSIM_OK) return rc;
@@ -541,6 +605,7 @@ int lbsim_step_ex(lbsim_t* h, const void* action, int action_dtype,
   if (facade_bad(h, out)) return fail(h, LBSIM_EINVAL, "agent_obs / state need num_agents * "
                                                        "servers_per_agent == num_servers");
   DeviceGuard g(h->device);
+  LaunchLog log(h, 0);
   const hipStream_t s = (hipStream_t)stream;
   const ObsOutputs o = obs_outputs(out, false);
   if (use_step_wave(h)) {
@@ -954,6 +1019,22 @@ int lbsim_profile_end_ex(lbsim_t* h, double* ms_out, int64_t* count_out, int n_c
     if (ms_out) ms_out[i] = ms[i];
     if (count_out) count_out[i] = cnt[i];
   }
+  return LBSIM_OK;
+}
+
+int lbsim_launch_names(lbsim_t* h, int which, char* buf, size_t buf_len) {
+  if (h == nullptr || which < 0 || which > 1 || buf == nullptr || buf_len == 0)
+    return LBSIM_EINVAL;
+  DeviceGuard g(h->device);
+  std::string txt;
+  for (const auto& [cls, fn] : h->launched[which]) {
+    const char* raw = hipKernelNameRefByPtr(fn, nullptr);
+    if (!txt.empty()) txt += ';';
+    txt += std::to_string(cls) + "=" + short_kernel_name(raw);
+  }
+  if (txt.size() + 1 > buf_len)
+    return fail(h, LBSIM_ESHAPE, "launch names need %zu bytes", txt.size() + 1);
+  memcpy(buf, txt.c_str(), txt.size() + 1);
   return LBSIM_OK;
 }
 

@@ -20,10 +20,10 @@ void launch_dyn(const LaunchCtx& L, const void* action, int dtype, int32_t* assi
   constexpr unsigned epb = 64u * kDynWaves<MAXS>;  // envs per workgroup (one per CU, kDynWaves)
   const dim3 block(epb), grid((unsigned)((L.B + epb - 1) / epb));
   if (L.prm.trace)
-    hipLaunchKernelGGL((dynamics_kernel<MAXS, MODE, POLICY, true>), grid, block, 0, stream, L.st,
+    LBSIM_LAUNCH((dynamics_kernel<MAXS, MODE, POLICY, true>), grid, block, 0, stream, L.st,
                        L.prm, action, dtype, assign, mask);
   else
-    hipLaunchKernelGGL((dynamics_kernel<MAXS, MODE, POLICY, false>), grid, block, 0, stream, L.st,
+    LBSIM_LAUNCH((dynamics_kernel<MAXS, MODE, POLICY, false>), grid, block, 0, stream, L.st,
                        L.prm, action, dtype, assign, mask);
 }
 
@@ -37,19 +37,19 @@ void launch_dyn_group(const LaunchCtx& L, const void* action, int dtype, int32_t
   if constexpr (MODE == kModeStep && POLICY == 0 && (G == 4 || G == 8)) {
     if ((int64_t)grid.x > 4 * (int64_t)L.simds) {
       if (L.prm.trace)
-        hipLaunchKernelGGL((dynamics_group_kernel<G, MODE, POLICY, true, 5>), grid, block, 0,
+        LBSIM_LAUNCH((dynamics_group_kernel<G, MODE, POLICY, true, 5>), grid, block, 0,
                            stream, L.st, L.prm, action, dtype, assign, mask);
       else
-        hipLaunchKernelGGL((dynamics_group_kernel<G, MODE, POLICY, false, 5>), grid, block, 0,
+        LBSIM_LAUNCH((dynamics_group_kernel<G, MODE, POLICY, false, 5>), grid, block, 0,
                            stream, L.st, L.prm, action, dtype, assign, mask);
       return;
     }
   }
   if (L.prm.trace)
-    hipLaunchKernelGGL((dynamics_group_kernel<G, MODE, POLICY, true>), grid, block, 0, stream,
+    LBSIM_LAUNCH((dynamics_group_kernel<G, MODE, POLICY, true>), grid, block, 0, stream,
                        L.st, L.prm, action, dtype, assign, mask);
   else
-    hipLaunchKernelGGL((dynamics_group_kernel<G, MODE, POLICY, false>), grid, block, 0, stream,
+    LBSIM_LAUNCH((dynamics_group_kernel<G, MODE, POLICY, false>), grid, block, 0, stream,
                        L.st, L.prm, action, dtype, assign, mask);
 }
 
@@ -85,10 +85,10 @@ void launch_dyn_wave(const LaunchCtx& L, const void* action, int dtype, int32_t*
                      const uint8_t* mask, hipStream_t stream) {
   const dim3 block(64), grid((unsigned)L.B);
   if (L.prm.trace)
-    hipLaunchKernelGGL((dynamics_wave_kernel<NR, MODE, POLICY, true>), grid, block, 0, stream,
+    LBSIM_LAUNCH((dynamics_wave_kernel<NR, MODE, POLICY, true>), grid, block, 0, stream,
                        L.st, L.prm, action, dtype, assign, mask);
   else
-    hipLaunchKernelGGL((dynamics_wave_kernel<NR, MODE, POLICY, false>), grid, block, 0, stream,
+    LBSIM_LAUNCH((dynamics_wave_kernel<NR, MODE, POLICY, false>), grid, block, 0, stream,
                        L.st, L.prm, action, dtype, assign, mask);
 }
 

@@ -391,6 +391,12 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
       key = adj ? k1 : k0;
       score = adj ? sc1 : sc0;
     } while (++bi < lim);
+    if (seq == (1u << 26)) {  // the 26-bit flush tag would wrap: older maxima in `own` would win
+      wave_sync();
+      for (int i = 0; i < kWaveMaxS * 128 / 64; ++i) Ld.own[i * 64 + lane] = 0u;
+      wave_sync();
+      seq = 1u;
+    }
     wave_flush(p, V, E, Bt, bi, lane, res_b, Ld, seq++, base_ms, base_rem);
     ta = rdl(Bt.ta, bi);
     if (ta >= dt) break;

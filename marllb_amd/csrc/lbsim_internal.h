@@ -18,6 +18,17 @@
 
 namespace lbk {
 
+// Launch log: every kernel launch of the library goes through LBSIM_LAUNCH, which records the
+// launched kernel's host stub for the API call in progress (lbsim_launch_names resolves the stubs
+// to their names afterwards, off the step path).  bench.py keys its committed PMC counter files by
+// these names, so counters of a kernel that did not run are never attached to a measurement.
+void note_launch(const void* host_fn);
+#define LBSIM_LAUNCH(KERNEL, GRID, BLOCK, LDS, STREAM, ...)                 \
+  do {                                                                    \
+    ::lbk::note_launch(reinterpret_cast<const void*>(&KERNEL));           \
+    hipLaunchKernelGGL(KERNEL, GRID, BLOCK, LDS, STREAM, __VA_ARGS__);    \
+  } while (0)
+
 // What a launcher needs of a handle.
 struct LaunchCtx {
   DevState st;

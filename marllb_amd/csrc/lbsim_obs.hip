@@ -18,16 +18,16 @@ void launch_observe_t(const LaunchCtx& L, const ObsOutputs& o, const uint8_t* ma
     (void)ok;
   }
   if (L.S <= 4)
-    hipLaunchKernelGGL((observe_kernel<4, MODE, FAC>), grid, block, lds, stream, L.st, L.prm, o,
+    LBSIM_LAUNCH((observe_kernel<4, MODE, FAC>), grid, block, lds, stream, L.st, L.prm, o,
                        mask);
   else if (L.S <= 8)
-    hipLaunchKernelGGL((observe_kernel<8, MODE, FAC>), grid, block, lds, stream, L.st, L.prm, o,
+    LBSIM_LAUNCH((observe_kernel<8, MODE, FAC>), grid, block, lds, stream, L.st, L.prm, o,
                        mask);
   else if (L.S <= 16)
-    hipLaunchKernelGGL((observe_kernel<16, MODE, FAC>), grid, block, lds, stream, L.st, L.prm, o,
+    LBSIM_LAUNCH((observe_kernel<16, MODE, FAC>), grid, block, lds, stream, L.st, L.prm, o,
                        mask);
   else
-    hipLaunchKernelGGL((observe_kernel<64, MODE, FAC>), grid, block, lds, stream, L.st, L.prm, o,
+    LBSIM_LAUNCH((observe_kernel<64, MODE, FAC>), grid, block, lds, stream, L.st, L.prm, o,
                        mask);
 }
 
@@ -41,10 +41,10 @@ void launch_observe_m(const LaunchCtx& L, const ObsOutputs& o, const uint8_t* ma
         block(64 * kObsResetEnvs);
     const size_t lds = kObsResetEnvs * sizeof(ObsScratch);
     if (fac)
-      hipLaunchKernelGGL(observe_reset_kernel<true>, grid, block, lds, stream, L.st, L.prm, o,
+      LBSIM_LAUNCH(observe_reset_kernel<true>, grid, block, lds, stream, L.st, L.prm, o,
                          mask);
     else
-      hipLaunchKernelGGL(observe_reset_kernel<false>, grid, block, lds, stream, L.st, L.prm, o,
+      LBSIM_LAUNCH(observe_reset_kernel<false>, grid, block, lds, stream, L.st, L.prm, o,
                          mask);
     return;
   }

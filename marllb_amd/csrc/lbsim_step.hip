@@ -76,17 +76,25 @@ void launch_wo(const LaunchCtx& L, const void* action, int dtype, int32_t* assig
                const ObsOutputs& o, hipStream_t s) {
   const dim3 block(64), grid((unsigned)L.B);
   if (L.prm.trace)
-    hipLaunchKernelGGL((step_wave_kernel<NG, POLICY, true, OCC>), grid, block, 0, s, L.st, L.prm,
+    LBSIM_LAUNCH((step_wave_kernel<NG, POLICY, true, OCC>), grid, block, 0, s, L.st, L.prm,
                        action, dtype, assign, o);
   else
-    hipLaunchKernelGGL((step_wave_kernel<NG, POLICY, false, OCC>), grid, block, 0, s, L.st,
+    LBSIM_LAUNCH((step_wave_kernel<NG, POLICY, false, OCC>), grid, block, 0, s, L.st,
                        L.prm, action, dtype, assign, o);
 }
 
+// OCC 2 up to 2 envs per SIMD, else 4; LBSIM_STEP_WAVE_OCC = 2 | 4 forces one form at every
+// batch size (the parity tests run the OCC-4 kernel that serves 2-4 envs per SIMD -- BASELINE
+// configs[1]'s 4096 x 4 -- on every small-batch case).
 template <int NG, int POLICY>
 void launch_w(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
               const ObsOutputs& o, hipStream_t s) {
-  if ((int64_t)L.B <= 2 * (int64_t)L.simds) launch_wo<NG, POLICY, 2>(L, action, dtype, assign, o, s);
+  static const int forced = [] {
+    const char* e = std::getenv("LBSIM_STEP_WAVE_OCC");
+    return e ? std::atoi(e) : 0;
+  }();
+  const bool occ2 = forced == 2 || (forced != 4 && (int64_t)L.B <= 2 * (int64_t)L.simds);
+  if (occ2) launch_wo<NG, POLICY, 2>(L, action, dtype, assign, o, s);
   else launch_wo<NG, POLICY, 4>(L, action, dtype, assign, o, s);
 }
 
@@ -107,10 +115,10 @@ void launch_g(const LaunchCtx& L, const void* action, int dtype, int32_t* assign
   constexpr int MAXS = G < 4 ? 4 : G;
   const dim3 block(64), grid((unsigned)((L.B + 64 / G - 1) / (64 / G)));
   if (L.prm.trace)
-    hipLaunchKernelGGL((fused_step_kernel<G, MAXS, POLICY, true>), grid, block, 0, s, L.st, L.prm,
+    LBSIM_LAUNCH((fused_step_kernel<G, MAXS, POLICY, true>), grid, block, 0, s, L.st, L.prm,
                        action, dtype, assign, o);
   else
-    hipLaunchKernelGGL((fused_step_kernel<G, MAXS, POLICY, false>), grid, block, 0, s, L.st,
+    LBSIM_LAUNCH((fused_step_kernel<G, MAXS, POLICY, false>), grid, block, 0, s, L.st,
                        L.prm, action, dtype, assign, o);
 }
 

@@ -596,6 +596,11 @@ class LoadBalanceEnv:
         if not v._reset_done:  # e.g. SHM mode whose reset came from a frame
             v.reset()
         io = self._io if self._io is not None else self._io_buffers()
+        cur = _torch().cuda.current_stream(v.device)
+        if cur.cuda_stream != io[7].value:
+            # the caller switched streams since the buffers were made: launch on the current one,
+            # so the step stays ordered after a reset() / _upstream issued on it
+            io = self._io = io[:6] + (cur, ctypes.c_void_p(cur.cuda_stream)) + io[8:]
         hview, aview, stream, sptr, dt, n, aptr, outref = (io[1], io[3], io[6], io[7], io[8],
                                                            io[9], io[10], io[11])
         aview[:] = idx_or_w

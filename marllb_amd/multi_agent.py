@@ -141,12 +141,13 @@ class VecMultiAgentLoadBalanceEnv:
         self.lib = _lib.load()
         self._state = None  # the state the last step / reset launch wrote (get_state)
 
-    def agent_obs(self, obs):
-        """(B, S, 11) -> (B, A, 4k + 7S) by lbsim_agent_obs."""
+    def agent_obs(self, obs, out=None):
+        """(B, S, 11) -> (B, A, 4k + 7S) by lbsim_agent_obs (into `out` when given)."""
         torch = _torch()
         obs = obs.contiguous()
-        out = torch.empty((obs.shape[0], self.num_agents, self.obs_dim), dtype=torch.float32,
-                          device=self.device)
+        if out is None:
+            out = torch.empty((obs.shape[0], self.num_agents, self.obs_dim), dtype=torch.float32,
+                              device=self.device)
         stream = torch.cuda.current_stream(self.device).cuda_stream
         self.vec.handle.check(self.lib.lbsim_agent_obs(
             ctypes.c_void_p(obs.data_ptr()), obs.shape[0], self.S, self.num_agents, self.k,
@@ -181,8 +182,12 @@ class VecMultiAgentLoadBalanceEnv:
         f = self._facade(mask is not None)
         obs = self.vec.reset(mask=mask, facade=f)
         ao = f[2]
-        if mask is not None and not self.vec.graph_mode:  # rows of envs not reset: their last
-            ao = self.agent_obs(obs)                       # agent observations
+        if self.vec.feature_mode == "upstream":
+            # the launch wrote agent_obs from problem-01 rows; _upstream then replaced columns
+            # 1-10 of obs: the agent observations follow the returned rows
+            ao = self.agent_obs(obs, out=ao)
+        elif mask is not None and not self.vec.graph_mode:  # rows of envs not reset: their last
+            ao = self.agent_obs(obs)                         # agent observations
         self._state = f[3]
         return ao
 
@@ -197,6 +202,9 @@ class VecMultiAgentLoadBalanceEnv:
         f = self._facade(False)
         obs, rew, done, info = v.step(self.expand_actions(actions), raw_obs=need_raw, facade=f)
         self._state = f[3]  # written by the step launch (and the auto-reset launch's rows)
+        ao = f[2]
+        if v.feature_mode == "upstream":  # as in reset(): the rows step() returns
+            ao = self.agent_obs(obs, out=ao)
         loads = (info["raw_obs"] if need_raw else obs)[:, :, 0]
         info = dict(info)
         info["server_loads"] = loads
@@ -207,7 +215,7 @@ class VecMultiAgentLoadBalanceEnv:
             s, sq = l.sum(2), (l * l).sum(2)
             rewards = torch.where(s == 0, torch.zeros_like(s),
                                   s * s / (self.k * sq + 1e-8)).float()
-        return f[2], rewards, done, info
+        return ao, rewards, done, info
 
     def get_state(self):
         """(B, 4S + 10): written by the last step / reset launch into a tensor of its own, never

@@ -250,30 +250,21 @@ def _compare_state(h_gpu, ora, B, S, Q, norm):
     np.testing.assert_array_equal(statelayout.live_ring(g, B, S, Q), statelayout.live_ring(o, B, S, Q))
 
 
-@pytest.mark.parametrize("mapping", ["env", "server", "server-fused"])
-@pytest.mark.parametrize("case", range(len(CONFIGS)))
-def test_simulator_bit_exact_vs_oracle(lib, oracle_mod, case, mapping):
-    """Both dynamics mappings (one lane per env / one lane per server) against the oracle; the
-    server mapping both as two launches (the default) and as the fused step kernel (S <= 16)."""
+def _run_vs_oracle(oracle_mod, B, S, kw, akw, case, mapping="auto", steps=12, post_steps=4,
+                   threads=4, autoreset=False):
+    """Step a VecLoadBalanceEnv and the oracle side by side from the same seeds: observations,
+    rewards, done and per-server assignment counts every step, the full device state word for word
+    after `steps` steps and again after a masked reset of every third env and `post_steps` more
+    steps.  Returns the env (open) for further checks."""
     from marllb_amd.env import VecLoadBalanceEnv, make_config
-    c = CONFIGS[case]
-    B, S, kw = c["B"], c["S"], resolve_kw(c["kw"])
-    if mapping == "server-fused":
-        mapping, kw["step_kernel"] = "server", "fused"
-    if mapping == "env" and S > 16:
-        with pytest.raises(ValueError, match="at most 16 servers"):
-            VecLoadBalanceEnv(B, S, device="cuda:0", dyn_mapping=mapping, **kw)
-        return
-    kw.setdefault("seed", 1000 + case)
-    akw = dict(c["kw"])  # action options (incl. test-only '_' keys)
-    env = VecLoadBalanceEnv(B, S, device="cuda:0", autoreset=False, dyn_mapping=mapping, **kw)
-    ora = oracle_mod.OracleEnv(make_config(B, S, **kw), threads=4, trace=kw.get("trace"))
+    env = VecLoadBalanceEnv(B, S, device="cuda:0", autoreset=autoreset, dyn_mapping=mapping, **kw)
+    ora = oracle_mod.OracleEnv(make_config(B, S, **kw), threads=threads, trace=kw.get("trace"))
     Q, norm = env.cfg.queue_capacity, bool(env.cfg.normalize_obs)
     obs_g = env.reset().cpu().numpy()
     obs_o = ora.reset()
     np.testing.assert_array_equal(obs_g, obs_o)
     rng = np.random.default_rng(case)
-    for k in range(12):
+    for k in range(steps):
         a = _actions(rng, B, S, akw)
         og, rg, dg, info = env.step(torch.from_numpy(a), assign_counts=True)
         oo, ro, do, ao = ora.step(a)
@@ -287,14 +278,112 @@ def test_simulator_bit_exact_vs_oracle(lib, oracle_mod, case, mapping):
     og = env.reset(mask=torch.from_numpy(mask)).cpu().numpy()
     oo = ora.reset(mask=mask, obs=og.copy())
     np.testing.assert_array_equal(og, oo)
-    for k in range(4):
+    for k in range(post_steps):
         a = _actions(rng, B, S, akw)
         og, rg, dg, _ = env.step(torch.from_numpy(a))
         oo, ro, do, _ = ora.step(a)
         np.testing.assert_array_equal(og.cpu().numpy(), oo)
         np.testing.assert_array_equal(rg.cpu().numpy(), ro)
     _compare_state(env.handle, ora, B, S, Q, norm)
+    ora.close()
+    return env
+
+
+@pytest.mark.parametrize("mapping", ["env", "server", "server-fused"])
+@pytest.mark.parametrize("case", range(len(CONFIGS)))
+def test_simulator_bit_exact_vs_oracle(lib, oracle_mod, case, mapping):
+    """Both dynamics mappings (one lane per env / one lane per server) against the oracle; the
+    server mapping both as two launches (the default) and as the fused step kernel (S <= 16)."""
+    from marllb_amd.env import VecLoadBalanceEnv
+    c = CONFIGS[case]
+    B, S, kw = c["B"], c["S"], resolve_kw(c["kw"])
+    if mapping == "server-fused":
+        mapping, kw["step_kernel"] = "server", "fused"
+    if mapping == "env" and S > 16:
+        with pytest.raises(ValueError, match="at most 16 servers"):
+            VecLoadBalanceEnv(B, S, device="cuda:0", dyn_mapping=mapping, **kw)
+        return
+    kw.setdefault("seed", 1000 + case)
+    env = _run_vs_oracle(oracle_mod, B, S, kw, dict(c["kw"]), case, mapping)
     env.close()
+
+
+def _simds():
+    return 4 * torch.cuda.get_device_properties(0).multi_processor_count
+
+
+def _expected_step_kernels(B, S, simds):
+    """The default dispatch (lbsim_api.hip use_step_wave, lbsim_internal.h dyn_wave_ok /
+    dyn_group_lanes, lbsim_step.hip launch_w) of a SED, Poisson, Q = 32 handle: {profile class:
+    kernel-name prefix} of one step."""
+    wave = B <= (4 if S <= 4 else 2) * simds
+    if wave and S <= 4:
+        ng = 1 if S <= 2 else 2
+        occ = 2 if B <= 2 * simds else 4
+        return {4: f"step_wave_kernel<{ng}, 0, false, {occ}>"}
+    if wave:
+        ng = 1 if S <= 2 else 2 if S <= 4 else 4
+        return {0: f"dynamics_wave_kernel<{ng}, 0, 0, false>", 1: "observe_kernel<"}
+    g = 2 if S <= 2 else (8 if B * 4 // 64 <= simds // 2 else 4) if S <= 4 else 8 if S <= 8 else 16
+    return {0: f"dynamics_group_kernel<{g}, 0, 0, false", 1: "observe_kernel<"}
+
+
+def test_configs1_default_dispatch_4096x4(lib, oracle_mod):
+    """BASELINE configs[1] as it runs by default: VecLoadBalanceEnv(4096, 4) with no override
+    (on 256 CUs the one-launch step_wave_kernel at 4 waves per SIMD), every env against the
+    oracle step by step and the full device state word for word (env.py:215-286,
+    reservoir.py:50-196)."""
+    from marllb_amd import _lib
+    B, S = 4096, 4
+    kw = {"seed": 4096}
+    env = _run_vs_oracle(oracle_mod, B, S, kw, {}, 77, threads=8)
+    names = _lib.launch_names(env.handle)
+    for cls, pfx in _expected_step_kernels(B, S, _simds()).items():
+        assert names.get(cls, "").startswith(pfx), (names, pfx)
+    env.close()
+
+
+@pytest.mark.parametrize("S,where", [(4, "2s"), (4, "2s+1"), (4, "4s"), (4, "4s+1"),
+                                     (8, "2s"), (8, "2s+1")])
+def test_dispatch_boundaries_bit_exact(lib, oracle_mod, S, where):
+    """Batches at the dispatch boundaries of the default step (in envs per SIMD of this device):
+    S = 4 at 2 and 4 envs per SIMD (step_wave_kernel OCC 2 -> OCC 4 -> server-per-lane groups),
+    S = 8 at 2 envs per SIMD (dynamics_wave_kernel -> groups).  The kernel that ran is checked by
+    name (lbsim_launch_names), the results against the oracle on every env."""
+    from marllb_amd import _lib
+    simds = _simds()
+    k, plus = (2, 0) if where == "2s" else (2, 1) if where == "2s+1" else (4, 0) if where == "4s" else (4, 1)
+    B = k * simds + plus
+    kw = {"seed": 500 + B + S, "assign_policy": "sed"}
+    env = _run_vs_oracle(oracle_mod, B, S, kw, {}, B + S, steps=6, post_steps=2, threads=8)
+    names = _lib.launch_names(env.handle)
+    for cls, pfx in _expected_step_kernels(B, S, simds).items():
+        assert names.get(cls, "").startswith(pfx), (B, S, names, pfx)
+    env.close()
+
+
+@pytest.mark.parametrize("occ", ["2", "4"])
+def test_step_wave_occupancy_forms_bit_exact(occ):
+    """LBSIM_STEP_WAVE_OCC forces one occupancy form of the one-launch step_wave_kernel at every
+    batch size, so each simulator case the default dispatch sends to it (S <= 4, Q <= 32, not
+    ALIAS, B <= 4 envs per SIMD: SED2, LSQ, LSQ2, trace arrivals, continuous and NaN actions, full
+    rings, normalisation off) runs on the OCC-4 form that serves 2-4 envs per SIMD -- BASELINE
+    configs[1]'s 4096 x 4 -- and on the OCC-2 form.  Child process (read once per process)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ks = [f"test_simulator_bit_exact_vs_oracle[{c}-{m}]" for c in range(len(CONFIGS))
+          for m in ("server", "server-fused")
+          if CONFIGS[c]["S"] <= 4 and CONFIGS[c]["B"] <= 4096
+          and CONFIGS[c]["kw"].get("queue_capacity", 32) <= 32
+          and CONFIGS[c]["kw"].get("assign_policy") != "alias"]
+    assert len(ks) >= 20
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p",
+                        "no:cacheprovider"] +
+                       [os.path.join(root, "tests", "test_gpu_parity.py") + "::" + k for k in ks],
+                       cwd=root, env={**os.environ, "LBSIM_STEP_WAVE_OCC": occ},
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
 
 
 @pytest.mark.parametrize("lanes", ["4", "8", "16"])
@@ -450,12 +539,17 @@ def test_full_size_trace_replay_c3(lib, oracle_mod):
 
 def test_dynamics_kernel_dispatch(lib):
     """lbsim_dynamics_kernel names the kernel the launches use: one wave per env for small S <= 8
-    batches (at most 4 envs per SIMD, queue capacity <= 32, not ALIAS), server-per-lane groups
-    otherwise, one lane per env when asked for."""
+    batches (at most 4 envs per SIMD for S <= 4, 2 for S <= 8, queue capacity <= 32, not ALIAS),
+    server-per-lane groups otherwise, one lane per env when asked for.  The batch limits are in
+    envs per SIMD of this device (dyn_wave_ok's rule), not a 256-CU constant."""
     from marllb_amd.env import VecLoadBalanceEnv
+    simds = _simds()
     cases = [(dict(num_envs=257, num_servers=4), 2), (dict(num_envs=1, num_servers=4), 2),
-             (dict(num_envs=8256, num_servers=4), 1), (dict(num_envs=64, num_servers=8), 2),
-             (dict(num_envs=4096, num_servers=4), 2), (dict(num_envs=4096, num_servers=8), 1),
+             (dict(num_envs=4 * simds + 1, num_servers=4), 1),
+             (dict(num_envs=64, num_servers=8), 2),
+             (dict(num_envs=4 * simds, num_servers=4), 2),
+             (dict(num_envs=2 * simds, num_servers=8), 2),
+             (dict(num_envs=2 * simds + 1, num_servers=8), 1),
              (dict(num_envs=64, num_servers=16), 1),
              (dict(num_envs=64, num_servers=4, assign_policy="alias"), 1),
              (dict(num_envs=64, num_servers=4, queue_capacity=64), 1),

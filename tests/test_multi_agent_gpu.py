@@ -124,22 +124,29 @@ def test_vec_terminal_step_local_rewards():
 
 
 @pytest.mark.parametrize("step_kernel", ["fused", "split"])
-@pytest.mark.parametrize("normalize", [False, True])
-def test_step_launch_writes_agent_obs_and_state(step_kernel, normalize):
+@pytest.mark.parametrize("normalize,feature_mode", [(False, "problem01"), (True, "problem01"),
+                                                    (False, "upstream")])
+def test_step_launch_writes_agent_obs_and_state(step_kernel, normalize, feature_mode):
     """The (B, A, 4k + 7S) agent observations and the (B, 74) state come from the step / reset
     launches themselves (lbsim_step_outputs_t agent_obs / state): equal to lbsim_agent_obs on the
-    returned rows and to zeros ++ [step / max_steps, A], across the auto-reset boundary."""
+    returned rows and to zeros ++ [step / max_steps, A], across the auto-reset boundary and a
+    masked reset.  feature_mode='upstream' replaces columns 1-10 of the returned rows after the
+    launch (shm_proxy.py process_reservoir): the agent observations follow those rows."""
     from marllb_amd import VecMultiAgentLoadBalanceEnv
     B, A, k, T = 96, 4, 4, 3
     env = VecMultiAgentLoadBalanceEnv(B, A, k, device="cuda:0", seed=21, action_type="discrete",
                                       max_steps=T, normalize_obs=normalize,
-                                      step_kernel=step_kernel)
+                                      step_kernel=step_kernel, feature_mode=feature_mode)
     ao = env.reset()
     ep = torch.zeros(B, dtype=torch.int32, device="cuda:0")
     g = torch.Generator(device="cuda:0")
     g.manual_seed(4)
-    for t in range(2 * T + 1):
-        if t > 0:
+    for t in range(2 * T + 2):
+        if t == T + 1:  # a masked reset of every other env
+            mask = (torch.arange(B, device="cuda:0") % 2 == 0)
+            ao = env.reset(mask=mask)
+            ep = torch.where(mask, torch.zeros_like(ep), ep)
+        elif t > 0:
             a = torch.randint(0, 3, (B, A), device="cuda:0", generator=g)
             ao, _, done, info = env.step(a)
             ep = torch.where(done, torch.zeros_like(ep), info["episode_length"])
@@ -150,4 +157,9 @@ def test_step_launch_writes_agent_obs_and_state(step_kernel, normalize):
         want[:, 72] = ep.float() / float(T)
         want[:, 73] = float(A)
         assert torch.equal(st, want), t
+    if feature_mode == "upstream":  # the rows really are the upstream features
+        ref = VecMultiAgentLoadBalanceEnv(B, A, k, device="cuda:0", seed=21,
+                                          action_type="discrete", max_steps=T)
+        assert not torch.equal(ref.reset(), env.reset())
+        ref.close()
     env.close()

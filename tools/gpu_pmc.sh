@@ -9,7 +9,7 @@ mkdir -p $O
 cd $R
 timeout -k 10 300 ./tools/ubench_valu > $O/ubench_valu.jsonl 2> $O/ubench_valu.err || exit 9
 cd /tmp && export TMPDIR=/tmp
-B="$R/bench.py --no-cpu-baseline --steps 6 --warmup 2 $@"
+B="$R/bench.py --no-cpu-baseline --no-graph --prewarm-ms 0 --steps 20 --warmup 5 $@"
 P="timeout -s KILL 240 rocprofv3"
 $P --pmc FETCH_SIZE -d $O/fetch -o run --output-format csv -- python3 $B > $O/fetch.log 2>&1 &&
 $P --pmc WRITE_SIZE -d $O/write -o run --output-format csv -- python3 $B > $O/write.log 2>&1 &&

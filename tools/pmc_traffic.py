@@ -15,14 +15,45 @@ import json
 import os
 
 
+def kernel_key(raw: str) -> str:
+    """rocprofv3's Kernel_Name -> the template signature lbsim_launch_names reports
+    ("observe_kernel<4, 0, false>"): bench.py matches counters to the kernels that ran by it."""
+    k = raw
+    depth = 0
+    for i, ch in enumerate(k):  # cut the parameter list (the first '(' outside <>)
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0 and not k.startswith("(anonymous namespace)", i):
+            k = k[:i]
+            break
+    for pre in ("void ", "lbk::", "(anonymous namespace)::"):
+        k = k.replace(pre, "")
+    return k.strip()
+
+
+def is_step_kernel(k: str) -> bool:
+    """Launches of lbsim_step (reset launches carry the warm-up): MODE is the second template
+    argument of dynamics_group_kernel / dynamics_kernel / dynamics_wave_kernel / observe_kernel;
+    step_wave_kernel and fused_step_kernel are step launches."""
+    name = k.split("<", 1)[0]
+    if name in ("step_wave_kernel", "fused_step_kernel"):
+        return True
+    if name not in ("dynamics_group_kernel", "dynamics_kernel", "dynamics_wave_kernel",
+                    "observe_kernel"):
+        return False
+    targs = [x.strip() for x in k.split("<", 1)[1].rstrip(">").split(",")]
+    return len(targs) > 1 and targs[1] == "0"
+
+
 def load(d, sub):
     agg = collections.defaultdict(list)
     path = os.path.join(d, sub, "run_counter_collection.csv")
     if not os.path.exists(path):
         return agg
     for r in csv.DictReader(open(path)):
-        k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("lbk::", "")
-        agg[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
+        agg[(kernel_key(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
     return agg
 
 
@@ -45,32 +76,22 @@ def main():
     f, w = load(a.dir, "fetch"), load(a.dir, "write")
     sq = {**load(a.dir, "sq1"), **load(a.dir, "sq2")}
     S = a.servers
-    m = 4 if S <= 4 else 8 if S <= 8 else 16
-    g = 2 if S <= 2 else m if S <= 16 else 32 if S <= 32 else 64
-    # step-mode launches: dynamics_group_kernel<G, 0, POLICY, TRACE> (default mapping) or
-    # dynamics_kernel<MAXS, 0, POLICY, TRACE> (env per lane), observe_kernel<MAXS, 0>
-    prefixes = {"dynamics_group_kernel": f"dynamics_group_kernel<{g}, 0",
-                "dynamics_kernel": f"dynamics_kernel<{m}, 0", "observe_kernel": f"observe_kernel<{m}, 0"}
-    prefixes = {n: pfx for n, pfx in prefixes.items()
-                if any(k.startswith(pfx) for k, _ in load(a.dir, "fetch"))}
-
-    def match(agg, prefix):
-        names = sorted({k for k, _ in agg if k.startswith(prefix)})
-        return names[0] if names else prefix
-
-    step = {n: match(load(a.dir, "fetch"), pfx) for n, pfx in prefixes.items()}
+    # every step-mode launch of the run, keyed by its full template signature
+    step = sorted({k for k, _ in f if is_step_kernel(k)})
     out = {"batch": a.batch, "servers": S, "fetch_calibration": fetch_factor,
-           "write_calibration": write_factor, "bytes_per_launch": {}, "detail": {}}
-    for name, kname in step.items():
+           "write_calibration": write_factor, "keys": "full template signature "
+           "(lbsim_launch_names / tools/pmc_traffic.py kernel_key)", "bytes_per_launch": {},
+           "detail": {}}
+    for kname in step:
         rd = mean(f[(kname, "FETCH_SIZE")]) * 1024 / fetch_factor
         wr = mean(w[(kname, "WRITE_SIZE")]) * 1024
-        out["bytes_per_launch"][name] = rd + wr
+        out["bytes_per_launch"][kname] = rd + wr
         det = {"read_bytes": rd, "write_bytes": wr,
                "read_bytes_per_env": rd / a.batch, "write_bytes_per_env": wr / a.batch}
         for (k, c), v in sq.items():
             if k == kname:
                 det[c] = mean(v)
-        out["detail"][name] = det
+        out["detail"][kname] = det
     txt = json.dumps(out, indent=1)
     print(txt)
     if a.out:

@@ -24,6 +24,10 @@ import collections
 import csv
 import json
 import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_traffic import is_step_kernel, kernel_key  # noqa: E402
 
 CLOCK_HZ = 2.4e9  # MI355X peak engine clock (MI355X_MICROARCH.md)
 SIMDS = 1024      # 256 CUs x 4
@@ -46,9 +50,7 @@ def load(d, sub):
     if not os.path.exists(path):
         return agg
     for r in csv.DictReader(open(path)):
-        k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("lbk::", "")
-        k = k.replace("(anonymous namespace)::", "")
-        agg[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
+        agg[(kernel_key(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
     return agg
 
 
@@ -81,19 +83,13 @@ def main():
     agg = {}
     for sub in ("sq1", "sq2", "vc1", "vc2"):
         agg.update(load(a.dir, sub))
-    kernels = sorted({k for k, _ in agg if ("step" in k or "dynamics" in k or "observe" in k)})
+    kernels = sorted({k for k, _ in agg if is_step_kernel(k)})
     out = {"batch": a.batch, "servers": a.servers, "clock_hz": CLOCK_HZ, "simds": SIMDS,
            "ubench_waves_per_simd": a.waves, "ubench_simd_cyc_per_inst": cost, "kernels": {}}
-    for k in kernels:
+    for k in kernels:  # keyed by the full template signature (lbsim_launch_names)
         c = {cn: mean(v) for (kn, cn), v in agg.items() if kn == k}
         if "SQ_INSTS_VALU" not in c:
             continue
-        # step-mode launches only (reset launches carry the warm-up): MODE is the second template
-        # argument of dynamics_group_kernel / dynamics_kernel / observe_kernel
-        if ("dynamics" in k or "observe" in k) and "<" in k:
-            targs = [x.strip() for x in k.split("<", 1)[1].rstrip(">").split(",")]
-            if len(targs) > 1 and targs[1] != "0":
-                continue
         cls = {n: c.get(n, 0.0) for n in PRICE if n != "other"}
         cls["other"] = max(0.0, c["SQ_INSTS_VALU"] - sum(cls.values()))
         cyc = 0.0
