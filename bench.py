@@ -607,7 +607,7 @@ def main():
                              "achieved_GBps": ach, "frac": ach / HBM_PEAK_GBS}
         # the template signature of each kernel the step launched (lbsim_launch_names), the key
         # of the committed PMC counter files
-        ran = _lib.launch_names(handle, 0)
+        ran = _lib.launch_names(handle, 0) if hasattr(lib, "lbsim_launch_names") else {}
         sigs = {names[c]: sig for c, sig in ran.items() if c in names}
         for k in per_kernel:
             per_kernel[k]["signature"] = sigs.get(k)

@@ -197,6 +197,8 @@ def load() -> ctypes.CDLL:
         pass
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in _SIGNATURES.items():
+        if os.environ.get("LBSIM_LIBRARY") and not hasattr(lib, name):
+            continue  # an A/B build of an older ABI: only the entry points it has
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -1271,12 +1271,8 @@ static_assert(kP90Lo == 114 && (kP90Lo & 15) != 15, "p90 pair inside one lane");
 // halves by row_ror:8.  LDS holds the 2^-48 fixed-point weights by slot (gathered after the sort;
 // 0 for empty slots) and, when n < K, the tail values and the sorted keys for the p90 pair.  Same
 // operations in the same order as the general path, so the same bits.
-// Returns false, having written nothing, when a valid slot of the chunk holds a sample >=
-// kPackLimit (the general path's two-pass sort is needed): that test runs on the values this path
-// loads anyway, so a chunk's records are fetched once (no qualification pass), and nothing loaded
-// here is live on the false path.
 template <bool INC, bool FULL>
-__device__ __forceinline__ bool observe_chunk_regs(const DevState& st, const SimParams& p, size_t b,
+__device__ __forceinline__ void observe_chunk_regs(const DevState& st, const SimParams& p, size_t b,
                                                    int s_base, int S, int n_in, ObsScratch& sc,
                                                    float* obs_out, int lane) {
   const size_t srow = b * (size_t)p.S + (size_t)s_base;
@@ -1297,16 +1293,6 @@ __device__ __forceinline__ bool observe_chunk_regs(const DevState& st, const Sim
   for (int q = 0; q < 8; ++q) {
     th[q] = rts[24 * q];
     if constexpr (!FULL) th[q] = 8 * (q + 8 * r) + j < n ? th[q] : 0u;  // empty slots: stale words
-  }
-  bool big;  // a valid sample >= kPackLimit: the results below are not used (checked at the end)
-  {
-    uint32_t vmax = 0;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const uint32_t v = (FULL || 8 * e + j < n) ? key[e] : 0u;  // empty slots: stale words
-      vmax = v > vmax ? v : vmax;
-    }
-    big = __any(act && vmax >= kPackLimit);
   }
   uint32_t tmax = 0;
 #pragma unroll
@@ -1475,10 +1461,6 @@ __device__ __forceinline__ bool observe_chunk_regs(const DevState& st, const Sim
     p90 = (gg >= 0.5f) ? (vb - diff * (1.0f - gg)) : (va + diff * gg);
     if constexpr (FULL) p90 = __uint_as_float(shfl_u32(__float_as_uint(p90), (lane & ~7) | 7));
   }
-  if (big) {  // rare: nothing written but LDS scratch; the general path redoes the chunk
-    wave_sync();
-    return false;
-  }
   // row of server u: lane j < 5 of group r writes feature j of reservoir r; lane 5 of the fct
   // group writes n_flow_on
   if (act) {
@@ -1492,27 +1474,42 @@ __device__ __forceinline__ bool observe_chunk_regs(const DevState& st, const Sim
     }
   }
   wave_sync();
-  return true;
 }
 
 // Chooses observe_chunk_regs for a chunk of simulator state: every reservoir with n >= 8 samples
-// (else false: the general path; reservoirs with n < 8 sum sequentially in numpy).  FULL (all
-// n = K, the steady state) is a wave-uniform choice.  observe_chunk_regs itself declines (false)
-// a chunk holding a sample >= 2^25 - 1 us (the two-pass sort of the general path).
+// and every sample below kPackLimit (else false: the general path; reservoirs with n < 8 sum
+// sequentially in numpy, samples >= 2^25 - 1 us need the two-pass sort).  FULL (all n = K, the
+// steady state) is a wave-uniform choice.
 template <bool INC>
 __device__ __forceinline__ bool observe_chunk_full(const DevState& st, const SimParams& p, size_t b,
                                                    int s_base, int S, ObsScratch& sc,
                                                    float* obs_out, int lane) {
   const size_t srow = b * (size_t)p.S + (size_t)s_base;
-  const int g = lane >> 3, u = g >> 1;
+  const int g = lane >> 3, j = lane & 7, u = g >> 1, r = g & 1;
   const bool act = u < S;
   const size_t sb = srow + (size_t)(act ? u : 0);
   const uint32_t rc = st.res_count[sb];
   const int n = rc < (uint32_t)K ? (int)rc : K;
   if (__any(act && n < 8)) return false;
   const bool full = !__any(act && n < K);
-  if (full) return observe_chunk_regs<INC, true>(st, p, b, s_base, S, K, sc, obs_out, lane);
-  return observe_chunk_regs<INC, false>(st, p, b, s_base, S, n, sc, obs_out, lane);
+  {
+    // qualification pass; its loads are dropped and re-issued (L1/L2 hits) so that no value stays
+    // live across the branch into the general path (which would spill at 96 VGPRs).  Empty slots
+    // (stale words of an earlier episode) are not masked: a stale sample >= 2^25 - 1 us only sends
+    // a partly filled chunk to the general path, which is exact for every input.
+    const uint32_t* rec = reinterpret_cast<const uint32_t*>(st.res + sb * K + (size_t)j);
+    uint32_t vmax = 0;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const uint32_t v = rec[24 * e + r];
+      vmax = v > vmax ? v : vmax;
+    }
+    if (__any(act && vmax >= kPackLimit)) return false;
+    __asm__ volatile("" ::: "memory");
+  }
+  if (full) observe_chunk_regs<INC, true>(st, p, b, s_base, S, K, sc, obs_out, lane);
+  else observe_chunk_regs<INC, false>(st, p, b, s_base, S, n, sc, obs_out, lane);
+  return true;
 }
 
 // The 11-column observation rows (features.py:256-286) of servers [s_base, s_base + S), S <= 4,
