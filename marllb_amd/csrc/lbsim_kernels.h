@@ -2023,6 +2023,39 @@ __global__ void __launch_bounds__(64 * kObsWavesPerEnv<MAXS>, 5)
   observe_outputs<MAXS, MODE, FAC>(st, p, out, b, s_obs, s_act, tid, nthr);
 }
 
+// Wide envs (S > 16: configs[4] read literally, 4 agents x 16 servers), in two launches instead of
+// one workgroup of S / 4 waves per env.  observe_chunks_kernel: one single-wave workgroup per (env,
+// chunk) computes the chunk's raw rows into out.obs; observe_rows_kernel: one wave per env reads
+// the env's rows back and runs observe_outputs (reward, episode words, normalisation, facade).  A
+// 16-wave workgroup holds 16 chunk scratches (125 KB of LDS: one workgroup per CU) and its waves
+// wait for the slowest chunk and for the reward; single-wave chunks schedule like S <= 4 envs.
+// Same routines in the same order: the same bits as observe_kernel.
+template <int MODE>
+__global__ void __launch_bounds__(64, 5)
+    observe_chunks_kernel(DevState st, SimParams p, ObsOutputs out, const uint8_t* reset_mask,
+                          int nchunks) {
+  const size_t b = blockIdx.x / (unsigned)nchunks;
+  const int c = (int)(blockIdx.x - b * (unsigned)nchunks);
+  if (MODE == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
+  __shared__ ObsScratch sc;
+  const int S = p.S, s0 = c * kObsChunk, lane = (int)threadIdx.x;
+  observe_chunk<true, MODE == kModeStep>(st, p, b, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk,
+                                         sc, out.obs + b * (size_t)S * NF, lane);
+}
+
+template <int MAXS, int MODE, bool FAC>
+__global__ void __launch_bounds__(64)
+    observe_rows_kernel(DevState st, SimParams p, ObsOutputs out, const uint8_t* reset_mask) {
+  const size_t b = blockIdx.x;
+  if (MODE == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
+  __shared__ float s_obs[MAXS * NF];
+  __shared__ float s_act[MAXS];
+  const int lane = (int)threadIdx.x, n = p.S * NF;
+  for (int e = lane; e < n; e += 64) s_obs[e] = out.obs[b * (size_t)n + (size_t)e];
+  wave_sync();
+  observe_outputs<MAXS, MODE, FAC>(st, p, out, b, s_obs, s_act, lane, 64);
+}
+
 // observe_kernel's work for env b by ONE wave, its chunks in sequence (fused_step_kernel's second
 // phase).  Same routines, same order: the same bits.
 template <int MAXS>

@@ -31,11 +31,41 @@ void launch_observe_t(const LaunchCtx& L, const ObsOutputs& o, const uint8_t* ma
                        mask);
 }
 
+// Envs of more than LBSIM_OBSERVE_SPLIT_S servers (default 16) observe in two launches
+// (observe_chunks_kernel + observe_rows_kernel) instead of one workgroup of S / 4 waves per env.
+int observe_split_s() {
+  static const int v = [] {
+    const char* e = std::getenv("LBSIM_OBSERVE_SPLIT_S");
+    return e ? std::atoi(e) : 16;
+  }();
+  return v;
+}
+
+template <int MODE, bool FAC>
+void launch_observe_split(const LaunchCtx& L, const ObsOutputs& o, const uint8_t* mask,
+                          hipStream_t stream) {
+  const int nchunks = (L.S + kObsChunk - 1) / kObsChunk;
+  LBSIM_LAUNCH(observe_chunks_kernel<MODE>, dim3((unsigned)((int64_t)L.B * nchunks)), dim3(64), 0,
+               stream, L.st, L.prm, o, mask, nchunks);
+  const dim3 grid((unsigned)L.B), block(64);
+  if (L.S <= 8)
+    LBSIM_LAUNCH((observe_rows_kernel<8, MODE, FAC>), grid, block, 0, stream, L.st, L.prm, o, mask);
+  else if (L.S <= 16)
+    LBSIM_LAUNCH((observe_rows_kernel<16, MODE, FAC>), grid, block, 0, stream, L.st, L.prm, o, mask);
+  else
+    LBSIM_LAUNCH((observe_rows_kernel<64, MODE, FAC>), grid, block, 0, stream, L.st, L.prm, o, mask);
+}
+
 // the problem-05 facade rows (agent_obs / state) come from their own instantiation
 template <int MODE>
 void launch_observe_m(const LaunchCtx& L, const ObsOutputs& o, const uint8_t* mask,
                       hipStream_t stream) {
   const bool fac = o.agent_obs != nullptr || o.state != nullptr;
+  if (L.S > kObsChunk && L.S > observe_split_s()) {
+    if (fac) launch_observe_split<MODE, true>(L, o, mask, stream);
+    else launch_observe_split<MODE, false>(L, o, mask, stream);
+    return;
+  }
   if (MODE == kModeReset && L.S <= kObsChunk) {  // kObsResetEnvs single-wave envs per workgroup
     const dim3 grid((unsigned)((L.B + kObsResetEnvs - 1) / kObsResetEnvs)),
         block(64 * kObsResetEnvs);

@@ -52,35 +52,47 @@ __global__ void __launch_bounds__(64)
 // Both take 118-120 VGPRs with no spill since the one-chunk observe is straight-line code (the
 // chunk loop took 194 and spilled 64 under the 128 cap: profiles/r03o/).  Out of line, the observe
 // phase's call frames went through 1 KB of scratch per lane (0.141 ms).
-template <int NG, int POLICY, bool TRACE, int OCC>
+// MAXS = 8 (S = 5-8, OCC 2 only: the two chunks observed one after the other by the wave take
+// ~190 VGPRs): the wave dynamics' S <= 8 form, then both chunks.
+template <int NG, int POLICY, bool TRACE, int OCC, int MAXS = kObsChunk>
 __global__ void __launch_bounds__(64, OCC)
     step_wave_kernel(DevState st, SimParams p, const void* action, int action_dtype,
                      int32_t* assign_out, ObsOutputs out) {
+  static_assert(MAXS == kObsChunk || OCC == 2, "S > 4 in one launch only at 2 waves per SIMD");
   __shared__ union {
     WaveLds dyn;
     ObsScratch obs;
   } L;
-  __shared__ float s_obs[kObsChunk * NF];
-  __shared__ float s_act[kObsChunk];
+  __shared__ float s_obs[MAXS * NF];
+  __shared__ float s_act[MAXS];
   const int lane = (int)threadIdx.x;
   if (!dyn_wave_env<NG, kModeStep, POLICY, TRACE, OCC == 2>(st, p, action, action_dtype,
                                                             assign_out, nullptr, blockIdx.x, lane,
                                                             L.dyn))
     return;
   __syncthreads();  // state stores complete and visible to this workgroup; LDS reused below
-  observe_env_wave<kObsChunk>(st, p, out, blockIdx.x, L.obs, s_obs, s_act, lane);
+  observe_env_wave<MAXS>(st, p, out, blockIdx.x, L.obs, s_obs, s_act, lane);
 }
 
 template <int NG, int POLICY, int OCC>
 void launch_wo(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
                const ObsOutputs& o, hipStream_t s) {
   const dim3 block(64), grid((unsigned)L.B);
-  if (L.prm.trace)
-    LBSIM_LAUNCH((step_wave_kernel<NG, POLICY, true, OCC>), grid, block, 0, s, L.st, L.prm,
-                       action, dtype, assign, o);
-  else
-    LBSIM_LAUNCH((step_wave_kernel<NG, POLICY, false, OCC>), grid, block, 0, s, L.st,
-                       L.prm, action, dtype, assign, o);
+  if constexpr (NG == 4) {  // S = 5-8 (OCC 2)
+    if (L.prm.trace)
+      LBSIM_LAUNCH((step_wave_kernel<4, POLICY, true, 2, 8>), grid, block, 0, s, L.st, L.prm,
+                   action, dtype, assign, o);
+    else
+      LBSIM_LAUNCH((step_wave_kernel<4, POLICY, false, 2, 8>), grid, block, 0, s, L.st, L.prm,
+                   action, dtype, assign, o);
+  } else {
+    if (L.prm.trace)
+      LBSIM_LAUNCH((step_wave_kernel<NG, POLICY, true, OCC>), grid, block, 0, s, L.st, L.prm,
+                   action, dtype, assign, o);
+    else
+      LBSIM_LAUNCH((step_wave_kernel<NG, POLICY, false, OCC>), grid, block, 0, s, L.st, L.prm,
+                   action, dtype, assign, o);
+  }
 }
 
 // OCC 2 up to 2 envs per SIMD, else 4; LBSIM_STEP_WAVE_OCC = 2 | 4 forces one form at every
@@ -93,7 +105,7 @@ void launch_w(const LaunchCtx& L, const void* action, int dtype, int32_t* assign
     const char* e = std::getenv("LBSIM_STEP_WAVE_OCC");
     return e ? std::atoi(e) : 0;
   }();
-  const bool occ2 = forced == 2 || (forced != 4 && (int64_t)L.B <= 2 * (int64_t)L.simds);
+  const bool occ2 = NG == 4 || forced == 2 || (forced != 4 && (int64_t)L.B <= 2 * (int64_t)L.simds);
   if (occ2) launch_wo<NG, POLICY, 2>(L, action, dtype, assign, o, s);
   else launch_wo<NG, POLICY, 4>(L, action, dtype, assign, o, s);
 }
@@ -139,7 +151,8 @@ void launch_pol(const LaunchCtx& L, const void* action, int dtype, int32_t* assi
 void launch_step_wave(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
                       const ObsOutputs& o, hipStream_t s) {
   if (L.S <= 2) launch_wpol<1>(L, action, dtype, assign, o, s);
-  else launch_wpol<2>(L, action, dtype, assign, o, s);
+  else if (L.S <= 4) launch_wpol<2>(L, action, dtype, assign, o, s);
+  else launch_wpol<4>(L, action, dtype, assign, o, s);
 }
 
 bool launch_fused_step(const LaunchCtx& L, int group_lanes, const void* action, int dtype,

@@ -320,10 +320,9 @@ def _expected_step_kernels(B, S, simds):
     if wave and S <= 4:
         ng = 1 if S <= 2 else 2
         occ = 2 if B <= 2 * simds else 4
-        return {4: f"step_wave_kernel<{ng}, 0, false, {occ}>"}
-    if wave:
-        ng = 1 if S <= 2 else 2 if S <= 4 else 4
-        return {0: f"dynamics_wave_kernel<{ng}, 0, 0, false>", 1: "observe_kernel<"}
+        return {4: f"step_wave_kernel<{ng}, 0, false, {occ}, 4>"}
+    if wave:  # S = 5-8: one launch at <= 2 envs per SIMD (the two-chunk observe, OCC 2)
+        return {4: "step_wave_kernel<4, 0, false, 2, 8>"}
     g = 2 if S <= 2 else (8 if B * 4 // 64 <= simds // 2 else 4) if S <= 4 else 8 if S <= 8 else 16
     return {0: f"dynamics_group_kernel<{g}, 0, 0, false", 1: "observe_kernel<"}
 
@@ -348,7 +347,7 @@ def test_configs1_default_dispatch_4096x4(lib, oracle_mod):
 def test_dispatch_boundaries_bit_exact(lib, oracle_mod, S, where):
     """Batches at the dispatch boundaries of the default step (in envs per SIMD of this device):
     S = 4 at 2 and 4 envs per SIMD (step_wave_kernel OCC 2 -> OCC 4 -> server-per-lane groups),
-    S = 8 at 2 envs per SIMD (dynamics_wave_kernel -> groups).  The kernel that ran is checked by
+    S = 8 at 2 envs per SIMD (step_wave_kernel's two-chunk form -> groups).  The kernel that ran is checked by
     name (lbsim_launch_names), the results against the oracle on every env."""
     from marllb_amd import _lib
     simds = _simds()
