@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define LBSIM_ABI_VERSION 5
+#define LBSIM_ABI_VERSION 6
 #define LBSIM_MAX_SERVERS 64   /* S <= 64: BASELINE configs[4] read literally is 4 agents x 16 */
                                /* servers = 64 (S > 16: server-per-lane dynamics only)       */
 #define LBSIM_RESERVOIR_K 128  /* reservoir.py:31 capacity=128, reservoir.h:24               */
@@ -138,7 +138,22 @@ typedef struct lbsim_config {
   int32_t warmup_steps;      /* simulated steps run inside reset() with weights 1.0         */
   int32_t dyn_mapping;       /* lbsim_dyn_mapping: how envs map onto lanes (results identical) */
   int32_t step_kernel;       /* lbsim_step_kernel: one fused launch or two (results identical) */
-  int32_t reserved[6];
+  /* Lost-FIN flows (VPP's timed-out flow sample, src/vpp/lb/lbhash.h:175-217, stats.h:27): a
+   * flow's FIN/RST is missed with probability lost_fin_prob; its flow-table entry expires
+   * flow_timeout_s after its last packet and the next flow hashed into its bucket (an exponential
+   * wait of mean flow_buckets / arrival_rate) wraps it up with fct = now - t_init - 40 s.  The
+   * sample (signed us) is recorded at the flow's completion.  0 = off. */
+  float lost_fin_prob;       /* [0, 1], default 0                                            */
+  float flow_timeout_s;      /* the lb plugin's flow timeout, default 40 (lb.c:1437)        */
+  int32_t flow_buckets;      /* sticky buckets per core, default 1024 (lb.h:46)             */
+  /* Server failure / recovery (THEORY.md §6.4 "server_failure ~ Bernoulli(p_fail)"): at the
+   * start of each step an up server fails with probability fail_prob (its queued flows are lost
+   * and counted as dropped, its reservoirs emptied: an all-zero observation row, inactive in the
+   * reward, env.py:410-413) and a down server recovers with probability recover_prob.  A down
+   * server takes no flows (as a full one).  fail_prob 0 = off (no state is allocated). */
+  float fail_prob;           /* [0, 1], default 0                                            */
+  float recover_prob;        /* [0, 1], default 0.1                                          */
+  int32_t reserved[1];
 } lbsim_config_t;
 
 typedef struct lbsim lbsim_t; /* opaque handle */

@@ -58,7 +58,12 @@ class LbsimConfig(ctypes.Structure):
         ("warmup_steps", ctypes.c_int32),
         ("dyn_mapping", ctypes.c_int32),
         ("step_kernel", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 6),
+        ("lost_fin_prob", ctypes.c_float),
+        ("flow_timeout_s", ctypes.c_float),
+        ("flow_buckets", ctypes.c_int32),
+        ("fail_prob", ctypes.c_float),
+        ("recover_prob", ctypes.c_float),
+        ("reserved", ctypes.c_int32 * 1),
     ]
 
 

@@ -154,6 +154,17 @@ int validate(const lbsim_config_t* c, char* msg, size_t n) {
     return bad("unknown dyn_mapping %d", c->dyn_mapping);
   if (c->step_kernel < LBSIM_STEP_AUTO || c->step_kernel > LBSIM_STEP_FUSED)
     return bad("unknown step_kernel %d", c->step_kernel);
+  if (!(c->lost_fin_prob >= 0.0f) || !(c->lost_fin_prob <= 1.0f))
+    return bad("lost_fin_prob must be in [0, 1]");
+  if (c->lost_fin_prob > 0.0f) {
+    if (!(c->flow_timeout_s >= 0.0f) || !(c->flow_timeout_s <= 3600.0f))
+      return bad("flow_timeout_s must be in [0, 3600]");
+    if (c->flow_buckets < 1 || (double)c->flow_buckets / (double)c->arrival_rate > 100.0)
+      return bad("flow_buckets must be >= 1 with flow_buckets / arrival_rate <= 100 s");
+  }
+  if (!(c->fail_prob >= 0.0f) || !(c->fail_prob <= 1.0f)) return bad("fail_prob must be in [0, 1]");
+  if (!(c->recover_prob >= 0.0f) || !(c->recover_prob <= 1.0f))
+    return bad("recover_prob must be in [0, 1]");
   if (c->dyn_mapping == LBSIM_DYN_ENV_PER_LANE && c->num_servers > 16)
     return bad("the env-per-lane dynamics mapping takes at most 16 servers (got %d)",
                c->num_servers);
@@ -187,6 +198,12 @@ void derive_params(const lbsim_config_t& c, SimParams& p) {
   p.normalize = c.normalize_obs ? 1 : 0;
   p.trace = c.arrival_source == LBSIM_ARRIVAL_TRACE ? 1 : 0;
   p.trace_rows = 0;
+  p.lf_thr = (uint32_t)std::llround((double)c.lost_fin_prob * 16777216.0);
+  p.lf_off_us = (int32_t)(std::llround((double)c.flow_timeout_s * 1e6) - 40000000LL);
+  p.lf_wait_us = c.lost_fin_prob > 0.0f
+                     ? (float)((double)c.flow_buckets * 1e6 / (double)c.arrival_rate) : 0.0f;
+  p.fail_thr = (uint32_t)std::llround((double)c.fail_prob * 16777216.0);
+  p.rec_thr = (uint32_t)std::llround((double)c.recover_prob * 16777216.0);
 }
 
 // State sections in snapshot order.
@@ -210,6 +227,7 @@ std::vector<Section> sections(lbsim_t* h) {
     v.push_back({(void**)&s.norm_mean, BS * NF * 8});
     v.push_back({(void**)&s.norm_std, BS * NF * 8});
   }
+  if (h->cfg.fail_prob > 0.0f) v.push_back({(void**)&s.down, BS * 4});
   return v;
 }
 
@@ -458,6 +476,11 @@ int lbsim_config_default(lbsim_config_t* c) {
   c->decay_factor = 0.9f;
   c->queue_capacity = 32;
   c->warmup_steps = 8;
+  c->lost_fin_prob = 0.0f;
+  c->flow_timeout_s = 40.0f;  // LB_DEFAULT_FLOW_TIMEOUT (lb.c:1437)
+  c->flow_buckets = 1024;     // LB_DEFAULT_PER_CPU_STICKY_BUCKETS (lb.h:46)
+  c->fail_prob = 0.0f;
+  c->recover_prob = 0.1f;
   return LBSIM_OK;
 }
 

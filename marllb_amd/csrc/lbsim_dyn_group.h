@@ -88,6 +88,16 @@ __device__ __forceinline__ int32_t group_min_i32(int32_t v) {
   return v;
 }
 template <int G>
+__device__ __forceinline__ uint32_t group_add(uint32_t v) {  // every lane holds the group's sum
+  v += gdpp<0xB1>(v);
+  if constexpr (G >= 4) v += gdpp<0x4E>(v);
+  if constexpr (G >= 8) v += gdpp<0x141>(v);
+  if constexpr (G >= 16) v += gdpp<0x140>(v);
+  if constexpr (G >= 32) v += (uint32_t)__shfl_xor((int)v, 16, 64);
+  if constexpr (G >= 64) v += (uint32_t)__shfl_xor((int)v, 32, 64);
+  return v;
+}
+template <int G>
 __device__ __forceinline__ uint32_t group_or(uint32_t v) {
   v |= gdpp<0xB1>(v);
   if constexpr (G >= 4) v |= gdpp<0x4E>(v);
@@ -106,6 +116,7 @@ __device__ __forceinline__ uint64_t group_bits(uint64_t m, int gbase) {
 // The server this lane owns (fields of DESIGN.md §4, in registers).
 struct SrvLane {
   int32_t cnt, head_tc, head, lh, tail, last, assigned;
+  int32_t qcap;     // Q, or 0 while the server is down (fail_prob > 0): not eligible, as full
   uint32_t rcnt;
   uint32_t* chgw;   // LDS [4][64]: word w of this lane's 128-bit mask of the reservoir slots
                     // written this launch (DevState::chg), set by one ds_or per insert
@@ -242,7 +253,7 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
         V.score = (float)q;
       }
     }
-    const bool elig = V.act && V.cnt < Q;
+    const bool elig = V.act && V.cnt < V.qcap;
     const uint64_t em = group_bits<G>(__ballot(elig), gbase);
     int chosen = -1;
     if constexpr (alias) {
@@ -291,8 +302,10 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
     // ---- the pushed flow's Algorithm R draw is this arrival's word r (E.u3)
     const int slot = reservoir_slot_r32(V.rcnt, E.u3);
     if (ins && slot >= 0) {
-      my_res[(uint32_t)slot] = make_uint3((uint32_t)(tc_a - ta), (uint32_t)svc,
-                                          gc.base_ms + (gc.base_rem + (uint32_t)tc_a) / 1000u);
+      my_res[(uint32_t)slot] = make_uint3(
+          lost_fct(p, (uint32_t)(tc_a - ta), gc.base_ms * 1000u + gc.base_rem + (uint32_t)ta, E.gid,
+                   E.episode),
+          (uint32_t)svc, gc.base_ms + (gc.base_rem + (uint32_t)tc_a) / 1000u);
       mark(slot);
     }
     if (mine) {
@@ -357,6 +370,26 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
     atomicOr(V.chgw + ((uint32_t)slot >> 5) * 64u, 1u << (slot & 31));
   };
 
+  // ---- 0. server failure / recovery (fail_prob > 0, a uniform branch): one Philox draw per
+  //      server, stream 5, counter (clock, gid, episode); a failing server loses its queue (the
+  //      flows count as dropped) and its reservoirs; a down server takes no flows
+  if (p.fail_thr != 0u) {
+    const u32x4 d = philox4x32_10(
+        u32x4{E.clock, E.gid, E.episode, (kStreamFailure << 24) | (uint32_t)s}, p.key0, p.key1);
+    const uint32_t u = d.x >> 8;
+    const bool was_down = V.qcap == 0;
+    const bool fails = V.act && !was_down && u < p.fail_thr;
+    const bool recovers = V.act && was_down && u < p.rec_thr;
+    E.dropped += group_add<G>(fails ? (uint32_t)V.cnt : 0u);
+    if (fails) {
+      V.cnt = 0;
+      V.last = kLastNone;
+      V.rcnt = 0u;
+      mark(0);  // emptied: the next observe recomputes the (zero) features
+    }
+    V.qcap = fails ? 0 : (recovers ? Q : V.qcap);
+  }
+
   // ---- 1. this lane's carried-in flows that complete in this step: samples in FIFO order
   if (V.act && V.cnt > 0 && V.head_tc <= dt) {
     int32_t prev = V.last;
@@ -369,9 +402,9 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
           u32x4{rc >> 1, E.gid, E.episode, (kStreamReservoir << 24) | (uint32_t)s}, p.key0, p.key1);
       const int slot = reservoir_slot(rc, d);
       if (slot >= 0) {
-        my_res[(uint32_t)slot] =
-            make_uint3((uint32_t)(etc - eta), (uint32_t)(etc - (eta > prev ? eta : prev)),
-                       base_ms + (base_rem + (uint32_t)etc) / 1000u);
+        my_res[(uint32_t)slot] = make_uint3(
+            lost_fct(p, (uint32_t)(etc - eta), (uint32_t)base_us + (uint32_t)eta, E.gid, E.episode),
+            (uint32_t)(etc - (eta > prev ? eta : prev)), base_ms + (base_rem + (uint32_t)etc) / 1000u);
         mark(slot);
       }
       prev = etc;
@@ -493,6 +526,7 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
     V.tail = 0;
     V.last = kLastNone;
     V.rcnt = 0u;
+    V.qcap = Q;  // every server is up at the episode start
 #pragma unroll
     for (int k = 0; k < G; ++k) wall[k] = 1.0f;
     for (int k = 0; k < p.warmup_steps; ++k)
@@ -516,7 +550,9 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
     V.tail = 0;
     V.last = kLastNone;
     V.rcnt = 0u;
+    V.qcap = Q;
     if (V.act) {
+      if (st.down != nullptr && st.down[sb] != 0u) V.qcap = 0;
       const uint32_t hc = st.hc[sb];
       V.head = (int)(hc & 0xFFFFu);
       V.cnt = (int32_t)(hc >> 16);
@@ -555,6 +591,7 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
     st.hc[sb] = (uint32_t)V.head | ((uint32_t)V.cnt << 16);
     st.last_tc[sb] = V.last;
     st.res_count[sb] = V.rcnt;
+    if (st.down != nullptr) st.down[sb] = V.qcap == 0 ? 1u : 0u;
     *reinterpret_cast<uint4*>(st.chg + (size_t)sb * 4) =
         make_uint4(chgw[lane], chgw[64 + lane], chgw[128 + lane], chgw[192 + lane]);
     if (MODE != kModeReset && assign_out != nullptr) assign_out[sb] = V.assigned;

@@ -199,8 +199,9 @@ __device__ __forceinline__ void wave_flush(const SimParams& p, WaveSrv& V, WaveE
   if (slot >= 0 && Ld.own[key] == me_tag) {
     int32_t svc = (int32_t)(Bt.wk * scale);
     svc = svc < 1 ? 1 : svc;
-    res_b[key] = make_uint3((uint32_t)(Bt.ltc - Bt.ta), (uint32_t)svc,
-                            base_ms + (base_rem + (uint32_t)Bt.ltc) / 1000u);
+    res_b[key] = make_uint3(lost_fct(p, (uint32_t)(Bt.ltc - Bt.ta),
+                                     base_ms * 1000u + base_rem + (uint32_t)Bt.ta, E.gid, E.episode),
+                            (uint32_t)svc, base_ms + (base_rem + (uint32_t)Bt.ltc) / 1000u);
   }
 }
 
@@ -452,9 +453,9 @@ __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParam
           p.key1);
       const int slot = reservoir_slot(rc, d);
       if (slot >= 0) {
-        res_b[(uint32_t)lane * K + (uint32_t)slot] =
-            make_uint3((uint32_t)(e.x - e.y), (uint32_t)(e.x - (e.y > prev ? e.y : prev)),
-                       base_ms + (base_rem + (uint32_t)e.x) / 1000u);
+        res_b[(uint32_t)lane * K + (uint32_t)slot] = make_uint3(
+            lost_fct(p, (uint32_t)(e.x - e.y), (uint32_t)base_us + (uint32_t)e.y, E.gid, E.episode),
+            (uint32_t)(e.x - (e.y > prev ? e.y : prev)), base_ms + (base_rem + (uint32_t)e.x) / 1000u);
         atomicOr(Ld.chg + ((uint32_t)slot >> 5) * kWaveMaxS + (uint32_t)lane, 1u << (slot & 31));
       }
       prev = e.x;

@@ -81,6 +81,7 @@ inline bool dyn_wave_ok(const LaunchCtx& L) {
   static const bool forced_lanes = std::getenv("LBSIM_DYN_GROUP_LANES") != nullptr;
   if (mode == 0 || forced_lanes || L.dyn_mapping == LBSIM_DYN_ENV_PER_LANE) return false;
   if (L.S > 8 || L.prm.Q > 32 || L.prm.policy == LBSIM_POLICY_ALIAS) return false;
+  if (L.prm.fail_thr != 0u) return false;  // server failures: the group / env-lane kernels
   const int64_t per_simd = L.S <= 4 ? 4 : 2;  // S = 8: 2048 envs 0.058 vs 0.078 ms, 4096 0.087 vs 0.083
   return mode == 1 || (int64_t)L.B <= (max_b >= 0 ? max_b : per_simd * (int64_t)L.simds);
 }

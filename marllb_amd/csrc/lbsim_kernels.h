@@ -62,6 +62,8 @@ struct DevState {
   // timestamps and n = min(count, K) are unchanged: count only grows without a write once full).
   uint32_t* chg;
   float* fcache;
+  // server failures (only if fail_prob > 0, else nullptr): down[b*S + s] = 1 while server s is down
+  uint32_t* down;
   // stateless features API only: caller's separate value / timestamp arrays [n*K]
   const uint32_t* feat_vals;
   const uint32_t* feat_ts;
@@ -94,7 +96,47 @@ struct SimParams {
   int32_t normalize;
   int32_t trace;          // 1: arrivals replay the trace (LBSIM_ARRIVAL_TRACE)
   uint32_t trace_rows;
+  // lost-FIN flows (lost_fct): 24-bit probability threshold (0 = off), flow_timeout - 40 s in us,
+  // mean bucket wait in us
+  uint32_t lf_thr;
+  int32_t lf_off_us;
+  float lf_wait_us;
+  // server failure / recovery (fail_transitions): 24-bit thresholds per server-step (fail 0 = off)
+  uint32_t fail_thr, rec_thr;
 };
+
+constexpr uint32_t kStreamFailure = 5u;  // Philox stream of the failure / recovery draws
+
+// murmur3's 32-bit finaliser (fmix32): the lost-FIN hash.
+__device__ __forceinline__ uint32_t lf_mix(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+
+// The fct sample of a completed flow, fct = tc - ta (lbhash.h:116-124, RSTACK: now - t_init), or,
+// for a flow whose FIN/RST the data plane missed (probability lost_fin_prob), VPP's timed-out guess
+// (lbhash.h:175-217): the entry expires flow_timeout after the flow's last packet (its completion),
+// the next flow hashed into the bucket takes it after an exponential wait of mean flow_buckets /
+// arrival_rate, and the plugin records now - t_init - LB_DEFAULT_FLOW_TIMEOUT (40 s, stats.h:27)
+// = fct + flow_timeout - 40 s + wait, signed us.  Lost or not and the wait are a hash of (seed,
+// global env id, episode, the flow's absolute arrival us mod 2^32): a pure function of the flow,
+// the same whichever step, kernel or shard records it (oracle_lost_fin_fct).  abs_ta =
+// (uint32)(clock * dt) + ta.  Off (lf_thr == 0, a uniform branch): fct unchanged.
+__device__ __forceinline__ uint32_t lost_fct(const SimParams& p, uint32_t fct, uint32_t abs_ta,
+                                             uint32_t gid, uint32_t episode) {
+  if (p.lf_thr == 0u) return fct;
+  const uint32_t salt =
+      lf_mix(lf_mix(p.key0 ^ (episode * 0x9E3779B9u)) ^ gid ^ (p.key1 * 0x85EBCA6Bu));
+  const uint32_t h = lf_mix(abs_ta ^ salt);
+  if ((h >> 8) >= p.lf_thr) return fct;
+  const uint32_t h2 = lf_mix(h ^ 0x6A09E667u);
+  const int32_t wait = (int32_t)(-lb_logf(u01_open0(h2)) * p.lf_wait_us);
+  return fct + (uint32_t)p.lf_off_us + (uint32_t)wait;
+}
 
 constexpr uint32_t kTraceEnvStride = 7919u;        // SURVEY §8d C3 per-env offset
 constexpr uint32_t kTraceEpisodeStride = 1000003u;  // next episode, another window
@@ -150,6 +192,7 @@ struct LaneState {
   float next_work;
   uint32_t u2, u3, arr_idx, episode, clock, dropped;
   uint32_t gid;
+  uint32_t downm;         // bit s: server s is down (fail_prob > 0), not eligible as a full one
   // TRACE: row of arrival arr_idx + 1 and its prefetched gap / work (loaded an arrival ahead so
   // the event loop never waits on the trace)
   uint32_t row;
@@ -330,6 +373,7 @@ template <int MAXS>
 __device__ __forceinline__ void load_servers(const DevState& st, const SimParams& p,
                                              LaneState<MAXS>& L, uint32_t b, const Lds& l) {
   constexpr int WL = LaneState<MAXS>::WL;
+  L.downm = 0u;
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) {
     L.cnt[s] = 0;
@@ -343,6 +387,7 @@ __device__ __forceinline__ void load_servers(const DevState& st, const SimParams
       const int head = (int)(hc & 0xFFFFu);
       L.cnt[s] = (int32_t)(hc >> 16);
       L.head[s] = head;
+      if (st.down != nullptr && st.down[sb] != 0u) L.downm |= 1u << s;
       L.last[s] = st.last_tc[sb];
       fld<MAXS>(l, F_RCNT, s) = (int32_t)st.res_count[sb];
       fld<MAXS>(l, F_ASSIGNED, s) = 0;
@@ -369,6 +414,7 @@ __device__ __forceinline__ void load_servers(const DevState& st, const SimParams
 template <int MAXS>
 __device__ __forceinline__ void clear_servers(const SimParams& p, LaneState<MAXS>& L,
                                               const Lds& l) {
+  L.downm = 0u;  // every server is up at the episode start
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) {
     L.cnt[s] = 0;
@@ -576,7 +622,7 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
     if constexpr (alias) {  // full server: the flow is dropped (ALIAS has no eligibility test)
       if (n_alias > 0) {
         const int a = alias_pick(FieldAliasTab<MAXS>{l}, n_alias, L.u2);
-        chosen = sel<MAXS>(L.cnt, a) < Q ? a : -1;
+        chosen = (sel<MAXS>(L.cnt, a) < Q && !((L.downm >> a) & 1u)) ? a : -1;
       }
     } else if constexpr (two_choice) {  // SED2 / LSQ2: keep the second candidate if strictly better
       const int h1 = two_choice_h1(L.u2, S);
@@ -586,9 +632,9 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
 #pragma unroll
       for (int s = 0; s < MAXS; ++s) {
         s1 = (s == h1) ? score[s] : s1;
-        ok1 = (s == h1) ? (L.cnt[s] < Q) : ok1;
+        ok1 = (s == h1) ? (L.cnt[s] < Q && !((L.downm >> s) & 1u)) : ok1;
         s2 = (s == h2) ? score[s] : s2;
-        ok2 = (s == h2) ? (L.cnt[s] < Q) : ok2;
+        ok2 = (s == h2) ? (L.cnt[s] < Q && !((L.downm >> s) & 1u)) : ok2;
       }
       chosen = (ok1 && ok2) ? ((s2 < s1) ? h2 : h1) : (ok1 ? h1 : (ok2 ? h2 : -1));
     } else {  // SED / LSQ: start at the hashed server, replace on strictly lower score
@@ -596,21 +642,22 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
       float best = __uint_as_float(0x7f800000u);  // +inf: any finite score replaces it
 #pragma unroll
       for (int s = 0; s < MAXS; ++s) {
-        const bool m = (s == h) & (L.cnt[s] < Q);
+        const bool m = (s == h) & (L.cnt[s] < Q) & !((L.downm >> s) & 1u);
         chosen = m ? s : chosen;
         best = m ? score[s] : best;
       }
       if (FAST || lsq) {  // every score finite: "replace on strictly lower" from +inf is exact
 #pragma unroll
         for (int s = 0; s < MAXS; ++s) {
-          const bool m = (s < S) & (L.cnt[s] < Q) & (score[s] < best);
+          const bool m = (s < S) & (L.cnt[s] < Q) & !((L.downm >> s) & 1u) & (score[s] < best);
           chosen = m ? s : chosen;
           best = m ? score[s] : best;
         }
       } else {  // NaN / inf scores: the first eligible server is taken whatever its score
 #pragma unroll
         for (int s = 0; s < MAXS; ++s) {
-          const bool m = (s < S) & (L.cnt[s] < Q) & ((chosen < 0) | (score[s] < best));
+          const bool m = (s < S) & (L.cnt[s] < Q) & !((L.downm >> s) & 1u) &
+                         ((chosen < 0) | (score[s] < best));
           chosen = m ? s : chosen;
           best = m ? score[s] : best;
         }
@@ -653,9 +700,10 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
                               ec.rk0, ec.rk1);
     const int slot = reservoir_slot_r32(cres, L.u3);
     if (ins && slot >= 0) {
-      my_res[(uint32_t)cs * (uint32_t)K + (uint32_t)slot] =
-          make_uint3((uint32_t)(tc_a - ta), (uint32_t)svc,
-                     ec.base_ms + (ec.base_rem + (uint32_t)tc_a) / 1000u);
+      my_res[(uint32_t)cs * (uint32_t)K + (uint32_t)slot] = make_uint3(
+          lost_fct(p, (uint32_t)(tc_a - ta), ec.base_ms * 1000u + ec.base_rem + (uint32_t)ta, L.gid,
+                   L.episode),
+          (uint32_t)svc, ec.base_ms + (ec.base_rem + (uint32_t)tc_a) / 1000u);
       mark_slot<MAXS>(l, cs, slot);
     }
     // queue index < WL: the LDS window (a push that does not happen writes the lane's scratch
@@ -789,6 +837,33 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
     }
   }
 
+  // ---- 0. server failure / recovery (fail_prob > 0, a uniform branch): one Philox draw per
+  //      server, stream 5, counter (clock, gid, episode); a failing server loses its queue (the
+  //      flows count as dropped) and its reservoirs; a down server takes no flows
+  if (p.fail_thr != 0u) {
+    for (int s = 0; s < S; ++s) {
+      const u32x4 d = philox4x32_10(
+          u32x4{L.clock, L.gid, L.episode, (kStreamFailure << 24) | (uint32_t)s}, p.key0, p.key1);
+      const uint32_t u = d.x >> 8;
+      const bool was_down = (L.downm >> s) & 1u;
+      if (was_down) {
+        if (u < p.rec_thr) L.downm &= ~(1u << s);
+      } else if (u < p.fail_thr) {
+        L.downm |= 1u << s;
+#pragma unroll
+        for (int k = 0; k < MAXS; ++k) {  // register arrays: constant indices only
+          if (k == s) {
+            L.dropped += (uint32_t)L.cnt[k];
+            L.cnt[k] = 0;
+            L.last[k] = kLastNone;
+          }
+        }
+        fld<MAXS>(l, F_RCNT, s) = 0;
+        mark_slot<MAXS>(l, s, 0);  // emptied: the next observe recomputes the (zero) features
+      }
+    }
+  }
+
   // ---- 1. carried-in flows completing in this step: samples in FIFO order per server
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) {
@@ -804,9 +879,9 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
             u32x4{rc >> 1, L.gid, L.episode, (kStreamReservoir << 24) | (uint32_t)s}, p.key0, p.key1);
         const int slot = reservoir_slot(rc, d);
         if (slot >= 0) {
-          my_res[(uint32_t)s * (uint32_t)K + (uint32_t)slot] =
-              make_uint3((uint32_t)(etc - eta), (uint32_t)(etc - (eta > prev ? eta : prev)),
-                         base_ms + (base_rem + (uint32_t)etc) / 1000u);
+          my_res[(uint32_t)s * (uint32_t)K + (uint32_t)slot] = make_uint3(
+              lost_fct(p, (uint32_t)(etc - eta), (uint32_t)base_us + (uint32_t)eta, L.gid, L.episode),
+              (uint32_t)(etc - (eta > prev ? eta : prev)), base_ms + (base_rem + (uint32_t)etc) / 1000u);
           mark_slot<MAXS>(l, s, slot);
         }
         prev = etc;
@@ -893,6 +968,7 @@ __device__ __forceinline__ void store_servers(const DevState& st, const SimParam
       st.hc[sb] = (uint32_t)head | ((uint32_t)L.cnt[s] << 16);
       st.last_tc[sb] = L.last[s];
       st.res_count[sb] = (uint32_t)fld<MAXS>(l, F_RCNT, s);
+      if (st.down != nullptr) st.down[sb] = (L.downm >> s) & 1u;
       if (assign_out != nullptr) assign_out[sb] = fld<MAXS>(l, F_ASSIGNED, s);
       *reinterpret_cast<uint4*>(st.chg + (size_t)sb * 4) =
           make_uint4(l.m[(s * 4 + 0) * 64 + l.lane], l.m[(s * 4 + 1) * 64 + l.lane],
@@ -1249,7 +1325,7 @@ __device__ __forceinline__ void bitonic128_keys_g8(uint32_t (&key)[16], int t) {
 // stateless features API hands in float bits.
 template <bool US>
 __device__ __forceinline__ float sample_value(uint32_t raw) {
-  if constexpr (US) return (float)raw * 1.0e-6f;
+  if constexpr (US) return (float)(int32_t)raw * 1.0e-6f;  // signed: lost-FIN guesses (lost_fct)
   else return __uint_as_float(raw);
 }
 
@@ -1672,7 +1748,10 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
         const int pos = 16 * j + e;
         const uint32_t slot = key[e] & 127u;
         if (pos < n) perm[pos] = (uint8_t)slot;
-        key[e] = pos < n ? (((vrow[slot] >> 16) << 7) | (uint32_t)pos) : 0xFFFFFFFFu;
+        // simulator samples are signed us (lost-FIN guesses can be negative): the high half
+        // with its sign bit flipped orders them as int32
+        const uint32_t hi = (vrow[slot] ^ (US ? 0x80000000u : 0u)) >> 16;
+        key[e] = pos < n ? ((hi << 7) | (uint32_t)pos) : 0xFFFFFFFFu;
       }
       bitonic128_keys_g8(key, j);
 #pragma unroll

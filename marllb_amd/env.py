@@ -102,7 +102,9 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
                 server_rates: Optional[List[float]] = None, load: float = 0.8,
                 queue_capacity: int = 32, warmup_steps: int = 8, decay_factor: float = 0.9,
                 assign_policy: str = "sed", trace=None,
-                dyn_mapping: str = "auto", step_kernel: str = "auto") -> _lib.LbsimConfig:
+                dyn_mapping: str = "auto", step_kernel: str = "auto",
+                lost_fin_prob: float = 0.0, flow_timeout: float = 40.0, flow_buckets: int = 1024,
+                fail_prob: float = 0.0, recover_prob: float = 0.1) -> _lib.LbsimConfig:
     """Build and validate an lbsim_config_t from reference-style kwargs.
 
     server_rates defaults to identical servers at utilisation `load`: mu = rate / (load * S).
@@ -112,6 +114,12 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
     dynamics kernel lays envs onto lanes; results are identical, only speed differs.
     step_kernel: "auto" | "split" (dynamics launch + observe launch) | "fused" (one launch that
     simulates then observes each workgroup's envs); results are identical.
+    lost_fin_prob / flow_timeout / flow_buckets: flows whose FIN/RST the VPP data plane misses
+    record its timed-out guess fct = now - t_init - 40 s (src/vpp/lb/lbhash.h:175-217) instead of
+    their fct: flow_timeout (s) is the lb plugin's entry timeout, flow_buckets / arrival_rate the
+    mean wait for the next flow in the bucket.  0 = off.
+    fail_prob / recover_prob: per server and step, an up server fails (its queue and reservoirs are
+    lost) and a down one recovers (THEORY.md §6.4 server_failure ~ Bernoulli(p_fail)).  0 = off.
     """
     if reward_metric not in _lib.METRICS:  # rewards.py:321-323
         raise ValueError(f"Unsupported metric: {reward_metric}. Supported: {_lib.METRICS}")
@@ -160,6 +168,11 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
     if step_kernel not in _lib.STEP_KERNELS:
         raise ValueError(f"Unknown step_kernel: {step_kernel}. Supported: {_lib.STEP_KERNELS}")
     cfg.step_kernel = _lib.STEP_KERNELS.index(step_kernel)
+    cfg.lost_fin_prob = float(lost_fin_prob)
+    cfg.flow_timeout_s = float(flow_timeout)
+    cfg.flow_buckets = int(flow_buckets)
+    cfg.fail_prob = float(fail_prob)
+    cfg.recover_prob = float(recover_prob)
     _lib.validate(cfg)
     return cfg
 

@@ -17,6 +17,8 @@
  *   - step/reset bookkeeping (done, return)           env.py:186-286
  *   - SED/SED2/LSQ/LSQ2 server choice                 src/vpp/lb/node.c:388-441
  *   - completion samples fct / duration               src/vpp/lb/lbhash.h:116-135
+ *   - lost-FIN flows' timed-out fct guess             src/vpp/lb/lbhash.h:175-217, stats.h:27
+ *   - server failure / recovery (Bernoulli per step)  problem-03 THEORY.md §6.4 (:687-693)
  * plus the flow dynamics the reference does not have (Poisson arrivals, per-server
  * FIFO service, Philox4x32-10 counter RNG).  Those are "parity unpinned" against the reference:
  * this file is their executable specification.
@@ -292,6 +294,12 @@ typedef struct oracle {
   int B, S, Q;
   int32_t dt_us;
   float mean_gap_us, svc_scale[LBSIM_MAX_SERVERS], decay_c;
+  /* lost-FIN flows: 24-bit probability threshold (0 = off), flow_timeout - 40 s in us, the mean
+   * bucket wait in us; server failures: 24-bit thresholds (fail 0 = off, no `down` section) */
+  uint32_t lf_thr;
+  int32_t lf_off_us;
+  float lf_wait_us;
+  uint32_t fail_thr, rec_thr;
   uint32_t key[2];
   int threads;
   int initialised;
@@ -311,6 +319,8 @@ typedef struct oracle {
    * observe */
   uint32_t* chg; float* fcache;
   double* norm_mean; double* norm_std;
+  /* server failures (only if fail_prob > 0): 1 = the server is down, per (env, server) */
+  uint32_t* down;
   /* TRACE arrivals (lbsim_set_trace semantics): us gap before each row, mean-1 work */
   uint32_t* trace_gap; float* trace_work; uint32_t trace_rows;
   /* not state: the Algorithm R draw word of each queued flow that arrived in the current step,
@@ -326,6 +336,12 @@ static void derive(oracle_t* o) {
   for (int s = 0; s < LBSIM_MAX_SERVERS; ++s)
     o->svc_scale[s] = s < c->num_servers ? (float)(1e6 / (double)c->server_rate[s]) : 0.0f;
   o->decay_c = oracle_decay_c(c->decay_factor);
+  o->lf_thr = (uint32_t)llround((double)c->lost_fin_prob * 16777216.0);
+  o->lf_off_us = (int32_t)(llround((double)c->flow_timeout_s * 1e6) - 40000000LL);
+  o->lf_wait_us = c->lost_fin_prob > 0.0f
+                      ? (float)((double)c->flow_buckets * 1e6 / (double)c->arrival_rate) : 0.0f;
+  o->fail_thr = (uint32_t)llround((double)c->fail_prob * 16777216.0);
+  o->rec_thr = (uint32_t)llround((double)c->recover_prob * 16777216.0);
   o->key[0] = (uint32_t)(c->seed & 0xFFFFFFFFull);
   o->key[1] = (uint32_t)(c->seed >> 32);
 }
@@ -339,7 +355,8 @@ oracle_t* oracle_create(const lbsim_config_t* cfg) {
   const size_t B = o->B, BS = (size_t)o->B * o->S, BSQ = BS * o->Q, BSK = BS * K;
   const size_t sz[] = {B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4,
                        B * 8, BS * 4, BS * 4, BS * 4, BSQ * 8, BSK * 12, BS * 16, BS * 40,
-                       cfg->normalize_obs ? BS * NF * 8 : 0, cfg->normalize_obs ? BS * NF * 8 : 0};
+                       cfg->normalize_obs ? BS * NF * 8 : 0, cfg->normalize_obs ? BS * NF * 8 : 0,
+                       cfg->fail_prob > 0.0f ? BS * 4 : 0};
   size_t total = 0;
   for (size_t i = 0; i < sizeof(sz) / sizeof(sz[0]); ++i) total += sz[i];
   o->bytes = total;
@@ -352,7 +369,7 @@ oracle_t* oracle_create(const lbsim_config_t* cfg) {
                    (void**)&o->norm_count, (void**)&o->ep_return, (void**)&o->hc,
                    (void**)&o->last_tc, (void**)&o->res_count, (void**)&o->ring,
                    (void**)&o->res, (void**)&o->chg, (void**)&o->fcache, (void**)&o->norm_mean,
-                   (void**)&o->norm_std};
+                   (void**)&o->norm_std, (void**)&o->down};
   for (size_t i = 0; i < sizeof(sz) / sizeof(sz[0]); ++i) {
     *ptrs[i] = sz[i] ? (void*)p : NULL;
     p += sz[i];
@@ -511,7 +528,33 @@ static void ring_set(oracle_t* o, size_t sb, int head, int cnt) {
 }
 
 /* A reservoir sample in seconds from its integer-microsecond form (env.py reports seconds). */
-static float us_to_seconds(uint32_t us) { return (float)us * 1.0e-6f; }
+static float us_to_seconds(uint32_t us) { return (float)(int32_t)us * 1.0e-6f; }
+
+/* murmur3's 32-bit finaliser (fmix32): the lost-FIN hash. */
+static uint32_t lf_mix(uint32_t h) {
+  h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+  return h;
+}
+
+/* The fct sample of a completed flow (lbhash.h:116-124 RSTACK: now - t_init) or, for a flow whose
+ * FIN/RST the data plane missed, VPP's timed-out guess (lbhash.h:175-217): its entry expires
+ * flow_timeout after the last packet (the completion tc), the next flow hashed into the bucket
+ * takes it after an exponential wait of mean flow_buckets / arrival_rate, and the plugin records
+ * now - t_init - LB_DEFAULT_FLOW_TIMEOUT (40 s, stats.h:27) = fct + flow_timeout - 40 s + wait.
+ * Lost or not, and the wait, are a hash of (seed, global env id, episode, the flow's absolute
+ * arrival us mod 2^32): a pure function of the flow, whichever step records it.  Signed us, in
+ * uint32 arithmetic. */
+uint32_t oracle_lost_fin_fct(uint32_t fct, uint32_t abs_ta, uint32_t gid, uint32_t episode,
+                             uint32_t key0, uint32_t key1, uint32_t thr, int32_t off_us,
+                             float wait_us) {
+  if (thr == 0u) return fct;
+  const uint32_t salt = lf_mix(lf_mix(key0 ^ (episode * 0x9E3779B9u)) ^ gid ^ (key1 * 0x85EBCA6Bu));
+  const uint32_t h = lf_mix(abs_ta ^ salt);
+  if ((h >> 8) >= thr) return fct;
+  const uint32_t h2 = lf_mix(h ^ 0x6A09E667u);
+  const int32_t wait = (int32_t)(-oracle_logf(u01(h2)) * wait_us);
+  return fct + (uint32_t)off_us + (uint32_t)wait;
+}
 
 /* Algorithm R slot for a flow that arrived in the step it completes in: the draw
  * is its arrival's word r (word 3 of the arrival's Philox block), j = floor(r (c + 1) / 2^32)
@@ -565,7 +608,10 @@ static void pop_until(env_ctx* e, int s, int32_t t, uint64_t base_us, double den
     const int32_t tc = ent[0], ta = ent[1];
     if (tc > t) break;
     const int32_t start = ta > o->last_tc[sb] ? ta : o->last_tc[sb];
-    const uint32_t fct = (uint32_t)(tc - ta);   /* the sample is (float)fct * 1e-6f seconds */
+    /* the sample is (float)(int32_t)fct * 1e-6f seconds */
+    const uint32_t fct = oracle_lost_fin_fct((uint32_t)(tc - ta), (uint32_t)base_us + (uint32_t)ta,
+                                             e->gid, o->episode[e->b], o->key[0], o->key[1],
+                                             o->lf_thr, o->lf_off_us, o->lf_wait_us);
     const uint32_t dur = (uint32_t)(tc - start);
     o->last_tc[sb] = tc;
     const uint32_t ts_ms = (uint32_t)((base_us + (uint64_t)(int64_t)tc) / 1000u);
@@ -620,6 +666,31 @@ static void sim_step(env_ctx* e, const float* w) {
     oracle_gen_alias(w_act, n_act, odd64, alias);
     for (int k = 0; k < n_act; ++k) odd[k] = (float)odd64[k];
   }
+  /* server failure / recovery at the step start (THEORY.md §6.4): one draw per server, stream 5,
+   * counter (clock, gid, episode); a failing server loses its queued flows (counted as dropped)
+   * and its reservoirs, and takes no flows while down (capacity 0, as a full server) */
+  int qcap[LBSIM_MAX_SERVERS];
+  for (int s = 0; s < S; ++s) qcap[s] = Q;
+  if (o->down) {
+    for (int s = 0; s < S; ++s) {
+      const size_t sb = b * (size_t)S + (size_t)s;
+      const uint32_t ctr[4] = {o->clock[b], e->gid, o->episode[b], (5u << 24) | (uint32_t)s};
+      uint32_t d[4];
+      oracle_philox(ctr, o->key, d);
+      const uint32_t u = d[0] >> 8;
+      if (o->down[sb]) {
+        if (u < o->rec_thr) o->down[sb] = 0u;
+      } else if (u < o->fail_thr) {
+        o->down[sb] = 1u;
+        o->dropped[b] += (uint32_t)ring_count(o, sb);
+        ring_set(o, sb, ring_head(o, sb), 0);
+        o->last_tc[sb] = LAST_NONE;
+        o->res_count[sb] = 0u;
+        o->chg[sb * 4] |= 1u; /* emptied: the next observe recomputes the (zero) features */
+      }
+      if (o->down[sb]) qcap[s] = 0;
+    }
+  }
 
   while (o->next_arr[b] < o->dt_us) {
     const int32_t ta = o->next_arr[b];
@@ -640,14 +711,14 @@ static void sim_step(env_ctx* e, const float* w) {
         int bucket = (int)rn;
         if (bucket > n_act - 1) bucket = n_act - 1;
         const int k = (rn - (float)bucket) > odd[bucket] ? alias[bucket] : bucket;
-        if (cnt[act[k]] < Q) chosen = act[k];
+        if (cnt[act[k]] < qcap[act[k]]) chosen = act[k];
       }
     } else if (policy == LBSIM_POLICY_SED2 || policy == LBSIM_POLICY_LSQ2) {
       /* node.c:409-417 / 433-441: two candidates, keep the second only if strictly better; the
        * candidates are the hash word's high and low 16 bits mapped to [0, S) */
       const int h1 = (int)(((o->next_u2[b] >> 16) * (uint32_t)S) >> 16);
       const int h2 = (int)(((o->next_u2[b] & 0xFFFFu) * (uint32_t)S) >> 16);
-      const int ok1 = cnt[h1] < Q, ok2 = cnt[h2] < Q;
+      const int ok1 = cnt[h1] < qcap[h1], ok2 = cnt[h2] < qcap[h2];
       if (ok1 && ok2) chosen = sc[h2] < sc[h1] ? h2 : h1;
       else if (ok1) chosen = h1;
       else if (ok2) chosen = h2;
@@ -655,9 +726,9 @@ static void sim_step(env_ctx* e, const float* w) {
       /* node.c:393-404: start at the hashed (Maglev) server, replace on strictly lower score */
       const int h = (int)(((uint64_t)o->next_u2[b] * (uint64_t)S) >> 32);
       float best = 0.0f;
-      if (cnt[h] < Q) { chosen = h; best = sc[h]; }
+      if (cnt[h] < qcap[h]) { chosen = h; best = sc[h]; }
       for (int s = 0; s < S; ++s)
-        if (cnt[s] < Q && (chosen < 0 || sc[s] < best)) { chosen = s; best = sc[s]; }
+        if (cnt[s] < qcap[s] && (chosen < 0 || sc[s] < best)) { chosen = s; best = sc[s]; }
     }
     if (chosen < 0) {
       o->dropped[b] += 1u;
@@ -795,6 +866,7 @@ static void reset_env(oracle_t* o, size_t b) {
     o->last_tc[sb] = LAST_NONE;
     o->res_count[sb] = 0u;
     for (int w = 0; w < 4; ++w) o->chg[sb * 4 + (size_t)w] = 0u;
+    if (o->down) o->down[sb] = 0u; /* every server is up at the episode start */
   }
   float w1[LBSIM_MAX_SERVERS];
   for (int s = 0; s < LBSIM_MAX_SERVERS; ++s) w1[s] = 1.0f;

@@ -4,7 +4,7 @@ import numpy as np
 K, NF = 128, 11
 
 
-def sections(B, S, Q, normalize):
+def sections(B, S, Q, normalize, failures=False):
     BS = B * S
     out = [("next_arr", np.int32, B), ("next_work", np.float32, B), ("next_u2", np.uint32, B),
            ("next_u3", np.uint32, B), ("arr_idx", np.uint32, B), ("episode", np.uint32, B),
@@ -14,12 +14,14 @@ def sections(B, S, Q, normalize):
            ("res", np.uint32, BS * K * 3), ("chg", np.uint32, BS * 4), ("fcache", np.float32, BS * 10)]
     if normalize:
         out += [("norm_mean", np.float64, BS * NF), ("norm_std", np.float64, BS * NF)]
+    if failures:
+        out += [("down", np.uint32, BS)]
     return out
 
 
-def parse(buf: bytes, B, S, Q, normalize):
+def parse(buf: bytes, B, S, Q, normalize, failures=False):
     d, off = {}, 0
-    for name, dt, n in sections(B, S, Q, normalize):
+    for name, dt, n in sections(B, S, Q, normalize, failures):
         nb = np.dtype(dt).itemsize * n
         d[name] = np.frombuffer(buf[off:off + nb], dtype=dt)
         off += nb

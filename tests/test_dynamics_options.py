@@ -1,0 +1,128 @@
+"""The optional dynamics of DESIGN.md §3.4 / §3.9 on the CPU oracle (their GPU parity is in
+tests/test_gpu_parity.py CONFIGS): lost-FIN flows (VPP's timed-out flow sample,
+src/vpp/lb/lbhash.h:175-217) and server failure / recovery (problem-03 THEORY.md §6.4).
+
+Parity vs the reference is unpinned for both, as for the rest of the flow dynamics (the reference's
+simulation mode has none): these tests pin the oracle's restatement to the semantics it states --
+off means bit-identical, the right flows are changed by the right amount, failed servers are empty,
+ineligible and inactive.
+"""
+import numpy as np
+import pytest
+
+from tests import statelayout
+
+pytest.importorskip("torch")
+
+
+def _run(oracle_mod, B, S, steps, seed=5, **kw):
+    from marllb_amd.env import make_config
+    cfg = make_config(B, S, seed=seed, **kw)
+    ora = oracle_mod.OracleEnv(cfg, threads=4)
+    ora.reset()
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(steps):
+        out.append(ora.step(rng.integers(0, 3, (B, S)).astype(np.int64)))
+    st = statelayout.parse(ora.state_bytes(), B, S, cfg.queue_capacity, False, cfg.fail_prob > 0)
+    ora.close()
+    return st, out
+
+
+def test_options_off_are_bit_identical(oracle_mod):
+    """lost_fin_prob = 0 ignores flow_timeout / flow_buckets and fail_prob = 0 ignores
+    recover_prob: the state and every output equal the default run's."""
+    st0, out0 = _run(oracle_mod, 64, 4, 6)
+    st1, out1 = _run(oracle_mod, 64, 4, 6, flow_timeout=3.0, flow_buckets=7, recover_prob=0.9)
+    for k in st0:
+        np.testing.assert_array_equal(st0[k], st1[k], err_msg=k)
+    for a, b in zip(out0, out1):
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+
+
+def test_lost_fin_changes_only_the_fct_of_lost_flows(oracle_mod):
+    """A lost flow's server-side life is unchanged (same queues, slots, durations, timestamps and
+    counts as the run without losses); only its fct sample becomes VPP's guess fct + flow_timeout
+    - 40 s + wait, wait ~ Exp(flow_buckets / arrival_rate), for the fraction lost_fin_prob of the
+    flows (lbhash.h:191,212 with LB_DEFAULT_FLOW_TIMEOUT = 40, stats.h:27)."""
+    B, S, steps = 96, 4, 10
+    st0, _ = _run(oracle_mod, B, S, steps)
+    for p, timeout, buckets in ((1.0, 40.0, 1024), (0.3, 10.0, 256)):
+        st, _ = _run(oracle_mod, B, S, steps, lost_fin_prob=p, flow_timeout=timeout,
+                     flow_buckets=buckets)
+        for k in ("res_dur", "res_ts", "res_count", "hc", "dropped", "clock", "arr_idx"):
+            np.testing.assert_array_equal(st[k], st0[k], err_msg=k)
+        n = np.minimum(st0["res_count"], 128).reshape(B, S)
+        valid = (np.arange(128)[None, None, :] < n[:, :, None]).reshape(-1)
+        f0 = st0["res_fct"].view(np.int32)[valid].astype(np.int64)
+        f1 = st["res_fct"].view(np.int32)[valid].astype(np.int64)
+        changed = f1 != f0
+        frac = changed.mean()
+        assert abs(frac - p) < 4 * np.sqrt(p * (1 - p) / len(f0)) + 1e-9, (p, frac)
+        wait = (f1 - f0)[changed] - (int(timeout * 1e6) - 40_000_000)
+        mean = buckets / 400.0 * 1e6  # arrival_rate 400 flows/s
+        assert (wait >= 0).all()
+        assert abs(wait.mean() / mean - 1) < 0.05, (wait.mean(), mean)
+        # exponential: P(wait > mean) = 1/e
+        assert abs((wait > mean).mean() - np.exp(-1)) < 0.03
+        if timeout < 40:
+            assert (f1[changed] < 0).mean() > 0.9  # fct - 30 s + a ~0.6 s wait: negative
+
+
+def test_server_failures(oracle_mod):
+    """fail_prob / recover_prob per server and step: the stationary down fraction is
+    fail / (fail + recover); a down server is empty (no queue, no samples: an all-zero
+    observation row, inactive in the reward, env.py:410-413), takes no flows, and its lost queue
+    counts as dropped."""
+    from marllb_amd.env import make_config
+    B, S, steps, pf, pr = 128, 4, 40, 0.1, 0.15
+    cfg = make_config(B, S, seed=11, fail_prob=pf, recover_prob=pr)
+    ora = oracle_mod.OracleEnv(cfg, threads=4)
+    ora.reset()
+    rng = np.random.default_rng(0)
+    down_frac = []
+    dropped_prev = 0
+    for k in range(steps):
+        obs, rew, done, assign = ora.step(rng.integers(0, 3, (B, S)).astype(np.int64))
+        st = statelayout.parse(ora.state_bytes(), B, S, cfg.queue_capacity, False, True)
+        down = st["down"].reshape(B, S).astype(bool)
+        assert (obs[down] == 0).all(), "a down server's row is all zeros"
+        assert (assign[down] == 0).all(), "a down server takes no flows"
+        assert (st["res_count"].reshape(B, S)[down] == 0).all()
+        assert ((st["hc"] >> 16).reshape(B, S)[down] == 0).all()
+        if k >= 15:
+            down_frac.append(down.mean())
+        dropped_prev = int(st["dropped"].sum())
+    ora.close()
+    f = float(np.mean(down_frac))
+    assert abs(f - pf / (pf + pr)) < 0.05, f
+    assert dropped_prev > 0, "failed queues count as dropped"
+
+
+def test_server_failures_reward_uses_active_rows(oracle_mod):
+    """The reward of a step with down servers equals the reference rule over the rows with any
+    column > 0 (env.py:410-413 -> rewards.py compute), evaluated by the library's stateless
+    reward entry point's oracle twin on the returned observation."""
+    from marllb_amd.env import make_config
+    B, S = 64, 6
+    cfg = make_config(B, S, seed=3, fail_prob=0.25, recover_prob=0.2, reward_metric="jain",
+                      reward_field="fct_mean")
+    ora = oracle_mod.OracleEnv(cfg, threads=4)
+    ora.reset()
+    rng = np.random.default_rng(1)
+    some_down = False
+    for _ in range(8):
+        obs, rew, _, _ = ora.step(rng.integers(0, 3, (B, S)).astype(np.int64))
+        active = (obs > 0).any(2)
+        some_down |= bool((~active).any())
+        for b in range(B):
+            x = obs[b, active[b], 1].astype(np.float64)  # fct_mean column
+            if len(x) == 0:
+                want = 0.0
+            else:
+                sv, sq = x.sum(), (x * x).sum()
+                want = 1.0 if sv < 1e-10 or sq < 1e-10 else sv * sv / (len(x) * sq)
+            assert abs(float(rew[b]) - want) <= 1e-6 * max(1.0, abs(want)), (b, rew[b], want)
+    assert some_down
+    ora.close()

@@ -5,6 +5,8 @@ kernels -- checked here on the CPU with the oracle, which follows the same state
   * arrivals dropped because every queue is full;
   * observe's unchanged-reservoir skip: steps in which dynamics wrote no slot of any server of
     an env (observe reuses the cached features) next to steps that wrote many;
+  * negative fct samples (lost-FIN flows with a flow timeout under 40 s) -> the signed sort;
+  * servers down at the end of the failure cases;
   * observe's register-resident path (every reservoir of a 4-server chunk holding >= 8 samples,
     every slot below 2^25 - 1 us), both full (n = 128) and partly filled, next to its general path
     (a reservoir with fewer than 8 samples, or a large sample in the chunk).
@@ -39,7 +41,8 @@ def run_case(oracle_mod, case, steps=12):
     #                                  filled / general path with a big sample / general with n < 8
     for _ in range(steps):
         ora.step(_actions(rng, B, S, c["kw"]))  # the GPU test's action stream
-        st = statelayout.parse(ora.state_bytes(), B, S, cfg.queue_capacity, bool(cfg.normalize_obs))
+        st = statelayout.parse(ora.state_bytes(), B, S, cfg.queue_capacity, bool(cfg.normalize_obs),
+                               cfg.fail_prob > 0)
         max_q = max(max_q, int((st["hc"] >> 16).max()))
         per_server = np.unpackbits(st["chg"].view(np.uint8)).reshape(B, S, 128).sum(2)
         written.append(per_server.sum(1))  # slots written per env (all its servers)
@@ -48,7 +51,8 @@ def run_case(oracle_mod, case, steps=12):
         cnt = st["res_count"].reshape(B, S)
         full = np.pad(cnt >= 128, ((0, 0), (0, pad)), constant_values=True)
         ge8 = np.pad(cnt >= 8, ((0, 0), (0, pad)), constant_values=True)
-        # the kernel's qualification reads all 128 slots (stale words of empty slots included)
+        # the kernel's qualification reads all 128 slots (stale words of empty slots included);
+        # negative (lost-FIN) samples are >= 2^31 as unsigned words
         big = np.maximum(st["res_fct"], st["res_dur"]).reshape(B, S, 128).max(2) >= PACK_LIMIT
         big = np.pad(big, ((0, 0), (0, pad)))
         chg = np.pad(per_server > 0, ((0, 0), (0, pad)))
@@ -57,12 +61,15 @@ def run_case(oracle_mod, case, steps=12):
         paths += [(cc & cf & ~cb).sum(), (cc & c8 & ~cf & ~cb).sum(), (cc & c8 & cb).sum(),
                   (cc & ~c8).sum()]
     run_case.written = np.concatenate(written)
+    run_case.negative = bool((st["res_fct"].view(np.int32) < 0).any())
+    run_case.down = int(st["down"].sum()) if "down" in st else 0
     run_case.paths = paths
     return st, max_q, S
 
 
 def test_parity_cases_cover_rare_paths(oracle_mod):
-    two_pass = overflow = dropped = False
+    two_pass = overflow = dropped = negative = False
+    down = 0
     written = []
     paths = np.zeros(4, np.int64)
     for case in range(len(CONFIGS)):
@@ -72,6 +79,8 @@ def test_parity_cases_cover_rare_paths(oracle_mod):
         dropped |= bool(st["dropped"].sum() > 0)
         written.append(run_case.written)
         paths += run_case.paths
+        negative |= run_case.negative
+        down += run_case.down
     w = np.concatenate(written)
     assert (paths > 20).all(), f"observe paths (register full / register partial / general with a " \
                                f"big sample / general with n < 8): {paths}"
@@ -80,4 +89,6 @@ def test_parity_cases_cover_rare_paths(oracle_mod):
     assert two_pass, "no parity case produces a sample >= 2^25 - 1 us"
     assert overflow, "no parity case queues more flows than the LDS window"
     assert dropped, "no parity case drops arrivals"
+    assert negative, "no parity case records a negative (lost-FIN) fct sample"
+    assert down > 20, "too few servers down at the end of the failure cases"
     assert any(c["kw"].get("_nan_actions") for c in CONFIGS), "no case with NaN SED scores"

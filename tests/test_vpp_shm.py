@@ -196,7 +196,7 @@ def test_gpu_simulator_as_live_vpp(oracle_mod, tmp_path):
                 m = np.arange(128) < cnt[b, s]
                 t = np.where(m, (rec[b, s, :, 2].astype(np.float64) * 1e-3).astype(np.float32), 0)
                 for r in range(2):
-                    v = np.where(m, rec[b, s, :, r].astype(np.float32) * np.float32(1e-6), 0)
+                    v = np.where(m, rec[b, s, :, r].view(np.int32).astype(np.float32) * np.float32(1e-6), 0)
                     np.testing.assert_array_equal(tv[b, s, r, :, 0], t)
                     np.testing.assert_array_equal(tv[b, s, r, :, 1], v.astype(np.float32))
         seqs = pub.publish()
@@ -231,7 +231,7 @@ def _tv_from_oracle_state(st, B, S):
     tv = np.zeros((B, S, 2, 128, 2), np.float32)
     for r in range(2):
         tv[:, :, r, :, 0] = t
-        tv[:, :, r, :, 1] = np.where(m, rec[..., r].astype(np.float32) * np.float32(1e-6),
+        tv[:, :, r, :, 1] = np.where(m, rec[..., r].view(np.int32).astype(np.float32) * np.float32(1e-6),
                                      np.float32(0))
     ts = (st["clock"].astype(np.float64) * 0.25).astype(np.float32)
     return tv, ts
