@@ -325,17 +325,21 @@ def async_groups(args, dev, shard, B, S, common, groups):
 
 def graph_leg(args, dev, shard, B, S, common, kernel_ms):
     """The same workload with one step captured into a torch.cuda.CUDAGraph (hipGraph) and
-    replayed: a fresh env in graph_mode (static buffers, the masked auto-reset launched every
-    step), the random policy's torch.randint (default generator, graph-safe) or the fused policy
-    kernel (Philox step counter on the device) inside the graph.  Same kernels and work per step
+    replayed: a fresh env in graph_mode with static buffers -- the random-policy rollout with
+    next-step auto-reset (the resets run inside the step launches, so the captured step is the
+    eager step's two launches and nothing else), the policy rollouts with the same-step masked
+    auto-reset launched every step -- the random policy's torch.randint (default generator,
+    graph-safe) or the fused policy kernel (Philox step counter on the device) inside the graph.  Same kernels and work per step
     as the eager headline, without the per-launch host path; `gap_ms_per_step` = replayed
     ms/step - the eager kernels' HIP-event averages = what the launches between the kernels
     still cost.  Reported beside `value`, never as it."""
     import torch
     from marllb_amd.env import VecLoadBalanceEnv
     common = dict(common, graph_mode=True)
+    autoreset = "same_step"
     if args.workload == "rollout":
-        env = VecLoadBalanceEnv(B, S, max_steps=10000, **common)
+        autoreset = "next_step"
+        env = VecLoadBalanceEnv(B, S, max_steps=10000, autoreset_mode=autoreset, **common)
         env.reset()
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
@@ -368,7 +372,7 @@ def graph_leg(args, dev, shard, B, S, common, kernel_ms):
     ms = el / args.steps * 1e3
     return {"value": B * args.steps / el, "unit": "env-steps/s", "ms_per_step": ms,
             "kernels_ms_per_step": kernel_ms, "gap_ms_per_step": ms - kernel_ms,
-            "form": "one step captured in a torch.cuda.CUDAGraph, replayed"}
+            "form": "one step captured in a torch.cuda.CUDAGraph, replayed", "autoreset": autoreset}
 
 
 def late_episode(args, env, handle, lib, one_step, rate, B, S, done_steps):

@@ -153,7 +153,13 @@ typedef struct lbsim_config {
    * server takes no flows (as a full one).  fail_prob 0 = off (no state is allocated). */
   float fail_prob;           /* [0, 1], default 0                                            */
   float recover_prob;        /* [0, 1], default 0.1                                          */
-  int32_t reserved[1];
+  /* Next-step auto-reset (gymnasium's NEXT_STEP autoreset mode): lbsim_step resets, in place of
+   * stepping, every env whose previous step returned done (episode step >= max_steps), ignoring
+   * its action; that env's outputs are its reset observation, reward 0, done 0, episode length
+   * and return 0, assignment counts 0.  Inside the step launches: no extra kernel, so a captured
+   * step needs no masked-reset launch; such a handle steps in two launches
+   * (dynamics, observe), not the one-launch forms.  0 = off (the caller resets).             */
+  int32_t next_step_reset;
 } lbsim_config_t;
 
 typedef struct lbsim lbsim_t; /* opaque handle */

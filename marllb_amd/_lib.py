@@ -63,7 +63,7 @@ class LbsimConfig(ctypes.Structure):
         ("flow_buckets", ctypes.c_int32),
         ("fail_prob", ctypes.c_float),
         ("recover_prob", ctypes.c_float),
-        ("reserved", ctypes.c_int32 * 1),
+        ("next_step_reset", ctypes.c_int32),
     ]
 
 

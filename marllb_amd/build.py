@@ -26,6 +26,7 @@ UNITS = [
     ("lbsim_api.hip", [], "api.o"),
     ("lbsim_dyn.hip", ["-DLBSIM_DYN_MODE=0"], "dyn_step.o"),
     ("lbsim_dyn.hip", ["-DLBSIM_DYN_MODE=1"], "dyn_reset.o"),
+    ("lbsim_dyn.hip", ["-DLBSIM_DYN_MODE=2"], "dyn_step_nr.o"),
     ("lbsim_obs.hip", [], "obs.o"),
     ("lbsim_pol.hip", [], "pol.o"),
     ("lbsim_step.hip", [], "step.o"),

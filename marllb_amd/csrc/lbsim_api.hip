@@ -163,6 +163,7 @@ int validate(const lbsim_config_t* c, char* msg, size_t n) {
       return bad("flow_buckets must be >= 1 with flow_buckets / arrival_rate <= 100 s");
   }
   if (!(c->fail_prob >= 0.0f) || !(c->fail_prob <= 1.0f)) return bad("fail_prob must be in [0, 1]");
+  if (c->next_step_reset != 0 && c->next_step_reset != 1) return bad("next_step_reset must be 0 or 1");
   if (!(c->recover_prob >= 0.0f) || !(c->recover_prob <= 1.0f))
     return bad("recover_prob must be in [0, 1]");
   if (c->dyn_mapping == LBSIM_DYN_ENV_PER_LANE && c->num_servers > 16)
@@ -204,6 +205,8 @@ void derive_params(const lbsim_config_t& c, SimParams& p) {
                      ? (float)((double)c.flow_buckets * 1e6 / (double)c.arrival_rate) : 0.0f;
   p.fail_thr = (uint32_t)std::llround((double)c.fail_prob * 16777216.0);
   p.rec_thr = (uint32_t)std::llround((double)c.recover_prob * 16777216.0);
+  p.big_in_step = (p.dt_us >= (int32_t)kPackLimit || p.lf_thr != 0u) ? 1 : 0;
+  p.next_reset = c.next_step_reset ? 1 : 0;
 }
 
 // State sections in snapshot order.
@@ -347,8 +350,12 @@ LaunchCtx ctx(const lbsim_t* h) {
 int launch_dynamics(lbsim_t* h, const void* action, int dtype, int32_t* assign,
                     const uint8_t* mask, int mode, hipStream_t stream) {
   ProfScope ps(h, stream, mode == kModeStep ? 0 : 2);
-  if (mode == kModeStep) launch_dynamics_step(ctx(h), action, dtype, assign, mask, stream);
-  else launch_dynamics_reset(ctx(h), action, dtype, assign, mask, stream);
+  if (mode == kModeStep && h->prm.next_reset)  // next-step auto-reset: done envs reset instead
+    launch_dynamics_step_nr(ctx(h), action, dtype, assign, mask, stream);
+  else if (mode == kModeStep)
+    launch_dynamics_step(ctx(h), action, dtype, assign, mask, stream);
+  else
+    launch_dynamics_reset(ctx(h), action, dtype, assign, mask, stream);
   return launch_check(h, "dynamics_kernel");
 }
 
@@ -398,7 +405,8 @@ bool use_step_wave(const lbsim_t* h) {
     return e ? (int64_t)std::atoll(e) : (int64_t)-1;
   }();
   const LaunchCtx L = ctx(h);
-  if (!dyn_wave_ok(L) || L.S > 8) return false;
+  // next-step auto-reset handles step in two launches (the dynamics' kModeStepNR instantiation)
+  if (!dyn_wave_ok(L) || L.S > 8 || h->prm.next_reset) return false;
   const int64_t per_simd = L.S <= kObsChunk ? 4 : 2;
   if (L.S > kObsChunk && (int64_t)L.B > 2 * (int64_t)L.simds) return false;
   const int k = step_kernel_of(h);
@@ -411,7 +419,7 @@ bool use_step_wave(const lbsim_t* h) {
 // a group width that has a fused form.
 bool use_fused_step(const lbsim_t* h) {
   // AUTO = SPLIT: the fused kernel measured slower at every shape tried
-  if (step_kernel_of(h) != LBSIM_STEP_FUSED) return false;
+  if (step_kernel_of(h) != LBSIM_STEP_FUSED || h->prm.next_reset) return false;
   const int g = dyn_group_lanes(ctx(h));
   return g >= 2 && g <= 16;
 }

@@ -1,18 +1,19 @@
 // lbsim_dyn.hip — dynamics launchers, one object per mode: built with
-// -DLBSIM_DYN_MODE=0 (kModeStep, launch_dynamics_step) and =1 (kModeReset, launch_dynamics_reset)
-// so the two halves of the template instantiations compile in parallel.
+// -DLBSIM_DYN_MODE=0 (kModeStep, launch_dynamics_step), =1 (kModeReset, launch_dynamics_reset)
+// and =2 (kModeStepNR, launch_dynamics_step_nr: the step of a next-step auto-reset handle) so the
+// thirds of the template instantiations compile in parallel.
 #include "lbsim_internal.h"
 #include "lbsim_dyn_group.h"
 #include "lbsim_dyn_wave.h"
 
 #ifndef LBSIM_DYN_MODE
-#error "build with -DLBSIM_DYN_MODE=0 (step) or 1 (reset)"
+#error "build with -DLBSIM_DYN_MODE=0 (step), 1 (reset) or 2 (step with next-step resets)"
 #endif
 
 namespace lbk {
 namespace {
 
-constexpr int MODE = LBSIM_DYN_MODE == 0 ? kModeStep : kModeReset;
+constexpr int MODE = LBSIM_DYN_MODE == 0 ? kModeStep : (LBSIM_DYN_MODE == 1 ? kModeReset : kModeStepNR);
 
 template <int MAXS, int POLICY>
 void launch_dyn(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
@@ -137,6 +138,11 @@ void launch_dynamics_t(const LaunchCtx& L, const void* action, int dtype, int32_
 #if LBSIM_DYN_MODE == 0
 void launch_dynamics_step(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
                           const uint8_t* mask, hipStream_t s) {
+  launch_dynamics_t(L, action, dtype, assign, mask, s);
+}
+#elif LBSIM_DYN_MODE == 2
+void launch_dynamics_step_nr(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
+                             const uint8_t* mask, hipStream_t s) {
   launch_dynamics_t(L, action, dtype, assign, mask, s);
 }
 #else

@@ -117,6 +117,7 @@ __device__ __forceinline__ uint64_t group_bits(uint64_t m, int gbase) {
 struct SrvLane {
   int32_t cnt, head_tc, head, lh, tail, last, assigned;
   int32_t qcap;     // Q, or 0 while the server is down (fail_prob > 0): not eligible, as full
+  bool big;         // the server's sticky kHcBig flag
   uint32_t rcnt;
   uint32_t* chgw;   // LDS [4][64]: word w of this lane's 128-bit mask of the reservoir slots
                     // written this launch (DevState::chg), set by one ds_or per insert
@@ -302,10 +303,11 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
     // ---- the pushed flow's Algorithm R draw is this arrival's word r (E.u3)
     const int slot = reservoir_slot_r32(V.rcnt, E.u3);
     if (ins && slot >= 0) {
-      my_res[(uint32_t)slot] = make_uint3(
-          lost_fct(p, (uint32_t)(tc_a - ta), gc.base_ms * 1000u + gc.base_rem + (uint32_t)ta, E.gid,
-                   E.episode),
-          (uint32_t)svc, gc.base_ms + (gc.base_rem + (uint32_t)tc_a) / 1000u);
+      const uint32_t fct = lost_fct(p, (uint32_t)(tc_a - ta),
+                                    gc.base_ms * 1000u + gc.base_rem + (uint32_t)ta, E.gid, E.episode);
+      if (p.big_in_step) V.big |= big_record(fct, (uint32_t)svc);  // uniform: off by default
+      my_res[(uint32_t)slot] =
+          make_uint3(fct, (uint32_t)svc, gc.base_ms + (gc.base_rem + (uint32_t)tc_a) / 1000u);
       mark(slot);
     }
     if (mine) {
@@ -385,6 +387,7 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
       V.cnt = 0;
       V.last = kLastNone;
       V.rcnt = 0u;
+      V.big = false;
       mark(0);  // emptied: the next observe recomputes the (zero) features
     }
     V.qcap = fails ? 0 : (recovers ? Q : V.qcap);
@@ -402,9 +405,11 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
           u32x4{rc >> 1, E.gid, E.episode, (kStreamReservoir << 24) | (uint32_t)s}, p.key0, p.key1);
       const int slot = reservoir_slot(rc, d);
       if (slot >= 0) {
-        my_res[(uint32_t)slot] = make_uint3(
-            lost_fct(p, (uint32_t)(etc - eta), (uint32_t)base_us + (uint32_t)eta, E.gid, E.episode),
-            (uint32_t)(etc - (eta > prev ? eta : prev)), base_ms + (base_rem + (uint32_t)etc) / 1000u);
+        const uint32_t fct =
+            lost_fct(p, (uint32_t)(etc - eta), (uint32_t)base_us + (uint32_t)eta, E.gid, E.episode);
+        const uint32_t dur = (uint32_t)(etc - (eta > prev ? eta : prev));
+        V.big |= big_record(fct, dur);
+        my_res[(uint32_t)slot] = make_uint3(fct, dur, base_ms + (base_rem + (uint32_t)etc) / 1000u);
         mark(slot);
       }
       prev = etc;
@@ -514,7 +519,7 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
   float wall[G];
   float w_own = 1.0f;
 
-  if (MODE == kModeReset) {
+  auto reset_in = [&]() {  // a new episode (env.py:186-213): its first arrival, empty servers
     E.episode = st.episode[b] + 1u;
     E.clock = 0u;
     E.dropped = 0u;
@@ -527,15 +532,11 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
     V.last = kLastNone;
     V.rcnt = 0u;
     V.qcap = Q;  // every server is up at the episode start
+    V.big = false;
 #pragma unroll
     for (int k = 0; k < G; ++k) wall[k] = 1.0f;
-    for (int k = 0; k < p.warmup_steps; ++k)
-      sim_step_group<G, POLICY, TRACE>(st, p, E, V, b, s, gbase, 1.0f, wall, win, atab, acache);
-    if (s == 0) {
-      st.ep_step[b] = 0;
-      st.ep_return[b] = 0.0;
-    }
-  } else {
+  };
+  auto load_in = [&]() {  // the env and this lane's server from HBM, the step's weights
     E.episode = st.episode[b];
     E.clock = st.clock[b];
     E.dropped = st.dropped[b];
@@ -551,10 +552,12 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
     V.last = kLastNone;
     V.rcnt = 0u;
     V.qcap = Q;
+    V.big = false;
     if (V.act) {
       if (st.down != nullptr && st.down[sb] != 0u) V.qcap = 0;
       const uint32_t hc = st.hc[sb];
-      V.head = (int)(hc & 0xFFFFu);
+      V.head = (int)(hc & kHcHead);
+      V.big = (hc & kHcBig) != 0u;
       V.cnt = (int32_t)(hc >> 16);
       V.last = st.last_tc[sb];
       V.rcnt = st.res_count[sb];
@@ -576,7 +579,36 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
       for (int k = 0; k < G; ++k)
         wall[k] = k < S ? action_weight(p, action, action_dtype, (size_t)b * S + (size_t)k) : 1.0f;
     }
+  };
+  auto reset_out = [&](int32_t ep_step) {  // episode counters; the warm-up's assignments are not
+    V.assigned = 0;                        // the step's
+    if (s == 0) {
+      st.ep_step[b] = ep_step;
+      st.ep_return[b] = 0.0;
+    }
+  };
+  if constexpr (MODE == kModeStep) {
+    load_in();
     sim_step_group<G, POLICY, TRACE>(st, p, E, V, b, s, gbase, w_own, wall, win, atab, acache);
+  } else if constexpr (MODE == kModeReset) {
+    reset_in();
+    for (int k = 0; k < p.warmup_steps; ++k)
+      sim_step_group<G, POLICY, TRACE>(st, p, E, V, b, s, gbase, 1.0f, wall, win, atab, acache);
+    reset_out(0);
+  } else {
+    // kModeStepNR (next-step auto-reset): an env whose last step returned done resets in place of
+    // stepping (its action ignored; ep_step = -1 tells the observe to report the reset).  Two call
+    // sites (113 VGPRs; one loop over both took 130, 3 waves per SIMD); a wave runs the branches
+    // of its groups one after the other, each with only its groups active.
+    if (st.ep_step[b] >= p.max_steps) {
+      reset_in();
+      for (int k = 0; k < p.warmup_steps; ++k)
+        sim_step_group<G, POLICY, TRACE>(st, p, E, V, b, s, gbase, 1.0f, wall, win, atab, acache);
+      reset_out(-1);
+    } else {
+      load_in();
+      sim_step_group<G, POLICY, TRACE>(st, p, E, V, b, s, gbase, w_own, wall, win, atab, acache);
+    }
   }
 
   // ---- this lane's server back to HBM (window into the ring), then the env words (lane 0)
@@ -588,13 +620,13 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
       li = li >= WL ? li - WL : li;
       st.ring[sb * (uint32_t)Q + (uint32_t)pos] = win[li * 64 + lane];
     }
-    st.hc[sb] = (uint32_t)V.head | ((uint32_t)V.cnt << 16);
+    st.hc[sb] = (uint32_t)V.head | (V.big ? kHcBig : 0u) | ((uint32_t)V.cnt << 16);
     st.last_tc[sb] = V.last;
     st.res_count[sb] = V.rcnt;
     if (st.down != nullptr) st.down[sb] = V.qcap == 0 ? 1u : 0u;
     *reinterpret_cast<uint4*>(st.chg + (size_t)sb * 4) =
         make_uint4(chgw[lane], chgw[64 + lane], chgw[128 + lane], chgw[192 + lane]);
-    if (MODE != kModeReset && assign_out != nullptr) assign_out[sb] = V.assigned;
+    if (MODE != kModeReset && assign_out != nullptr) assign_out[sb] = V.assigned;  // 0 if reset
   }
   if (s == 0) {
     st.episode[b] = E.episode;

@@ -91,6 +91,7 @@ struct WaveLds {
   int2 img[32 * kWaveMaxS];       // ring image [pos][server] for the carried-in walk and `last`
   uint32_t own[kWaveMaxS * 128];  // insert owner of each (server, slot) in a flush: seq << 6 | lane
   uint32_t chg[4 * kWaveMaxS];    // written-slot masks [word][server]
+  uint32_t big[kWaveMaxS];        // the servers' sticky kHcBig flags
 };
 // Server lanes a reduction / key table covers: 4 for NG <= 2 (S <= 4), 8 for NG = 4 (S <= 8).
 template <int NG>
@@ -199,9 +200,10 @@ __device__ __forceinline__ void wave_flush(const SimParams& p, WaveSrv& V, WaveE
   if (slot >= 0 && Ld.own[key] == me_tag) {
     int32_t svc = (int32_t)(Bt.wk * scale);
     svc = svc < 1 ? 1 : svc;
-    res_b[key] = make_uint3(lost_fct(p, (uint32_t)(Bt.ltc - Bt.ta),
-                                     base_ms * 1000u + base_rem + (uint32_t)Bt.ta, E.gid, E.episode),
-                            (uint32_t)svc, base_ms + (base_rem + (uint32_t)Bt.ltc) / 1000u);
+    const uint32_t fct = lost_fct(p, (uint32_t)(Bt.ltc - Bt.ta),
+                                  base_ms * 1000u + base_rem + (uint32_t)Bt.ta, E.gid, E.episode);
+    if (p.big_in_step && big_record(fct, (uint32_t)svc)) atomicOr(&Ld.big[Bt.lc], 1u);  // rare
+    res_b[key] = make_uint3(fct, (uint32_t)svc, base_ms + (base_rem + (uint32_t)Bt.ltc) / 1000u);
   }
 }
 
@@ -453,9 +455,12 @@ __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParam
           p.key1);
       const int slot = reservoir_slot(rc, d);
       if (slot >= 0) {
-        res_b[(uint32_t)lane * K + (uint32_t)slot] = make_uint3(
-            lost_fct(p, (uint32_t)(e.x - e.y), (uint32_t)base_us + (uint32_t)e.y, E.gid, E.episode),
-            (uint32_t)(e.x - (e.y > prev ? e.y : prev)), base_ms + (base_rem + (uint32_t)e.x) / 1000u);
+        const uint32_t fct =
+            lost_fct(p, (uint32_t)(e.x - e.y), (uint32_t)base_us + (uint32_t)e.y, E.gid, E.episode);
+        const uint32_t dur = (uint32_t)(e.x - (e.y > prev ? e.y : prev));
+        if (big_record(fct, dur)) Ld.big[lane] = 1u;  // this lane's own server
+        res_b[(uint32_t)lane * K + (uint32_t)slot] =
+            make_uint3(fct, dur, base_ms + (base_rem + (uint32_t)e.x) / 1000u);
         atomicOr(Ld.chg + ((uint32_t)slot >> 5) * kWaveMaxS + (uint32_t)lane, 1u << (slot & 31));
       }
       prev = e.x;
@@ -534,6 +539,7 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
   V.assigned = 0;
   V.saved = 0;
   if (lane < 4 * kWaveMaxS) Ld.chg[lane] = 0u;
+  if (lane < kWaveMaxS) Ld.big[lane] = 0u;
 #pragma unroll
   for (int i = 0; i < kWaveMaxS * 128 / 64; ++i) Ld.own[i * 64 + lane] = 0u;
   uint32_t seq = 1u;
@@ -545,7 +551,8 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
   }
   const uint32_t sb = b * (uint32_t)S + (uint32_t)lane;  // server lane's server (lane < S)
 
-  if (MODE == kModeReset) {
+  float w_own = 1.0f;
+  auto reset_in = [&]() {  // a new episode (env.py:186-213): its first arrival, empty servers
     E.episode = st.episode[b] + 1u;
     E.clock = 0u;
     E.dropped = 0u;
@@ -573,14 +580,8 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
     V.tail = 0;
     V.last = kLastNone;
     V.rcnt = 0u;
-    wave_sync();
-    for (int k = 0; k < p.warmup_steps; ++k)
-      sim_step_wave<NG, POLICY, TRACE, VC>(st, p, E, V, R, lane, res_b, Ld, seq, 1.0f);
-    if (lane == 0) {
-      st.ep_step[b] = 0;
-      st.ep_return[b] = 0.0;
-    }
-  } else {
+  };
+  auto load_in = [&]() {  // the env, its ring lanes and server fields from HBM, the step's weight
     E.episode = st.episode[b];
     E.clock = st.clock[b];
     E.dropped = st.dropped[b];
@@ -596,7 +597,7 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
       if (srv < S && rpos < Q) {  // the slot and its server's head / count, loaded together
         const int2 e = st.ring[(size_t)(b * (uint32_t)S + (uint32_t)srv) * (size_t)Q + rpos];
         const uint32_t hc = st.hc[b * (uint32_t)S + (uint32_t)srv];
-        const int head = (int)(hc & 0xFFFFu), cnt = (int)(hc >> 16);
+        const int head = (int)(hc & kHcHead), cnt = (int)(hc >> 16);
         int rel = rpos - head;
         rel = rel < 0 ? rel + Q : rel;
         R.tc[g] = rel < cnt ? e.x : kDead;
@@ -608,11 +609,11 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
     V.tail = 0;
     V.last = kLastNone;
     V.rcnt = 0u;
-    float w_own = 1.0f;
     if (V.act) {
       const uint32_t hc = st.hc[sb];
-      const int head = (int)(hc & 0xFFFFu);
+      const int head = (int)(hc & kHcHead);
       V.cnt0 = (int32_t)(hc >> 16);
+      Ld.big[lane] = (hc & kHcBig) ? 1u : 0u;
       const int wp = head + V.cnt0;
       V.wp = wp >= Q ? wp - Q : wp;
       V.last = st.last_tc[sb];
@@ -630,8 +631,37 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
       }
       V.tail = (V.act && V.cnt0 > 0) ? tl : 0;
     }
+  };
+  auto reset_out = [&](int32_t ep_step) {
+    V.assigned = 0;  // the warm-up's assignments are not the step's
+    if (lane == 0) {
+      st.ep_step[b] = ep_step;
+      st.ep_return[b] = 0.0;
+    }
+  };
+  if constexpr (MODE == kModeStep) {
+    load_in();
     wave_sync();
     sim_step_wave<NG, POLICY, TRACE, VC>(st, p, E, V, R, lane, res_b, Ld, seq, w_own);
+  } else if constexpr (MODE == kModeReset) {
+    reset_in();
+    wave_sync();
+    for (int k = 0; k < p.warmup_steps; ++k)
+      sim_step_wave<NG, POLICY, TRACE, VC>(st, p, E, V, R, lane, res_b, Ld, seq, 1.0f);
+    reset_out(0);
+  } else {  // kModeStepNR: an env done last step resets in place of stepping (ep_step = -1)
+    const bool rs = st.ep_step[b] >= p.max_steps;
+    int nsim = 1;
+    if (rs) {
+      reset_in();
+      nsim = p.warmup_steps;
+    } else {
+      load_in();
+    }
+    wave_sync();
+    for (int k = 0; k < nsim; ++k)
+      sim_step_wave<NG, POLICY, TRACE, VC>(st, p, E, V, R, lane, res_b, Ld, seq, w_own);
+    if (rs) reset_out(-1);
   }
 
   // ---- state out: the queued flows, the server fields, the env words
@@ -646,7 +676,7 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
   if (V.act) {
     int head = V.wp - V.cnt0;
     head = head < 0 ? head + Q : head;
-    st.hc[sb] = (uint32_t)head | ((uint32_t)V.cnt0 << 16);
+    st.hc[sb] = (uint32_t)head | (Ld.big[lane] ? kHcBig : 0u) | ((uint32_t)V.cnt0 << 16);
     st.last_tc[sb] = V.last;
     st.res_count[sb] = V.rcnt;
     *reinterpret_cast<uint4*>(st.chg + (size_t)sb * 4) =

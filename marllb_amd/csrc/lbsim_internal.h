@@ -91,6 +91,9 @@ void launch_dynamics_step(const LaunchCtx& L, const void* action, int dtype, int
                           const uint8_t* mask, hipStream_t s);
 void launch_dynamics_reset(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
                            const uint8_t* mask, hipStream_t s);
+// The step of a next-step auto-reset handle (kModeStepNR): envs done last step reset instead.
+void launch_dynamics_step_nr(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
+                             const uint8_t* mask, hipStream_t s);
 
 void launch_observe_step(const LaunchCtx& L, const ObsOutputs& o, const uint8_t* mask,
                          hipStream_t s);

@@ -31,6 +31,10 @@ constexpr int kModeStep = 0;
 // s_waitcnt immediate with vmcnt = 0 and expcnt/lgkmcnt left at their maxima (gfx9 encoding).
 constexpr int kWaitVmcnt0 = 0x0F70;
 constexpr int kModeReset = 1;
+// A step launch of a handle with next-step auto-reset (lbsim_config_t::next_step_reset): the
+// dynamics reset, in place of stepping, the envs whose last step returned done.  A separate
+// instantiation, so the default step kernels carry none of the reset code.
+constexpr int kModeStepNR = 2;
 
 struct DevState {
   // per env [B]
@@ -103,9 +107,29 @@ struct SimParams {
   float lf_wait_us;
   // server failure / recovery (fail_transitions): 24-bit thresholds per server-step (fail 0 = off)
   uint32_t fail_thr, rec_thr;
+  // a flow that arrives and completes in one step can store a sample >= kPackLimit (the kHcBig
+  // flag then needs tracking inside the event loop): only with dt >= kPackLimit us or lost-FIN
+  // guesses (an in-step fct is <= dt and its duration <= its fct otherwise)
+  int32_t big_in_step;
+  // next-step auto-reset (lbsim_config_t::next_step_reset): a step launch resets the envs whose
+  // last step returned done (ep_step >= max_steps) instead of stepping them
+  int32_t next_reset;
 };
 
 constexpr uint32_t kStreamFailure = 5u;  // Philox stream of the failure / recovery draws
+
+// us << 7 | slot must stay below the 0xFFFFFFFF filler of empty slots (observe's one-pass sort).
+constexpr uint32_t kPackLimit = (1u << 25) - 1u;
+// DevState::hc = ring head | kHcBig | count << 16 (head < Q <= 64).  kHcBig is sticky: a record
+// with a sample >= kPackLimit us (as an unsigned word: negative lost-FIN guesses included) was
+// stored in the server's reservoirs since they were last emptied (reset, failure).  Observe's
+// register-resident path (one-pass sort of us << 7 | slot) needs every sample below kPackLimit;
+// the flag lets it decide from the hc word it loads anyway, without a pass over the records.
+constexpr uint32_t kHcBig = 1u << 15;
+constexpr uint32_t kHcHead = kHcBig - 1u;
+__device__ __forceinline__ bool big_record(uint32_t fct, uint32_t dur) {
+  return (fct > dur ? fct : dur) >= kPackLimit;
+}
 
 // murmur3's 32-bit finaliser (fmix32): the lost-FIN hash.
 __device__ __forceinline__ uint32_t lf_mix(uint32_t h) {
@@ -193,6 +217,7 @@ struct LaneState {
   uint32_t u2, u3, arr_idx, episode, clock, dropped;
   uint32_t gid;
   uint32_t downm;         // bit s: server s is down (fail_prob > 0), not eligible as a full one
+  uint32_t bigm;          // bit s: server s's kHcBig flag
   // TRACE: row of arrival arr_idx + 1 and its prefetched gap / work (loaded an arrival ahead so
   // the event loop never waits on the trace)
   uint32_t row;
@@ -374,6 +399,7 @@ __device__ __forceinline__ void load_servers(const DevState& st, const SimParams
                                              LaneState<MAXS>& L, uint32_t b, const Lds& l) {
   constexpr int WL = LaneState<MAXS>::WL;
   L.downm = 0u;
+  L.bigm = 0u;
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) {
     L.cnt[s] = 0;
@@ -384,9 +410,10 @@ __device__ __forceinline__ void load_servers(const DevState& st, const SimParams
     if (s < p.S) {
       const uint32_t sb = b * (uint32_t)p.S + (uint32_t)s;
       const uint32_t hc = st.hc[sb];
-      const int head = (int)(hc & 0xFFFFu);
+      const int head = (int)(hc & kHcHead);
       L.cnt[s] = (int32_t)(hc >> 16);
       L.head[s] = head;
+      L.bigm |= (hc & kHcBig) ? 1u << s : 0u;
       if (st.down != nullptr && st.down[sb] != 0u) L.downm |= 1u << s;
       L.last[s] = st.last_tc[sb];
       fld<MAXS>(l, F_RCNT, s) = (int32_t)st.res_count[sb];
@@ -415,6 +442,7 @@ template <int MAXS>
 __device__ __forceinline__ void clear_servers(const SimParams& p, LaneState<MAXS>& L,
                                               const Lds& l) {
   L.downm = 0u;  // every server is up at the episode start
+  L.bigm = 0u;
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) {
     L.cnt[s] = 0;
@@ -700,10 +728,11 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
                               ec.rk0, ec.rk1);
     const int slot = reservoir_slot_r32(cres, L.u3);
     if (ins && slot >= 0) {
-      my_res[(uint32_t)cs * (uint32_t)K + (uint32_t)slot] = make_uint3(
-          lost_fct(p, (uint32_t)(tc_a - ta), ec.base_ms * 1000u + ec.base_rem + (uint32_t)ta, L.gid,
-                   L.episode),
-          (uint32_t)svc, ec.base_ms + (ec.base_rem + (uint32_t)tc_a) / 1000u);
+      const uint32_t fct = lost_fct(p, (uint32_t)(tc_a - ta),
+                                    ec.base_ms * 1000u + ec.base_rem + (uint32_t)ta, L.gid, L.episode);
+      if (p.big_in_step) L.bigm |= big_record(fct, (uint32_t)svc) ? 1u << cs : 0u;
+      my_res[(uint32_t)cs * (uint32_t)K + (uint32_t)slot] =
+          make_uint3(fct, (uint32_t)svc, ec.base_ms + (ec.base_rem + (uint32_t)tc_a) / 1000u);
       mark_slot<MAXS>(l, cs, slot);
     }
     // queue index < WL: the LDS window (a push that does not happen writes the lane's scratch
@@ -850,6 +879,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
         if (u < p.rec_thr) L.downm &= ~(1u << s);
       } else if (u < p.fail_thr) {
         L.downm |= 1u << s;
+        L.bigm &= ~(1u << s);
 #pragma unroll
         for (int k = 0; k < MAXS; ++k) {  // register arrays: constant indices only
           if (k == s) {
@@ -879,9 +909,12 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
             u32x4{rc >> 1, L.gid, L.episode, (kStreamReservoir << 24) | (uint32_t)s}, p.key0, p.key1);
         const int slot = reservoir_slot(rc, d);
         if (slot >= 0) {
-          my_res[(uint32_t)s * (uint32_t)K + (uint32_t)slot] = make_uint3(
-              lost_fct(p, (uint32_t)(etc - eta), (uint32_t)base_us + (uint32_t)eta, L.gid, L.episode),
-              (uint32_t)(etc - (eta > prev ? eta : prev)), base_ms + (base_rem + (uint32_t)etc) / 1000u);
+          const uint32_t fct =
+              lost_fct(p, (uint32_t)(etc - eta), (uint32_t)base_us + (uint32_t)eta, L.gid, L.episode);
+          const uint32_t dur = (uint32_t)(etc - (eta > prev ? eta : prev));
+          L.bigm |= big_record(fct, dur) ? 1u << s : 0u;
+          my_res[(uint32_t)s * (uint32_t)K + (uint32_t)slot] =
+              make_uint3(fct, dur, base_ms + (base_rem + (uint32_t)etc) / 1000u);
           mark_slot<MAXS>(l, s, slot);
         }
         prev = etc;
@@ -965,7 +998,7 @@ __device__ __forceinline__ void store_servers(const DevState& st, const SimParam
         li = li >= WL ? li - WL : li;
         st.ring[sb * (uint32_t)p.Q + (uint32_t)pos] = *qslot<MAXS>(l, s, li);
       }
-      st.hc[sb] = (uint32_t)head | ((uint32_t)L.cnt[s] << 16);
+      st.hc[sb] = (uint32_t)head | ((L.bigm >> s) & 1u ? kHcBig : 0u) | ((uint32_t)L.cnt[s] << 16);
       st.last_tc[sb] = L.last[s];
       st.res_count[sb] = (uint32_t)fld<MAXS>(l, F_RCNT, s);
       if (st.down != nullptr) st.down[sb] = (L.downm >> s) & 1u;
@@ -1021,8 +1054,9 @@ __global__ void __launch_bounds__(64 * kDynWaves<MAXS>)
   LaneState<MAXS> L;
   L.gid = p.env_id_offset + b;
 
-  if (mode == kModeReset) {
-    if (reset_mask != nullptr && reset_mask[b] == 0) return;
+  if (mode == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
+  float w[MAXS];
+  auto reset_in = [&]() {  // a new episode (env.py:186-213): its first arrival, empty servers
     L.episode = st.episode[b] + 1u;
     L.clock = 0u;
     L.dropped = 0u;
@@ -1030,14 +1064,10 @@ __global__ void __launch_bounds__(64 * kDynWaves<MAXS>)
     draw_arrival<MAXS>(st, p, L, 0);
     trace_prefetch<MAXS>(st, p, L);
     clear_servers<MAXS>(p, L, l);
-    float w1[MAXS];
 #pragma unroll
-    for (int s = 0; s < MAXS; ++s) w1[s] = 1.0f;
-    for (int k = 0; k < p.warmup_steps; ++k) sim_step<MAXS, POLICY, TRACE>(st, p, L, b, w1, l);
-    st.ep_step[b] = 0;
-    st.ep_return[b] = 0.0;
-    store_servers<MAXS>(st, p, L, b, l, nullptr);
-  } else {
+    for (int s = 0; s < MAXS; ++s) w[s] = 1.0f;
+  };
+  auto load_in = [&]() {  // the env and its servers from HBM, the step's weights
     L.episode = st.episode[b];
     L.clock = st.clock[b];
     L.dropped = st.dropped[b];
@@ -1048,13 +1078,34 @@ __global__ void __launch_bounds__(64 * kDynWaves<MAXS>)
     L.u3 = st.next_u3[b];
     trace_prefetch<MAXS>(st, p, L);
     load_servers<MAXS>(st, p, L, b, l);
-    float w[MAXS];
 #pragma unroll
     for (int s = 0; s < MAXS; ++s)
       w[s] = (s < S) ? action_weight(p, action, action_dtype, (size_t)b * S + (size_t)s) : 1.0f;
+  };
+  auto reset_out = [&](int32_t ep_step) {
+    st.ep_step[b] = ep_step;
+    st.ep_return[b] = 0.0;
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) fld<MAXS>(l, F_ASSIGNED, s) = 0;  // not the warm-up's
+  };
+  if constexpr (mode == kModeStep) {
+    load_in();
     sim_step<MAXS, POLICY, TRACE>(st, p, L, b, w, l);
-    store_servers<MAXS>(st, p, L, b, l, assign_out);
+  } else if constexpr (mode == kModeReset) {
+    reset_in();
+    for (int k = 0; k < p.warmup_steps; ++k) sim_step<MAXS, POLICY, TRACE>(st, p, L, b, w, l);
+    reset_out(0);
+  } else {  // kModeStepNR: an env done last step resets in place of stepping (ep_step = -1)
+    if (st.ep_step[b] >= p.max_steps) {
+      reset_in();
+      for (int k = 0; k < p.warmup_steps; ++k) sim_step<MAXS, POLICY, TRACE>(st, p, L, b, w, l);
+      reset_out(-1);
+    } else {
+      load_in();
+      sim_step<MAXS, POLICY, TRACE>(st, p, L, b, w, l);
+    }
   }
+  store_servers<MAXS>(st, p, L, b, l, mode == kModeReset ? nullptr : assign_out);
   st.episode[b] = L.episode;
   st.clock[b] = L.clock;
   st.dropped[b] = L.dropped;
@@ -1329,8 +1380,6 @@ __device__ __forceinline__ float sample_value(uint32_t raw) {
   else return __uint_as_float(raw);
 }
 
-// us << 7 | slot must stay below the 0xFFFFFFFF filler of empty slots.
-constexpr uint32_t kPackLimit = (1u << 25) - 1u;
 
 // p90 of a full reservoir (numpy 'linear', float32 virtual index (K - 1) * 0.9f): sorted
 // positions 114 and 115, both in lane 7 of the sorting group (sorted position 16 t + e).
@@ -1556,33 +1605,19 @@ __device__ __forceinline__ void observe_chunk_regs(const DevState& st, const Sim
 // and every sample below kPackLimit (else false: the general path; reservoirs with n < 8 sum
 // sequentially in numpy, samples >= 2^25 - 1 us need the two-pass sort).  FULL (all n = K, the
 // steady state) is a wave-uniform choice.
+// rc / hcw: res_count and hc of the lane's server s_base + (lane >> 4), loaded by the caller
+// together with the written-slot masks (one round trip for the three).
 template <bool INC>
 __device__ __forceinline__ bool observe_chunk_full(const DevState& st, const SimParams& p, size_t b,
                                                    int s_base, int S, ObsScratch& sc,
-                                                   float* obs_out, int lane) {
-  const size_t srow = b * (size_t)p.S + (size_t)s_base;
-  const int g = lane >> 3, j = lane & 7, u = g >> 1, r = g & 1;
-  const bool act = u < S;
-  const size_t sb = srow + (size_t)(act ? u : 0);
-  const uint32_t rc = st.res_count[sb];
+                                                   float* obs_out, int lane, uint32_t rc,
+                                                   uint32_t hcw) {
+  const bool act = (lane >> 4) < S;
   const int n = rc < (uint32_t)K ? (int)rc : K;
-  if (__any(act && n < 8)) return false;
+  // a reservoir with fewer than 8 samples, or one that ever stored a sample >= kPackLimit since it
+  // was emptied (the sticky kHcBig flag the dynamics set): the general path
+  if (__any(act && (n < 8 || (hcw & kHcBig) != 0u))) return false;
   const bool full = !__any(act && n < K);
-  {
-    // qualification pass; its loads are dropped and re-issued (L1/L2 hits) so that no value stays
-    // live across the branch into the general path (which would spill at 96 VGPRs).  Empty slots
-    // (stale words of an earlier episode) are not masked: a stale sample >= 2^25 - 1 us only sends
-    // a partly filled chunk to the general path, which is exact for every input.
-    const uint32_t* rec = reinterpret_cast<const uint32_t*>(st.res + sb * K + (size_t)j);
-    uint32_t vmax = 0;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const uint32_t v = rec[24 * e + r];
-      vmax = v > vmax ? v : vmax;
-    }
-    if (__any(act && vmax >= kPackLimit)) return false;
-    __asm__ volatile("" ::: "memory");
-  }
   if (full) observe_chunk_regs<INC, true>(st, p, b, s_base, S, K, sc, obs_out, lane);
   else observe_chunk_regs<INC, false>(st, p, b, s_base, S, n, sc, obs_out, lane);
   return true;
@@ -1594,16 +1629,26 @@ __device__ __forceinline__ bool observe_chunk_full(const DevState& st, const Sim
 // INC (step mode with state): a chunk none of whose reservoirs this step's dynamics wrote
 // (DevState::chg all zero) takes its features from DevState::fcache instead of recomputing them;
 // every computed chunk refreshes the cache (US: reset and step modes).
+// fresh: the env was reset by this step (next-step auto-reset): every chunk is recomputed (the
+// cached features are the previous episode's).
 template <bool US, bool INC>
 __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParams& p, size_t b,
                                               int s_base, int S, ObsScratch& sc, float* obs_out,
-                                              int lane) {
+                                              int lane, bool fresh = false) {
   const size_t srow = b * (size_t)p.S + (size_t)s_base;  // first (env, server) of the chunk
   const int R = 2 * S;
   const int g = lane >> 3, j = lane & 7;
+  // the register path's decision words, issued with the written-slot masks (no round trip of
+  // their own after the unchanged-chunk test)
+  uint32_t rc = 0u, hcw = 0u;
+  if constexpr (US) {
+    const size_t usb = srow + (size_t)((lane >> 4) < S ? (lane >> 4) : 0);
+    rc = st.res_count[usb];
+    hcw = st.hc[usb];
+  }
   if constexpr (INC) {
     const uint32_t w = lane < 4 * S ? st.chg[(srow + (size_t)(lane >> 2)) * 4 + (lane & 3)] : 0u;
-    if (!__any(w != 0u)) {  // no reservoir of the chunk changed: the cached features
+    if (!fresh && !__any(w != 0u)) {  // no reservoir of the chunk changed: the cached features
       for (int e = lane; e < S * NF; e += 64) {
         const int s = e / NF, c = e - s * NF;
         obs_out[s_base * NF + e] = c == 0 ? (float)(st.hc[srow + (size_t)s] >> 16)
@@ -1614,7 +1659,7 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
     }
   }
   if constexpr (US) {
-    if (observe_chunk_full<INC>(st, p, b, s_base, S, sc, obs_out, lane)) return;
+    if (observe_chunk_full<INC>(st, p, b, s_base, S, sc, obs_out, lane, rc, hcw)) return;
   }
   // ---- phase 1: reservoirs into LDS, decay weights relative to each server's newest sample.
   //      Loads of 4 servers are issued before any is consumed (memory-level parallelism).
@@ -2007,7 +2052,9 @@ __device__ __forceinline__ void observe_outputs(const DevState& st, const SimPar
     if (MODE == kModeStep && lane == 0) {
       const int na = __popcll(act_mask);
       double r = 0.0;
-      if (fok) {
+      // reset by this step (next-step auto-reset, ep_step = -1): reward 0, episode step 0, not done
+      const bool fresh = p.next_reset && st.ep_step[b] < 0;
+      if (fok && !fresh) {
         // (compile-time for observe_kernel<4>; fused G = 8 with S <= 4 at run time)
         if ((MAXS <= kObsChunk || S <= kObsChunk) && p.reward_metric == 0)
           r = jain_upto4(na, s_act);
@@ -2015,8 +2062,8 @@ __device__ __forceinline__ void observe_outputs(const DevState& st, const SimPar
           r = reward_values(na, [&](int i) { return (double)s_act[i]; }, p.reward_metric);
       }
       out.reward[b] = (float)r;
-      const int32_t es = st.ep_step[b] + 1;
-      const double er = st.ep_return[b] + r;
+      const int32_t es = st.ep_step[b] + 1;  // -1 + 1 = 0 for a fresh env
+      const double er = st.ep_return[b] + r;  // 0 + 0
       st.ep_step[b] = es;
       st.ep_return[b] = er;
       out.done[b] = (uint8_t)(es >= p.max_steps ? 1 : 0);
@@ -2095,8 +2142,9 @@ __global__ void __launch_bounds__(64 * kObsWavesPerEnv<MAXS>, 5)
   const int S = p.S;
   {
     const int s0 = wv * kObsChunk;  // the launch has ceil(S / 4) waves
+    const bool fresh = mode == kModeStep && p.next_reset && st.ep_step[b] < 0;
     observe_chunk<true, mode == kModeStep>(st, p, b, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk,
-                                           sc, s_obs, lane);
+                                           sc, s_obs, lane, fresh);
   }
   __syncthreads();
   observe_outputs<MAXS, MODE, FAC>(st, p, out, b, s_obs, s_act, tid, nthr);
@@ -2118,8 +2166,9 @@ __global__ void __launch_bounds__(64, 5)
   if (MODE == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
   __shared__ ObsScratch sc;
   const int S = p.S, s0 = c * kObsChunk, lane = (int)threadIdx.x;
+  const bool fresh = MODE == kModeStep && p.next_reset && st.ep_step[b] < 0;
   observe_chunk<true, MODE == kModeStep>(st, p, b, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk,
-                                         sc, out.obs + b * (size_t)S * NF, lane);
+                                         sc, out.obs + b * (size_t)S * NF, lane, fresh);
 }
 
 template <int MAXS, int MODE, bool FAC>
@@ -2142,12 +2191,13 @@ __device__ __forceinline__ void observe_env_wave(const DevState& st, const SimPa
                                                  const ObsOutputs& out, size_t b, ObsScratch& sc,
                                                  float* s_obs, float* s_act, int lane) {
   const int S = p.S;
+  const bool fresh = p.next_reset && st.ep_step[b] < 0;
   if constexpr (MAXS <= kObsChunk) {  // one chunk: straight-line code, no loop-carried s0
-    observe_chunk<true, true>(st, p, b, 0, S, sc, s_obs, lane);
+    observe_chunk<true, true>(st, p, b, 0, S, sc, s_obs, lane, fresh);
   } else {
     for (int s0 = 0; s0 < S; s0 += kObsChunk)
       observe_chunk<true, true>(st, p, b, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk, sc, s_obs,
-                                lane);
+                                lane, fresh);
   }
   observe_outputs<MAXS, kModeStep, true>(st, p, out, b, s_obs, s_act, lane, 64);
   wave_sync();  // s_obs / s_act reused by the next env

@@ -104,7 +104,8 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
                 assign_policy: str = "sed", trace=None,
                 dyn_mapping: str = "auto", step_kernel: str = "auto",
                 lost_fin_prob: float = 0.0, flow_timeout: float = 40.0, flow_buckets: int = 1024,
-                fail_prob: float = 0.0, recover_prob: float = 0.1) -> _lib.LbsimConfig:
+                fail_prob: float = 0.0, recover_prob: float = 0.1,
+                next_step_reset: bool = False) -> _lib.LbsimConfig:
     """Build and validate an lbsim_config_t from reference-style kwargs.
 
     server_rates defaults to identical servers at utilisation `load`: mu = rate / (load * S).
@@ -120,6 +121,8 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
     mean wait for the next flow in the bucket.  0 = off.
     fail_prob / recover_prob: per server and step, an up server fails (its queue and reservoirs are
     lost) and a down one recovers (THEORY.md §6.4 server_failure ~ Bernoulli(p_fail)).  0 = off.
+    next_step_reset: lbsim_step resets, in place of stepping, the envs whose last step returned
+    done (gymnasium's NEXT_STEP autoreset; VecLoadBalanceEnv(autoreset_mode="next_step")).
     """
     if reward_metric not in _lib.METRICS:  # rewards.py:321-323
         raise ValueError(f"Unsupported metric: {reward_metric}. Supported: {_lib.METRICS}")
@@ -173,6 +176,7 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
     cfg.flow_buckets = int(flow_buckets)
     cfg.fail_prob = float(fail_prob)
     cfg.recover_prob = float(recover_prob)
+    cfg.next_step_reset = 1 if next_step_reset else 0
     _lib.validate(cfg)
     return cfg
 
@@ -236,7 +240,11 @@ class VecLoadBalanceEnv:
     the range on the host before every launch (one sync per step; for debugging callers).
     With autoreset=True, envs whose episode ended are reset inside step(); their returned obs is
     the first obs of the new episode and info['terminal_obs'] (if keep_terminal_obs) holds the
-    last one, as gym/SB3 vector envs do.
+    last one, as gym/SB3 vector envs do (autoreset_mode="same_step", a masked reset launch after
+    the step when some env can be done).  autoreset_mode="next_step" is gymnasium's NEXT_STEP
+    mode: the step that ends an episode returns its last obs with done True, and the NEXT step
+    resets that env instead of stepping it (its action is ignored; reset obs, reward 0, done
+    False, episode length 0) -- inside the step's own launches, so no reset launch ever runs.
     graph_mode=True makes one step() capturable into a torch.cuda.CUDAGraph (hipGraph) and
     replayable: every output is a buffer allocated once and rewritten by each step (callers that
     keep a step's outputs must copy them), and the masked auto-reset launch runs every step (it
@@ -246,8 +254,15 @@ class VecLoadBalanceEnv:
     def __init__(self, num_envs: int, num_servers: int = 4, *, device=None,
                  autoreset: bool = True, keep_terminal_obs: bool = False,
                  strict_actions: bool = False, feature_mode: str = "problem01",
-                 graph_mode: bool = False, **kwargs):
+                 graph_mode: bool = False, autoreset_mode: str = "same_step", **kwargs):
         torch = _torch()
+        if autoreset_mode not in ("same_step", "next_step"):
+            raise ValueError(f"Unknown autoreset_mode: {autoreset_mode}")
+        if autoreset_mode == "next_step" and feature_mode == "upstream":
+            raise ValueError("autoreset_mode='next_step' does not combine with feature_mode='upstream'")
+        self.next_step = bool(autoreset) and autoreset_mode == "next_step"
+        if self.next_step:
+            kwargs["next_step_reset"] = True
         self.graph_mode = graph_mode
         self._static = {}  # graph_mode: output buffers by name
         # feature_mode "upstream": columns 1-10 follow the live agent's process_reservoir
@@ -453,7 +468,9 @@ class VecLoadBalanceEnv:
         if raw is not None:
             info["raw_obs"] = raw
         self._step_bound += 1
-        if self.autoreset and (self.graph_mode or self._step_bound >= self.cfg.max_steps):
+        if self.next_step:  # done envs reset inside the next step's launches
+            pass
+        elif self.autoreset and (self.graph_mode or self._step_bound >= self.cfg.max_steps):
             if self.keep_terminal_obs:
                 info["terminal_obs"] = obs.clone()
             if self._synced and not self.graph_mode:

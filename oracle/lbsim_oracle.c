@@ -521,10 +521,16 @@ uint32_t oracle_vose_sample(const float* prob, const uint32_t* alias, int n, uin
   return state;
 }
 
-static int ring_head(const oracle_t* o, size_t sb) { return (int)(o->hc[sb] & 0xFFFFu); }
+/* hc = ring head | HC_BIG | count << 16.  HC_BIG (sticky): a record holding a sample >= 2^25 - 1
+ * us as an unsigned word (negative lost-FIN guesses included) was stored in the server's
+ * reservoirs since they were last emptied (reset, failure) -- the GPU observe's test for its
+ * one-pass key sort; part of the state, so restated here. */
+#define HC_BIG 0x8000u
+#define PACK_LIMIT ((1u << 25) - 1u)
+static int ring_head(const oracle_t* o, size_t sb) { return (int)(o->hc[sb] & (HC_BIG - 1u)); }
 static int ring_count(const oracle_t* o, size_t sb) { return (int)(o->hc[sb] >> 16); }
 static void ring_set(oracle_t* o, size_t sb, int head, int cnt) {
-  o->hc[sb] = (uint32_t)head | ((uint32_t)cnt << 16);
+  o->hc[sb] = (o->hc[sb] & HC_BIG) | (uint32_t)head | ((uint32_t)cnt << 16);
 }
 
 /* A reservoir sample in seconds from its integer-microsecond form (env.py reports seconds). */
@@ -591,6 +597,7 @@ static void reservoir_add(env_ctx* e, int s, uint32_t fct, uint32_t dur, uint32_
   }
   if (slot >= 0) {
     const size_t r = sb * K + (size_t)slot;
+    if ((fct > dur ? fct : dur) >= PACK_LIMIT) o->hc[sb] |= HC_BIG;
     o->res[3 * r + 0] = fct;
     o->res[3 * r + 1] = dur;
     o->res[3 * r + 2] = ts_ms;
@@ -683,7 +690,7 @@ static void sim_step(env_ctx* e, const float* w) {
       } else if (u < o->fail_thr) {
         o->down[sb] = 1u;
         o->dropped[b] += (uint32_t)ring_count(o, sb);
-        ring_set(o, sb, ring_head(o, sb), 0);
+        o->hc[sb] = (uint32_t)ring_head(o, sb); /* empty queue, reservoirs emptied: no HC_BIG */
         o->last_tc[sb] = LAST_NONE;
         o->res_count[sb] = 0u;
         o->chg[sb * 4] |= 1u; /* emptied: the next observe recomputes the (zero) features */
@@ -898,9 +905,20 @@ int oracle_step(oracle_t* o, const void* action, int dtype, float* obs_out, floa
     env_ctx e;
     memset(&e, 0, sizeof(e));
     e.o = o; e.b = (size_t)b; e.gid = (uint32_t)(o->cfg.env_id_offset + (int64_t)b);
+    for (size_t i = 0; i < (size_t)S * 4; ++i) o->chg[(size_t)b * S * 4 + i] = 0u;
+    if (o->cfg.next_step_reset && o->ep_step[b] >= o->cfg.max_steps) {
+      /* gymnasium NEXT_STEP autoreset: the env that returned done last step resets instead of
+       * stepping (its action is ignored): reset observation, reward 0, done 0, counts 0 */
+      reset_env(o, (size_t)b);
+      if (assign_out)
+        for (int s = 0; s < S; ++s) assign_out[(size_t)b * S + (size_t)s] = 0;
+      observe(o, (size_t)b, obs_out, NULL, NULL, 0);
+      reward_out[b] = 0.0f;
+      done_out[b] = 0u;
+      continue;
+    }
     float w[LBSIM_MAX_SERVERS];
     for (int s = 0; s < S; ++s) w[s] = action_weight(o, action, dtype, (size_t)b * S + (size_t)s);
-    for (size_t i = 0; i < (size_t)S * 4; ++i) o->chg[(size_t)b * S * 4 + i] = 0u;
     sim_step(&e, w);
     if (assign_out)
       for (int s = 0; s < S; ++s) assign_out[(size_t)b * S + (size_t)s] = e.assigned[s];

@@ -38,7 +38,7 @@ def live_ring(d, B, S, Q):
     live = np.zeros((B, S, Q), bool)
     for b in range(B):
         for s in range(S):
-            h, c = int(hc[b, s] & 0xFFFF), int(hc[b, s] >> 16)
+            h, c = int(hc[b, s] & 0x7FFF), int(hc[b, s] >> 16)  # bit 15: the sticky big flag
             for i in range(c):
                 live[b, s, (h + i) % Q] = True
     return np.where(live[..., None], ring, 0)

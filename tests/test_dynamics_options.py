@@ -51,8 +51,10 @@ def test_lost_fin_changes_only_the_fct_of_lost_flows(oracle_mod):
     for p, timeout, buckets in ((1.0, 40.0, 1024), (0.3, 10.0, 256)):
         st, _ = _run(oracle_mod, B, S, steps, lost_fin_prob=p, flow_timeout=timeout,
                      flow_buckets=buckets)
-        for k in ("res_dur", "res_ts", "res_count", "hc", "dropped", "clock", "arr_idx"):
+        for k in ("res_dur", "res_ts", "res_count", "dropped", "clock", "arr_idx"):
             np.testing.assert_array_equal(st[k], st0[k], err_msg=k)
+        # queues equal; bit 15 of hc is the sticky big-sample flag (set by negative guesses)
+        np.testing.assert_array_equal(st["hc"] & ~np.uint32(0x8000), st0["hc"] & ~np.uint32(0x8000))
         n = np.minimum(st0["res_count"], 128).reshape(B, S)
         valid = (np.arange(128)[None, None, :] < n[:, :, None]).reshape(-1)
         f0 = st0["res_fct"].view(np.int32)[valid].astype(np.int64)
@@ -126,3 +128,39 @@ def test_server_failures_reward_uses_active_rows(oracle_mod):
             assert abs(float(rew[b]) - want) <= 1e-6 * max(1.0, abs(want)), (b, rew[b], want)
     assert some_down
     ora.close()
+
+
+def test_next_step_reset_equals_same_step_shifted(oracle_mod):
+    """Next-step auto-reset (gymnasium NEXT_STEP) on the oracle: the step that ends an episode
+    returns the terminal obs with done; the next step resets the env instead of stepping it
+    (action ignored; reward 0, done 0) and returns exactly the observation a same-step reset
+    returns (a reset does not depend on the episode before it), after which both runs walk the
+    same trajectory when fed the same actions."""
+    from marllb_amd.env import make_config
+    B, S, T = 48, 4, 3
+    nxt = oracle_mod.OracleEnv(make_config(B, S, seed=9, max_steps=T, next_step_reset=True), threads=4)
+    same = oracle_mod.OracleEnv(make_config(B, S, seed=9, max_steps=T), threads=4)
+    np.testing.assert_array_equal(nxt.reset(), same.reset())
+    rng = np.random.default_rng(2)
+    acts = [rng.integers(0, 3, (B, S)).astype(np.int64) for _ in range(3 * T)]
+    for k in range(T):  # the first episode: identical
+        o1, r1, d1, a1 = nxt.step(acts[k])
+        o2, r2, d2, a2 = same.step(acts[k])
+        for x, y in ((o1, o2), (r1, r2), (d1, d2), (a1, a2)):
+            np.testing.assert_array_equal(x, y)
+    assert d1.all()
+    reset_obs = same.reset(mask=d2.astype(np.uint8), obs=o2.copy())  # same-step: reset now
+    o1, r1, d1, a1 = nxt.step(acts[T])  # next-step: this step resets, its action ignored
+    np.testing.assert_array_equal(o1, reset_obs)
+    assert (r1 == 0).all() and not d1.any() and (a1 == 0).all()
+    ln, rt = nxt.episode_stats()
+    assert (ln == 0).all() and (rt == 0).all()
+    for k in range(T + 1, 2 * T + 1):  # the second episode, actions shifted by one step
+        o1, r1, d1, _ = nxt.step(acts[k])
+        o2, r2, d2, _ = same.step(acts[k])
+        np.testing.assert_array_equal(o1, o2)
+        np.testing.assert_array_equal(r1, r2)
+        np.testing.assert_array_equal(d1, d2)
+    np.testing.assert_array_equal(nxt.state_bytes(), same.state_bytes())
+    nxt.close()
+    same.close()

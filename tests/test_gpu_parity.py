@@ -234,6 +234,15 @@ CONFIGS = [
                          "lost_fin_prob": 0.2}),
     dict(B=48, S=8, kw={"fail_prob": 0.3, "recover_prob": 0.1, "lost_fin_prob": 0.1,
                         "trace": "short", "load": 1.2}),
+    # next-step auto-reset (gymnasium NEXT_STEP): envs done last step reset inside the step
+    # launches (warm-up included, action ignored, reward 0) -- short episodes cross several
+    # boundaries; one-wave-per-env and group dispatch, S > 16 (two-launch observe), failures
+    dict(B=70, S=4, kw={"max_steps": 3, "next_step_reset": True}),
+    dict(B=40, S=6, kw={"max_steps": 4, "next_step_reset": True, "assign_policy": "sed2",
+                        "normalize_obs": True}),
+    dict(B=30, S=20, kw={"max_steps": 2, "next_step_reset": True, "fail_prob": 0.1,
+                         "lost_fin_prob": 0.2}),
+    dict(B=8256, S=4, kw={"max_steps": 5, "next_step_reset": True}),
 ]
 
 

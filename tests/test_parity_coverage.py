@@ -51,9 +51,10 @@ def run_case(oracle_mod, case, steps=12):
         cnt = st["res_count"].reshape(B, S)
         full = np.pad(cnt >= 128, ((0, 0), (0, pad)), constant_values=True)
         ge8 = np.pad(cnt >= 8, ((0, 0), (0, pad)), constant_values=True)
-        # the kernel's qualification reads all 128 slots (stale words of empty slots included);
-        # negative (lost-FIN) samples are >= 2^31 as unsigned words
-        big = np.maximum(st["res_fct"], st["res_dur"]).reshape(B, S, 128).max(2) >= PACK_LIMIT
+        # the kernel decides by the sticky kHcBig flag of hc (bit 15): a record with a sample
+        # >= 2^25 - 1 us (negative lost-FIN guesses: >= 2^31 as unsigned words) stored since the
+        # reservoir was emptied
+        big = ((st["hc"] >> 15) & 1).reshape(B, S).astype(bool)
         big = np.pad(big, ((0, 0), (0, pad)))
         chg = np.pad(per_server > 0, ((0, 0), (0, pad)))
         full, ge8, big, chg = (x.reshape(B, nc, 4) for x in (full, ge8, big, chg))

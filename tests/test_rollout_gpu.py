@@ -103,6 +103,68 @@ def test_env_step_graph_capture_replays_bit_exact():
     graph.close()
 
 
+@pytest.mark.parametrize("B", [1024, 8256])
+def test_env_step_graph_next_step_autoreset(oracle_mod, B):
+    """autoreset_mode="next_step" (gymnasium NEXT_STEP): the captured step holds only the step's
+    own launches (no masked-reset kernel: the reset of an env done last step runs inside them),
+    and replays over three episode boundaries equal the oracle with next_step_reset, bit for bit
+    (obs, reward, done, episode length / return); the step after done reports the reset obs,
+    reward 0 and done False.  B = 1024: the one-launch wave step; 8256: group dynamics + observe."""
+    import numpy as np
+    from marllb_amd import VecLoadBalanceEnv
+    from marllb_amd.env import make_config
+    S, T = 4, 3
+    graph = VecLoadBalanceEnv(B, S, device="cuda:0", seed=12, max_steps=T, graph_mode=True,
+                              autoreset_mode="next_step")
+    ora = oracle_mod.OracleEnv(make_config(B, S, seed=12, max_steps=T, next_step_reset=True),
+                               threads=8)
+    np.testing.assert_array_equal(graph.reset().cpu().numpy(), ora.reset())
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(3)
+    acts = [torch.randint(0, 3, (B, S), device="cuda:0", generator=g) for _ in range(4 * (T + 1))]
+    a_static = acts[0].clone()
+
+    class Spy:  # counts the facade's reset calls (graph_mode same-step would make one per step)
+        def __init__(self, lib):
+            self._lib, self.resets = lib, 0
+
+        def __getattr__(self, name):
+            f = getattr(self._lib, name)
+            if name != "lbsim_reset_ex":
+                return f
+
+            def counted(*a):
+                self.resets += 1
+                return f(*a)
+            return counted
+    spy = graph.handle.lib = Spy(graph.handle.lib)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):  # warm-up step (eager, graph_mode buffers)
+        o, r, d, _ = graph.step(a_static)
+    torch.cuda.current_stream().wait_stream(side)
+    oo, ro, do, _ = ora.step(acts[0].cpu().numpy())
+    assert np.array_equal(o.cpu().numpy(), oo) and np.array_equal(r.cpu().numpy(), ro)
+    cg = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(cg):
+        obs, rew, done, info = graph.step(a_static)
+    assert spy.resets == 0  # the captured step holds no masked-reset launch
+    for k in range(1, len(acts)):
+        a_static.copy_(acts[k])
+        cg.replay()
+        oo, ro, do, _ = ora.step(acts[k].cpu().numpy())
+        ln, rt = ora.episode_stats()
+        np.testing.assert_array_equal(obs.cpu().numpy(), oo, err_msg=f"step {k}")
+        np.testing.assert_array_equal(rew.cpu().numpy(), ro, err_msg=f"step {k}")
+        np.testing.assert_array_equal(done.cpu().numpy().astype(np.uint8), do, err_msg=f"step {k}")
+        np.testing.assert_array_equal(info["episode_length"].cpu().numpy(), ln)
+        np.testing.assert_array_equal(info["episode_return"].cpu().numpy(), rt)
+        if k % (T + 1) == T:  # the step after the episode end: the reset, reward 0
+            assert not do.any() and (ro == 0).all() and (ln == 0).all()
+    ora.close()
+    graph.close()
+
+
 def test_qmix_rollout_graph_capture_replays_bit_exact():
     """One QMIXRollout.step -- the fused QMIX policy kernel (Philox step counter on the device),
     the fused env step writing the agent observations and the state, the auto-reset -- captured
