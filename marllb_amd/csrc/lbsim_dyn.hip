@@ -32,26 +32,33 @@ void launch_dyn(const LaunchCtx& L, const void* action, int dtype, int32_t* assi
 template <int G, int POLICY>
 void launch_dyn_group(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
                       const uint8_t* mask, hipStream_t stream) {
-  constexpr int epw = 64 / G;
+  // envs per wave: 64 / G; LBSIM_DYN_EPW (1 .. 64 / G) runs fewer per wave, more waves
+  static const int forced_epw = [] {
+    const char* e = std::getenv("LBSIM_DYN_EPW");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int epw = (forced_epw >= 1 && forced_epw <= 64 / G) ? forced_epw : 64 / G;
+  SimParams prm = L.prm;
+  prm.dyn_epw = epw;
   const dim3 block(64), grid((unsigned)((L.B + epw - 1) / epw));
   // a step grid of more than 4 waves per SIMD: the 5-wave register budget (SED, 4 / 8 lanes)
   if constexpr (MODE == kModeStep && POLICY == 0 && (G == 4 || G == 8)) {
     if ((int64_t)grid.x > 4 * (int64_t)L.simds) {
       if (L.prm.trace)
         LBSIM_LAUNCH((dynamics_group_kernel<G, MODE, POLICY, true, 5>), grid, block, 0,
-                           stream, L.st, L.prm, action, dtype, assign, mask);
+                           stream, L.st, prm, action, dtype, assign, mask);
       else
         LBSIM_LAUNCH((dynamics_group_kernel<G, MODE, POLICY, false, 5>), grid, block, 0,
-                           stream, L.st, L.prm, action, dtype, assign, mask);
+                           stream, L.st, prm, action, dtype, assign, mask);
       return;
     }
   }
   if (L.prm.trace)
     LBSIM_LAUNCH((dynamics_group_kernel<G, MODE, POLICY, true>), grid, block, 0, stream,
-                       L.st, L.prm, action, dtype, assign, mask);
+                       L.st, prm, action, dtype, assign, mask);
   else
     LBSIM_LAUNCH((dynamics_group_kernel<G, MODE, POLICY, false>), grid, block, 0, stream,
-                       L.st, L.prm, action, dtype, assign, mask);
+                       L.st, prm, action, dtype, assign, mask);
 }
 
 template <int MAXS>

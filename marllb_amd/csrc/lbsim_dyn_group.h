@@ -305,7 +305,6 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
     if (ins && slot >= 0) {
       const uint32_t fct = lost_fct(p, (uint32_t)(tc_a - ta),
                                     gc.base_ms * 1000u + gc.base_rem + (uint32_t)ta, E.gid, E.episode);
-      if (p.big_in_step) V.big |= big_record(fct, (uint32_t)svc);  // uniform: off by default
       my_res[(uint32_t)slot] =
           make_uint3(fct, (uint32_t)svc, gc.base_ms + (gc.base_rem + (uint32_t)tc_a) / 1000u);
       mark(slot);
@@ -495,7 +494,11 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
   uint32_t* const chgw = L.chgw;
   const int s = lane & (G - 1);
   const int gbase = lane & ~(G - 1);
-  const uint32_t b = wave * (uint32_t)(64 / G) + (uint32_t)(lane / G);
+  // envs per wave: 64 / G, or fewer (p.dyn_epw) to put more waves in flight -- lanes of groups
+  // past it leave at once, like envs past B
+  const int epw = p.dyn_epw > 0 ? p.dyn_epw : 64 / G;
+  if (lane / G >= epw) return;
+  const uint32_t b = wave * (uint32_t)epw + (uint32_t)(lane / G);
   if (b >= (uint32_t)p.B) return;  // whole groups leave together
   const int S = p.S, Q = p.Q;
   if (MODE == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
@@ -619,6 +622,12 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
       int li = V.lh + i;
       li = li >= WL ? li - WL : li;
       st.ring[sb * (uint32_t)Q + (uint32_t)pos] = win[li * 64 + lane];
+    }
+    if (p.big_in_step) {  // the in-step records this launch wrote (big_written)
+      const uint32_t cw[4] = {chgw[lane], chgw[64 + lane], chgw[128 + lane], chgw[192 + lane]};
+      __builtin_amdgcn_s_waitcnt(0);  // the wave's stores acknowledged by L2 (vmcnt 0)
+      __asm__ volatile("" ::: "memory");
+      V.big |= big_written(st.res + (size_t)sb * K, cw, V.rcnt);
     }
     st.hc[sb] = (uint32_t)V.head | (V.big ? kHcBig : 0u) | ((uint32_t)V.cnt << 16);
     st.last_tc[sb] = V.last;

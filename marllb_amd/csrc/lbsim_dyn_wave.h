@@ -202,7 +202,6 @@ __device__ __forceinline__ void wave_flush(const SimParams& p, WaveSrv& V, WaveE
     svc = svc < 1 ? 1 : svc;
     const uint32_t fct = lost_fct(p, (uint32_t)(Bt.ltc - Bt.ta),
                                   base_ms * 1000u + base_rem + (uint32_t)Bt.ta, E.gid, E.episode);
-    if (p.big_in_step && big_record(fct, (uint32_t)svc)) atomicOr(&Ld.big[Bt.lc], 1u);  // rare
     res_b[key] = make_uint3(fct, (uint32_t)svc, base_ms + (base_rem + (uint32_t)Bt.ltc) / 1000u);
   }
 }
@@ -676,7 +675,15 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
   if (V.act) {
     int head = V.wp - V.cnt0;
     head = head < 0 ? head + Q : head;
-    st.hc[sb] = (uint32_t)head | (Ld.big[lane] ? kHcBig : 0u) | ((uint32_t)V.cnt0 << 16);
+    bool big = Ld.big[lane] != 0u;
+    if (p.big_in_step) {  // the in-step records this launch wrote (big_written), by any lane
+      const uint32_t cw[4] = {Ld.chg[lane], Ld.chg[kWaveMaxS + lane], Ld.chg[2 * kWaveMaxS + lane],
+                              Ld.chg[3 * kWaveMaxS + lane]};
+      __builtin_amdgcn_s_waitcnt(0);  // the wave's stores acknowledged by L2 (vmcnt 0)
+      __asm__ volatile("" ::: "memory");
+      big |= big_written(st.res + (size_t)sb * K, cw, V.rcnt);
+    }
+    st.hc[sb] = (uint32_t)head | (big ? kHcBig : 0u) | ((uint32_t)V.cnt0 << 16);
     st.last_tc[sb] = V.last;
     st.res_count[sb] = V.rcnt;
     *reinterpret_cast<uint4*>(st.chg + (size_t)sb * 4) =

@@ -114,6 +114,8 @@ struct SimParams {
   // next-step auto-reset (lbsim_config_t::next_step_reset): a step launch resets the envs whose
   // last step returned done (ep_step >= max_steps) instead of stepping them
   int32_t next_reset;
+  // envs per wave of dynamics_group_kernel (0: 64 / G, every lane used); set by its launcher
+  int32_t dyn_epw;
 };
 
 constexpr uint32_t kStreamFailure = 5u;  // Philox stream of the failure / recovery draws
@@ -129,6 +131,29 @@ constexpr uint32_t kHcBig = 1u << 15;
 constexpr uint32_t kHcHead = kHcBig - 1u;
 __device__ __forceinline__ bool big_record(uint32_t fct, uint32_t dur) {
   return (fct > dur ? fct : dur) >= kPackLimit;
+}
+// When it is set: a carried-in flow's record (its fct spans earlier steps) at its store; a record
+// of a flow that arrived and completed in the launch's steps only if such a record can be big
+// (SimParams::big_in_step: dt >= kPackLimit us, or lost-FIN guesses), by one scan of the slots
+// the launch wrote (below the count) at its end -- nothing in the event loop.  oracle: the same.
+// The record words are read device-coherent: in the wave kernel other lanes stored them.
+__device__ __forceinline__ bool big_written(const uint3* res_s, const uint32_t (&chg)[4],
+                                            uint32_t count) {
+  const uint32_t n = count < (uint32_t)K ? count : (uint32_t)K;
+  bool big = false;
+  for (int w = 0; w < 4; ++w) {
+    uint32_t m = chg[w];
+    while (m) {
+      const uint32_t slot = 32u * (uint32_t)w + (uint32_t)__builtin_ctz(m);
+      m &= m - 1u;
+      if (slot >= n) continue;
+      const uint32_t* r = reinterpret_cast<const uint32_t*>(res_s + slot);
+      const uint32_t f = __hip_atomic_load(r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t d = __hip_atomic_load(r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      big |= big_record(f, d);
+    }
+  }
+  return big;
 }
 
 // murmur3's 32-bit finaliser (fmix32): the lost-FIN hash.
@@ -730,7 +755,6 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
     if (ins && slot >= 0) {
       const uint32_t fct = lost_fct(p, (uint32_t)(tc_a - ta),
                                     ec.base_ms * 1000u + ec.base_rem + (uint32_t)ta, L.gid, L.episode);
-      if (p.big_in_step) L.bigm |= big_record(fct, (uint32_t)svc) ? 1u << cs : 0u;
       my_res[(uint32_t)cs * (uint32_t)K + (uint32_t)slot] =
           make_uint3(fct, (uint32_t)svc, ec.base_ms + (ec.base_rem + (uint32_t)tc_a) / 1000u);
       mark_slot<MAXS>(l, cs, slot);
@@ -998,7 +1022,15 @@ __device__ __forceinline__ void store_servers(const DevState& st, const SimParam
         li = li >= WL ? li - WL : li;
         st.ring[sb * (uint32_t)p.Q + (uint32_t)pos] = *qslot<MAXS>(l, s, li);
       }
-      st.hc[sb] = (uint32_t)head | ((L.bigm >> s) & 1u ? kHcBig : 0u) | ((uint32_t)L.cnt[s] << 16);
+      bool big = (L.bigm >> s) & 1u;
+      if (p.big_in_step) {  // the in-step records this launch wrote (big_written)
+        const uint32_t cw[4] = {l.m[(s * 4 + 0) * 64 + l.lane], l.m[(s * 4 + 1) * 64 + l.lane],
+                                l.m[(s * 4 + 2) * 64 + l.lane], l.m[(s * 4 + 3) * 64 + l.lane]};
+        __builtin_amdgcn_s_waitcnt(0);  // the wave's stores acknowledged by L2 (vmcnt 0)
+        __asm__ volatile("" ::: "memory");
+        big |= big_written(st.res + (size_t)sb * K, cw, (uint32_t)fld<MAXS>(l, F_RCNT, s));
+      }
+      st.hc[sb] = (uint32_t)head | (big ? kHcBig : 0u) | ((uint32_t)L.cnt[s] << 16);
       st.last_tc[sb] = L.last[s];
       st.res_count[sb] = (uint32_t)fld<MAXS>(l, F_RCNT, s);
       if (st.down != nullptr) st.down[sb] = (L.downm >> s) & 1u;

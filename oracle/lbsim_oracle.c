@@ -300,6 +300,7 @@ typedef struct oracle {
   int32_t lf_off_us;
   float lf_wait_us;
   uint32_t fail_thr, rec_thr;
+  int big_in_step; /* an in-step record can hold a sample >= PACK_LIMIT (dt >= it, or lost-FIN) */
   uint32_t key[2];
   int threads;
   int initialised;
@@ -342,6 +343,7 @@ static void derive(oracle_t* o) {
                       ? (float)((double)c->flow_buckets * 1e6 / (double)c->arrival_rate) : 0.0f;
   o->fail_thr = (uint32_t)llround((double)c->fail_prob * 16777216.0);
   o->rec_thr = (uint32_t)llround((double)c->recover_prob * 16777216.0);
+  o->big_in_step = (o->dt_us >= (int32_t)((1u << 25) - 1u)) || o->lf_thr != 0u;
   o->key[0] = (uint32_t)(c->seed & 0xFFFFFFFFull);
   o->key[1] = (uint32_t)(c->seed >> 32);
 }
@@ -597,13 +599,31 @@ static void reservoir_add(env_ctx* e, int s, uint32_t fct, uint32_t dur, uint32_
   }
   if (slot >= 0) {
     const size_t r = sb * K + (size_t)slot;
-    if ((fct > dur ? fct : dur) >= PACK_LIMIT) o->hc[sb] |= HC_BIG;
+    /* HC_BIG at the store for a flow carried in from an earlier step; in-step records by the
+     * end-of-launch scan (big_scan) */
+    if (!has_r && (fct > dur ? fct : dur) >= PACK_LIMIT) o->hc[sb] |= HC_BIG;
     o->res[3 * r + 0] = fct;
     o->res[3 * r + 1] = dur;
     o->res[3 * r + 2] = ts_ms;
     o->chg[sb * 4 + (size_t)(slot >> 5)] |= 1u << (slot & 31);
   }
   if (c != 0xFFFFFFFFu) o->res_count[sb] = c + 1u;
+}
+
+/* End of a dynamics launch (a step, or a reset with its warm-up): when an in-step record can be
+ * big, HC_BIG |= any slot the launch wrote (below the count) holding one -- the GPU's big_written. */
+static void big_scan(oracle_t* o, size_t b) {
+  if (!o->big_in_step) return;
+  for (int s = 0; s < o->S; ++s) {
+    const size_t sb = b * (size_t)o->S + (size_t)s;
+    const uint32_t c = o->res_count[sb];
+    const uint32_t n = c < (uint32_t)K ? c : (uint32_t)K;
+    for (uint32_t slot = 0; slot < n; ++slot) {
+      if (!((o->chg[sb * 4 + (slot >> 5)] >> (slot & 31)) & 1u)) continue;
+      const uint32_t f = o->res[3 * (sb * K + slot)], d = o->res[3 * (sb * K + slot) + 1];
+      if ((f > d ? f : d) >= PACK_LIMIT) o->hc[sb] |= HC_BIG;
+    }
+  }
 }
 
 static void pop_until(env_ctx* e, int s, int32_t t, uint64_t base_us, double den) {
@@ -878,6 +898,7 @@ static void reset_env(oracle_t* o, size_t b) {
   float w1[LBSIM_MAX_SERVERS];
   for (int s = 0; s < LBSIM_MAX_SERVERS; ++s) w1[s] = 1.0f;
   for (int k = 0; k < o->cfg.warmup_steps; ++k) sim_step(&e, w1);
+  big_scan(o, b);
   o->ep_step[b] = 0;
   o->ep_return[b] = 0.0;
 }
@@ -920,6 +941,7 @@ int oracle_step(oracle_t* o, const void* action, int dtype, float* obs_out, floa
     float w[LBSIM_MAX_SERVERS];
     for (int s = 0; s < S; ++s) w[s] = action_weight(o, action, dtype, (size_t)b * S + (size_t)s);
     sim_step(&e, w);
+    big_scan(o, (size_t)b);
     if (assign_out)
       for (int s = 0; s < S; ++s) assign_out[(size_t)b * S + (size_t)s] = e.assigned[s];
     observe(o, (size_t)b, obs_out, reward_out, done_out, 1);
