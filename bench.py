@@ -156,6 +156,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dyn-mapping", default="auto", choices=["auto", "env", "server"],
                     help="dynamics kernel mapping: one lane per env / per server (same results)")
+    ap.add_argument("--graph-steps", type=int, default=5,
+                    help="steps captured per graph in the graph leg (one replay = that many steps)")
     ap.add_argument("--no-graph", action="store_true",
                     help="skip the graph leg (N=1: the same workload with one step captured in a "
                          "hipGraph and replayed, reported beside `value` as `graph`)")
@@ -337,6 +339,7 @@ def graph_leg(args, dev, shard, B, S, common, kernel_ms):
     from marllb_amd.env import VecLoadBalanceEnv
     common = dict(common, graph_mode=True)
     autoreset = "same_step"
+    k = max(1, args.graph_steps)  # steps per captured graph (one replay = k steps)
     if args.workload == "rollout":
         autoreset = "next_step"
         env = VecLoadBalanceEnv(B, S, max_steps=10000, autoreset_mode=autoreset, **common)
@@ -349,30 +352,34 @@ def graph_leg(args, dev, shard, B, S, common, kernel_ms):
         torch.cuda.current_stream(dev).wait_stream(side)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            env.step(torch.randint(0, 3, (B, S), device=dev, dtype=torch.int64))
+            for _ in range(k):
+                env.step(torch.randint(0, 3, (B, S), device=dev, dtype=torch.int64))
     elif args.workload == "sac-gru":
         from marllb_amd.rollout import SACGRURollout
         env = VecLoadBalanceEnv(B, S, action_type="continuous", max_steps=10000, **common)
-        g = SACGRURollout(env, seed=args.seed + shard.rank).capture()
+        g = SACGRURollout(env, seed=args.seed + shard.rank).capture(steps=k)
     else:
         from marllb_amd.multi_agent import VecMultiAgentLoadBalanceEnv
         from marllb_amd.rollout import QMIXRollout
         env = VecMultiAgentLoadBalanceEnv(B, 4, S // 4, action_type="discrete", max_steps=100,
                                           **common)
-        g = QMIXRollout(env, seed=args.seed + shard.rank).capture()
-    for _ in range(args.warmup):
+        g = QMIXRollout(env, seed=args.seed + shard.rank).capture(steps=k)
+    reps = max(1, -(-args.steps // k))  # replays covering at least --steps steps
+    for _ in range(max(1, -(-args.warmup // k))):
         g.replay()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(reps):
         g.replay()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     env.close()
-    ms = el / args.steps * 1e3
-    return {"value": B * args.steps / el, "unit": "env-steps/s", "ms_per_step": ms,
+    n = reps * k
+    ms = el / n * 1e3
+    return {"value": B * n / el, "unit": "env-steps/s", "ms_per_step": ms, "steps": n,
             "kernels_ms_per_step": kernel_ms, "gap_ms_per_step": ms - kernel_ms,
-            "form": "one step captured in a torch.cuda.CUDAGraph, replayed", "autoreset": autoreset}
+            "form": f"{k} steps captured in one torch.cuda.CUDAGraph, replayed",
+            "steps_per_graph": k, "autoreset": autoreset}
 
 
 def late_episode(args, env, handle, lib, one_step, rate, B, S, done_steps):

@@ -46,10 +46,12 @@ class SACGRURollout:
             return self._h
         return self._h * (~self._reset).view(1, -1, 1).to(self._h.dtype)
 
-    def capture(self, warmup: int = 2) -> "torch.cuda.CUDAGraph":
-        """One step() captured into a torch.cuda.CUDAGraph (as QMIXRollout.capture): needs the
-        one-launch actor kernel and an env in graph_mode; `warmup` eager steps first on a side
-        stream, then g.replay() == step() on the same static buffers (self.obs, self.last)."""
+    def capture(self, warmup: int = 2, steps: int = 1) -> "torch.cuda.CUDAGraph":
+        """`steps` step()s captured into one torch.cuda.CUDAGraph (as QMIXRollout.capture): needs
+        the one-launch actor kernel and an env in graph_mode; `warmup` eager steps first on a side
+        stream, then g.replay() == `steps` step()s on the same static buffers (self.obs,
+        self.last: the last step's outputs).  Several steps per graph amortise the replay's own
+        launch cost."""
         if self.fused is None or self.fused.kernel is None or not self.env.graph_mode:
             raise ValueError("capture needs the fused SAC actor kernel and graph_mode=True")
         self.fused.use_device_step()
@@ -61,7 +63,8 @@ class SACGRURollout:
         torch.cuda.current_stream(self.env.device).wait_stream(side)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self.last = self.step()
+            for _ in range(max(1, steps)):
+                self.last = self.step()
         return g
 
     @torch.no_grad()
@@ -114,11 +117,12 @@ class QMIXRollout:
             self.hidden = [torch.zeros(1, env.num_envs, H, device=dev) for _ in self.agents]
         self.obs = env.reset()
 
-    def capture(self, warmup: int = 2) -> "torch.cuda.CUDAGraph":
-        """One step() captured into a torch.cuda.CUDAGraph: needs the fused kernel and an env in
-        graph_mode (static buffers, auto-reset launched every step); the Philox step counter
-        moves to the device.  `warmup` eager steps first (on a side stream, as torch requires),
-        then g.replay() == step() on the same static buffers (self.obs, self.hidden, ...)."""
+    def capture(self, warmup: int = 2, steps: int = 1) -> "torch.cuda.CUDAGraph":
+        """`steps` step()s captured into one torch.cuda.CUDAGraph: needs the fused kernel and an
+        env in graph_mode (static buffers, auto-reset launched every step); the Philox step
+        counter moves to the device.  `warmup` eager steps first (on a side stream, as torch
+        requires), then g.replay() == `steps` step()s on the same static buffers (self.obs,
+        self.hidden, ...)."""
         if self.kernel is None or not self.env.vec.graph_mode:
             raise ValueError("capture needs the fused QMIX kernel and graph_mode=True")
         self.kernel.use_device_step()
@@ -130,7 +134,8 @@ class QMIXRollout:
         torch.cuda.current_stream(self.env.device).wait_stream(side)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self.last = self.step()
+            for _ in range(max(1, steps)):
+                self.last = self.step()
         return g
 
     @torch.no_grad()

@@ -199,10 +199,12 @@ def test_qmix_rollout_graph_capture_replays_bit_exact():
             assert torch.equal(x, y), k
 
 
-def test_sac_rollout_graph_capture_replays_bit_exact():
-    """One SACGRURollout.step -- the one-launch SAC-GRU actor (Philox step counter on the device,
+@pytest.mark.parametrize("per_graph", [1, 3])
+def test_sac_rollout_graph_capture_replays_bit_exact(per_graph):
+    """SACGRURollout.step -- the one-launch SAC-GRU actor (Philox step counter on the device,
     hidden state updated in place, finished envs restarted from h = 0) and the env step -- captured
-    and replayed equals the eager rollout bit for bit across episode ends (max_steps 3)."""
+    (one or three steps per graph) and replayed equals the eager rollout bit for bit across
+    episode ends (max_steps 3)."""
     from marllb_amd import VecLoadBalanceEnv
     from marllb_amd.rollout import SACGRURollout
     B, S, T = 512, 8, 3
@@ -214,16 +216,16 @@ def test_sac_rollout_graph_capture_replays_bit_exact():
         ro = SACGRURollout(env, seed=3)
         seq = []
         if graph_mode:
-            cg = ro.capture(warmup=2)
-            for _ in range(3 * T):
-                cg.replay()
+            cg = ro.capture(warmup=2, steps=per_graph)
+            for _ in range(3 * T // per_graph):
+                cg.replay()  # per_graph steps; the outputs are the last one's
                 rew, done, _ = ro.last
                 seq.append((rew.clone(), done.clone(), ro.obs.clone(), ro._h.clone()))
         else:
             for _ in range(2 + 3 * T):
                 rew, done, _ = ro.step()
                 seq.append((rew.clone(), done.clone(), ro.obs.clone(), ro._h.clone()))
-            seq = seq[2:]
+            seq = seq[2:][per_graph - 1::per_graph]
         outs.append(seq)
         env.close()
     for k, (a, b) in enumerate(zip(*outs)):
