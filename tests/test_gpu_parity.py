@@ -412,13 +412,15 @@ def test_step_wave_occupancy_forms_bit_exact(occ):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
 
 
-@pytest.mark.parametrize("lanes", ["4", "8", "16"])
-def test_wider_groups_bit_exact(lanes):
+@pytest.mark.parametrize("lanes,epw", [("4", ""), ("8", ""), ("16", ""), ("4", "13"), ("8", "3")])
+def test_wider_groups_bit_exact(lanes, epw):
     """LBSIM_DYN_GROUP_LANES forces the server-per-lane group width (lanes past S hold no server and
     only draw arrivals ahead): the simulator cases with S <= lanes stay bit-exact vs the oracle.
     lanes = 4 runs the headline 65536 x 4 kernel (4-lane groups) on every S <= 4 case -- every
     policy, trace arrivals, NaN fallbacks -- which the default small-batch dispatch sends to 8-lane
-    groups.  The setting is read once per process, so the cases run in a child process."""
+    groups.  epw (LBSIM_DYN_EPW): fewer envs per wave than 64 / lanes (lanes of the groups past it
+    idle), e.g. 13 4-lane envs per wave.  The settings are read once per process, so the cases run
+    in a child process."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -427,7 +429,8 @@ def test_wider_groups_bit_exact(lanes):
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p",
                         "no:cacheprovider"] +
                        [os.path.join(root, "tests", "test_gpu_parity.py") + "::" + k for k in ks],
-                       cwd=root, env={**os.environ, "LBSIM_DYN_GROUP_LANES": lanes},
+                       cwd=root, env={**os.environ, "LBSIM_DYN_GROUP_LANES": lanes,
+                                      **({"LBSIM_DYN_EPW": epw} if epw else {})},
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
 
