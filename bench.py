@@ -666,6 +666,12 @@ def main():
                          "signature": sigs.get(dom), "algorithmic_bytes_per_launch": ab,
                          "avg_launch_ms": avg[dom],
                          "kernel_avg_ms": avg, "kernels": per_kernel, "valu": valu,
+                         # the two simulator kernels take about equal time: `kernel` is the longer
+                         # one this run; the dynamics kernel moves few bytes by construction (an
+                         # event loop, latency-bound: see `valu`), observe is the HBM-heavy one
+                         "hbm_heavy_kernel": (max(per_kernel, key=lambda k: per_kernel[k]
+                                                  ["algorithmic_bytes_per_launch"])
+                                              if per_kernel else None),
                          "accounting": {"reservoir_slots_written_per_env_step": slots / B,
                                         "flows_in_flight_per_env": inflight / B,
                                         "basis": "lbsim_step_stats after each step of an exact "

@@ -17,7 +17,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-me
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 11
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || exit 12
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-graph --steps 30 > $O/prof_bench.log 2>&1 || exit 13
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-graph --steps 30 --warmup 10 > $O/prof_bench.log 2>&1 || exit 13
 cd $R
 : > $O/workloads.jsonl
 for a in "--batch 4096" "--trace poisson_for_loop_rate_500 --servers 8" "--workload sac-gru" "--workload qmix" "--workload qmix --servers 64"; do
