@@ -217,6 +217,10 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
       acache[lane] = make_int4(gap, __float_as_int(wk), (int)d.z, (int)d.w);
       __builtin_amdgcn_wave_barrier();
     }
+    // the next arrival (arr_idx + 1, within the draw-ahead window: at most one arrival per
+    // iteration since the refill) is read now, so its LDS round trip overlaps the queue head's
+    // instead of following the choice
+    const int4 nx = acache[gbase + (int)(E.arr_idx + 1u - cbase)];
     ++it;
     const bool arrival_due = E.next_arr < dt;  // the same in every lane of the group
     const int32_t th = arrival_due ? E.next_arr : dt;
@@ -328,7 +332,6 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
 
     // ---- next arrival (identical in every lane of the group): arrival arr_idx + 1 from the
     //      group's draw-ahead slots
-    const int4 nx = acache[gbase + (int)(E.arr_idx + 1u - cbase)];
     const int32_t na = ta + nx.x;
     const float nw = __int_as_float(nx.y);
     const uint32_t nu2 = (uint32_t)nx.z, nu3 = (uint32_t)nx.w;
