@@ -31,9 +31,6 @@
 namespace lbk {
 
 constexpr int kGroupWL = 8;  // LDS queue window per server: 64 lanes x 8 x 8 B = 4 KiB per wave
-// Arrivals each lane draws ahead per refill: a group refills every G * kDraw iterations, and a
-// lane's kDraw Philox blocks are independent chains the compiler interleaves.
-constexpr int kDraw = 2;
 
 // Reductions over the aligned G-lane group (G <= 16: one DPP row).  Lanes read only within their
 // group, so groups that left the event loop (inactive lanes) are never read.  mov_dpp with
@@ -192,46 +189,38 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
   uint32_t kbase = E.arr_idx + 1u, rbase = 0u;
   if constexpr (TRACE) rbase = trace_row(p, E.gid, E.episode, kbase);
   for (;;) {
-    if ((it & (uint32_t)(G * kDraw - 1)) == 0u) {
+    if ((it & (uint32_t)(G - 1)) == 0u) {
       cbase = E.arr_idx + 1u;
+      const uint32_t k = cbase + (uint32_t)s;
       uint32_t rk0[10], rk1[10];
 #pragma unroll
       for (int r = 0; r < 10; ++r) {
         rk0[r] = gc.k0 + (uint32_t)r * 0x9E3779B9u;
         rk1[r] = gc.k1 + (uint32_t)r * 0xBB67AE85u;
       }
-      u32x4 d[kDraw];
-#pragma unroll
-      for (int m = 0; m < kDraw; ++m)
-        d[m] = philox_rk(u32x4{cbase + (uint32_t)(s + G * m), E.gid, E.episode,
-                               kStreamArrival << 24}, rk0, rk1);
+      const u32x4 d = philox_rk(u32x4{k, E.gid, E.episode, kStreamArrival << 24}, rk0, rk1);
+      int32_t gap;
+      float wk;
       if constexpr (TRACE) {
-        rbase += cbase - kbase;  // <= G * kDraw arrivals since the last refill
+        const uint32_t rows = p.trace_rows;
+        rbase += cbase - kbase;  // <= G arrivals since the last refill
         kbase = cbase;
-        while (rbase >= p.trace_rows) rbase -= p.trace_rows;
+        while (rbase >= rows) rbase -= rows;
+        uint32_t r = rbase + (uint32_t)s;
+        while (r >= rows) r -= rows;
+        gap = (int32_t)st.trace_gap[r];
+        wk = st.trace_work[r];
+      } else {
+        gap = (int32_t)(-lb_logf(u01_open0(d.x)) * gc.mean_gap);
+        wk = -lb_logf(u01_open0(d.y));
       }
-#pragma unroll
-      for (int m = 0; m < kDraw; ++m) {
-        int32_t gap;
-        float wk;
-        if constexpr (TRACE) {
-          uint32_t r = rbase + (uint32_t)(s + G * m);
-          while (r >= p.trace_rows) r -= p.trace_rows;
-          gap = (int32_t)st.trace_gap[r];
-          wk = st.trace_work[r];
-        } else {
-          gap = (int32_t)(-lb_logf(u01_open0(d[m].x)) * gc.mean_gap);
-          wk = -lb_logf(u01_open0(d[m].y));
-        }
-        acache[gbase * kDraw + G * m + s] = make_int4(gap, __float_as_int(wk), (int)d[m].z,
-                                                      (int)d[m].w);
-      }
+      acache[lane] = make_int4(gap, __float_as_int(wk), (int)d.z, (int)d.w);
       __builtin_amdgcn_wave_barrier();
     }
     // the next arrival (arr_idx + 1, within the draw-ahead window: at most one arrival per
     // iteration since the refill) is read now, so its LDS round trip overlaps the queue head's
     // instead of following the choice
-    const int4 nx = acache[gbase * kDraw + (int)(E.arr_idx + 1u - cbase)];
+    const int4 nx = acache[gbase + (int)(E.arr_idx + 1u - cbase)];
     ++it;
     const bool arrival_due = E.next_arr < dt;  // the same in every lane of the group
     const int32_t th = arrival_due ? E.next_arr : dt;
@@ -484,7 +473,7 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
 template <int POLICY>
 struct DynGroupLds {
   int2 win[kGroupWL * 64];                          // queue windows, [slot][lane]
-  int4 acache[64 * kDraw];                          // draw-ahead arrival slots, [group][G kDraw]
+  int4 acache[64];                                  // draw-ahead arrival slots, [group][G]
   uint32_t chgw[4 * 64];                            // written-slot masks, [word][lane]
   int32_t atab[POLICY == kPolicyAlias ? 2 * 64 : 1];  // ALIAS tables, [word][lane] (last: the
                                                       // others keep their 16-B aligned offsets)
