@@ -66,3 +66,26 @@ def test_make_config_errors():
     assert c.reward_field == -1 and c.seed == 5
     c = E.make_config(8, 4, arrival_rate=400.0, load=0.8)
     assert list(c.server_rate)[:4] == [125.0] * 4
+
+
+def test_optional_dynamics_config():
+    """The round-4 config fields (include/lbsim.h): defaults (VPP's 40 s flow timeout and 1024
+    sticky buckets, lb.c:1437 / lb.h:46; failures and lost-FIN off; same-step auto-reset), their
+    validation, and the facade's autoreset_mode."""
+    c = E.make_config(8, 4)
+    assert c.lost_fin_prob == 0.0 and c.flow_timeout_s == 40.0 and c.flow_buckets == 1024
+    assert c.fail_prob == 0.0 and c.recover_prob == pytest.approx(0.1) and c.next_step_reset == 0
+    c = E.make_config(8, 4, lost_fin_prob=0.5, flow_timeout=10.0, flow_buckets=64, fail_prob=0.2,
+                      recover_prob=0.3, next_step_reset=True)
+    assert (c.lost_fin_prob, c.flow_timeout_s, c.flow_buckets) == (0.5, 10.0, 64)
+    assert c.fail_prob == pytest.approx(0.2) and c.next_step_reset == 1
+    for kw, msg in [({"lost_fin_prob": 1.5}, "lost_fin_prob"),
+                    ({"lost_fin_prob": 0.1, "flow_timeout": -1.0}, "flow_timeout_s"),
+                    ({"lost_fin_prob": 0.1, "flow_buckets": 0}, "flow_buckets"),
+                    ({"lost_fin_prob": 0.1, "flow_buckets": 10 ** 6}, "flow_buckets"),
+                    ({"fail_prob": -0.1}, "fail_prob"),
+                    ({"recover_prob": 2.0}, "recover_prob")]:
+        with pytest.raises(ValueError, match=msg):
+            E.make_config(8, 4, **kw)
+    with pytest.raises(ValueError, match="autoreset_mode"):
+        E.VecLoadBalanceEnv(8, 4, autoreset_mode="sometimes")
