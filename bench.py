@@ -602,7 +602,11 @@ def main():
         # lbsim_profile times each class
         dyn = ("dynamics_kernel", "dynamics_group_kernel",
                "dynamics_wave_kernel")[lib.lbsim_dynamics_kernel(handle.h)]
-        fused = "step_wave_kernel" if dyn == "dynamics_wave_kernel" else "fused_step_kernel"
+        # the template signature of each kernel the step launched (lbsim_launch_names), the key
+        # of the committed PMC counter files; the one-launch step's kernel named from it
+        ran = _lib.launch_names(handle, 0) if hasattr(lib, "lbsim_launch_names") else {}
+        fused = ran.get(4, "").split("<")[0] or (
+            "step_wave_kernel" if dyn == "dynamics_wave_kernel" else "fused_step_kernel")
         names = {0: dyn, 1: "observe_kernel", 4: fused}
         avg = {names[i]: ms[i] / cnt[i] for i in names if cnt[i] > 0}
         rate = tr.rate if tr is not None else ARRIVAL_RATE
@@ -616,9 +620,6 @@ def main():
             ach = ab_k / (avg[k] * 1e-3) / 1e9
             per_kernel[k] = {"avg_launch_ms": avg[k], "algorithmic_bytes_per_launch": ab_k,
                              "achieved_GBps": ach, "frac": ach / HBM_PEAK_GBS}
-        # the template signature of each kernel the step launched (lbsim_launch_names), the key
-        # of the committed PMC counter files
-        ran = _lib.launch_names(handle, 0) if hasattr(lib, "lbsim_launch_names") else {}
         sigs = {names[c]: sig for c, sig in ran.items() if c in names}
         for k in per_kernel:
             per_kernel[k]["signature"] = sigs.get(k)

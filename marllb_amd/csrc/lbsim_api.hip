@@ -393,12 +393,12 @@ int step_kernel_of(const lbsim_t* h) {
   return h->cfg.step_kernel != LBSIM_STEP_AUTO ? h->cfg.step_kernel : env;
 }
 
-// The one-launch wave step (step_wave_kernel): one wave per env and S <= 4, FUSED asked for, or
-// AUTO on batches of at most 4 envs per SIMD (every S <= 4 wave batch; LBSIM_STEP_WAVE_MAX_B
-// overrides), where one launch instead of two pays: 2048 x 4 0.0711 -> 0.0620 ms per step, 4096 x 4
-// +2.5 % (profiles/r03w/ab_step_wave_fused.txt).
-// S = 5-8: the two-chunk observe in the one-launch kernel needs the OCC-2 register budget, so
-// only batches of at most 2 envs per SIMD (where the wave dynamics serve S <= 8 anyway).
+// The one-launch wave step (step_wave_kernel): one wave per env and S <= 8, FUSED asked for, or
+// AUTO on batches of at most 4 envs per SIMD (LBSIM_STEP_WAVE_MAX_B overrides), where one launch
+// instead of two pays: 2048 x 4 0.0711 -> 0.0620 ms per step, 4096 x 4 +2.5 %
+// (profiles/r03w/ab_step_wave_fused.txt).  S = 5-8 between 2 and 4 envs per SIMD: the wave
+// dynamics alone lose to the server-per-lane groups there (dyn_wave_ok), the one launch with both
+// chunks observed in it wins (profiles/r04s/).
 bool use_step_wave(const lbsim_t* h) {
   static const int64_t max_b = [] {
     const char* e = std::getenv("LBSIM_STEP_WAVE_MAX_B");
@@ -406,13 +406,10 @@ bool use_step_wave(const lbsim_t* h) {
   }();
   const LaunchCtx L = ctx(h);
   // next-step auto-reset handles step in two launches (the dynamics' kModeStepNR instantiation)
-  if (!dyn_wave_ok(L) || L.S > 8 || h->prm.next_reset) return false;
-  const int64_t per_simd = L.S <= kObsChunk ? 4 : 2;
-  if (L.S > kObsChunk && (int64_t)L.B > 2 * (int64_t)L.simds) return false;
+  if (!dyn_wave_fits(L) || h->prm.next_reset) return false;
   const int k = step_kernel_of(h);
-  if (k == LBSIM_STEP_FUSED) return true;
-  return k == LBSIM_STEP_AUTO &&
-         (int64_t)L.B <= (max_b >= 0 ? max_b : per_simd * (int64_t)L.simds);
+  if (k == LBSIM_STEP_FUSED) return dyn_wave_ok(L);
+  return k == LBSIM_STEP_AUTO && (int64_t)L.B <= (max_b >= 0 ? max_b : 4 * (int64_t)L.simds);
 }
 
 // The fused step for this handle: its config (LBSIM_STEP_KERNEL=split|fused overrides AUTO) and

@@ -69,19 +69,29 @@ inline int dyn_group_lanes(const LaunchCtx& L) {
 // issue-bound, the groups win); S = 8 2048 envs 0.058 vs 0.078, 4096 0.087 vs 0.083.
 // LBSIM_DYN_WAVE_MAX_B overrides the limit; LBSIM_DYN_WAVE = 0 disables the kernel, 1 uses it at
 // every batch size it applies to; a forced LBSIM_DYN_GROUP_LANES width wins over both.
-inline bool dyn_wave_ok(const LaunchCtx& L) {
+inline int dyn_wave_mode() {
   static const int mode = [] {
     const char* e = std::getenv("LBSIM_DYN_WAVE");
     return e ? std::atoi(e) : -1;
   }();
+  return mode;
+}
+
+// Whether the wave dynamics can serve this handle at all (batch size aside).
+inline bool dyn_wave_fits(const LaunchCtx& L) {
+  static const bool forced_lanes = std::getenv("LBSIM_DYN_GROUP_LANES") != nullptr;
+  if (dyn_wave_mode() == 0 || forced_lanes || L.dyn_mapping == LBSIM_DYN_ENV_PER_LANE) return false;
+  if (L.S > 8 || L.prm.Q > 32 || L.prm.policy == LBSIM_POLICY_ALIAS) return false;
+  return L.prm.fail_thr == 0u;  // server failures: the group / env-lane kernels
+}
+
+inline bool dyn_wave_ok(const LaunchCtx& L) {
   static const int64_t max_b = [] {
     const char* e = std::getenv("LBSIM_DYN_WAVE_MAX_B");
     return e ? (int64_t)std::atoll(e) : (int64_t)-1;
   }();
-  static const bool forced_lanes = std::getenv("LBSIM_DYN_GROUP_LANES") != nullptr;
-  if (mode == 0 || forced_lanes || L.dyn_mapping == LBSIM_DYN_ENV_PER_LANE) return false;
-  if (L.S > 8 || L.prm.Q > 32 || L.prm.policy == LBSIM_POLICY_ALIAS) return false;
-  if (L.prm.fail_thr != 0u) return false;  // server failures: the group / env-lane kernels
+  if (!dyn_wave_fits(L)) return false;
+  const int mode = dyn_wave_mode();
   const int64_t per_simd = L.S <= 4 ? 4 : 2;  // S = 8: 2048 envs 0.058 vs 0.078 ms, 4096 0.087 vs 0.083
   return mode == 1 || (int64_t)L.B <= (max_b >= 0 ? max_b : per_simd * (int64_t)L.simds);
 }

@@ -2227,9 +2227,16 @@ __device__ __forceinline__ void observe_env_wave(const DevState& st, const SimPa
   if constexpr (MAXS <= kObsChunk) {  // one chunk: straight-line code, no loop-carried s0
     observe_chunk<true, true>(st, p, b, 0, S, sc, s_obs, lane, fresh);
   } else {
-    for (int s0 = 0; s0 < S; s0 += kObsChunk)
-      observe_chunk<true, true>(st, p, b, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk, sc, s_obs,
-                                lane, fresh);
+    // rolled, with b and lane opaque per chunk: nothing derived from them is hoisted and held
+    // across both chunks (step_wave_kernel<4, ..., 8>: 124 VGPRs instead of 184 B of spills/lane)
+#pragma clang loop unroll(disable)
+    for (int s0 = 0; s0 < S; s0 += kObsChunk) {
+      size_t bb = b;
+      int ln = lane;
+      asm volatile("" : "+s"(bb), "+v"(ln));
+      observe_chunk<true, true>(st, p, bb, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk, sc, s_obs,
+                                ln, fresh);
+    }
   }
   observe_outputs<MAXS, kModeStep, true>(st, p, out, b, s_obs, s_act, lane, 64);
   wave_sync();  // s_obs / s_act reused by the next env

@@ -52,13 +52,14 @@ __global__ void __launch_bounds__(64)
 // Both take 118-120 VGPRs with no spill since the one-chunk observe is straight-line code (the
 // chunk loop took 194 and spilled 64 under the 128 cap: profiles/r03o/).  Out of line, the observe
 // phase's call frames went through 1 KB of scratch per lane (0.141 ms).
-// MAXS = 8 (S = 5-8, OCC 2 only: the two chunks observed one after the other by the wave take
-// ~190 VGPRs): the wave dynamics' S <= 8 form, then both chunks.
+// MAXS = 8 (S = 5-8): the wave dynamics' S <= 8 form, then both chunks, one after the other, in a
+// rolled loop whose inputs are opaque to the compiler (observe_env_wave), so that no chunk-invariant
+// value is held across the two: 124 VGPRs, no scratch, hence OCC 4 too (hoisted, 170 and 184 B of
+// spills per lane at the 128 cap).
 template <int NG, int POLICY, bool TRACE, int OCC, int MAXS = kObsChunk>
 __global__ void __launch_bounds__(64, OCC)
     step_wave_kernel(DevState st, SimParams p, const void* action, int action_dtype,
                      int32_t* assign_out, ObsOutputs out) {
-  static_assert(MAXS == kObsChunk || OCC == 2, "S > 4 in one launch only at 2 waves per SIMD");
   __shared__ union {
     WaveLds dyn;
     ObsScratch obs;
@@ -78,12 +79,12 @@ template <int NG, int POLICY, int OCC>
 void launch_wo(const LaunchCtx& L, const void* action, int dtype, int32_t* assign,
                const ObsOutputs& o, hipStream_t s) {
   const dim3 block(64), grid((unsigned)L.B);
-  if constexpr (NG == 4) {  // S = 5-8 (OCC 2)
+  if constexpr (NG == 4) {  // S = 5-8: both chunks
     if (L.prm.trace)
-      LBSIM_LAUNCH((step_wave_kernel<4, POLICY, true, 2, 8>), grid, block, 0, s, L.st, L.prm,
+      LBSIM_LAUNCH((step_wave_kernel<4, POLICY, true, OCC, 8>), grid, block, 0, s, L.st, L.prm,
                    action, dtype, assign, o);
     else
-      LBSIM_LAUNCH((step_wave_kernel<4, POLICY, false, 2, 8>), grid, block, 0, s, L.st, L.prm,
+      LBSIM_LAUNCH((step_wave_kernel<4, POLICY, false, OCC, 8>), grid, block, 0, s, L.st, L.prm,
                    action, dtype, assign, o);
   } else {
     if (L.prm.trace)
@@ -105,7 +106,7 @@ void launch_w(const LaunchCtx& L, const void* action, int dtype, int32_t* assign
     const char* e = std::getenv("LBSIM_STEP_WAVE_OCC");
     return e ? std::atoi(e) : 0;
   }();
-  const bool occ2 = NG == 4 || forced == 2 || (forced != 4 && (int64_t)L.B <= 2 * (int64_t)L.simds);
+  const bool occ2 = forced == 2 || (forced != 4 && (int64_t)L.B <= 2 * (int64_t)L.simds);
   if (occ2) launch_wo<NG, POLICY, 2>(L, action, dtype, assign, o, s);
   else launch_wo<NG, POLICY, 4>(L, action, dtype, assign, o, s);
 }

@@ -343,13 +343,10 @@ def _expected_step_kernels(B, S, simds):
     """The default dispatch (lbsim_api.hip use_step_wave, lbsim_internal.h dyn_wave_ok /
     dyn_group_lanes, lbsim_step.hip launch_w) of a SED, Poisson, Q = 32 handle: {profile class:
     kernel-name prefix} of one step."""
-    wave = B <= (4 if S <= 4 else 2) * simds
-    if wave and S <= 4:
-        ng = 1 if S <= 2 else 2
+    if B <= 4 * simds and S <= 8:  # one launch; S = 5-8: both chunks observed by the wave
+        ng = 1 if S <= 2 else 2 if S <= 4 else 4
         occ = 2 if B <= 2 * simds else 4
-        return {4: f"step_wave_kernel<{ng}, 0, false, {occ}, 4>"}
-    if wave:  # S = 5-8: one launch at <= 2 envs per SIMD (the two-chunk observe, OCC 2)
-        return {4: "step_wave_kernel<4, 0, false, 2, 8>"}
+        return {4: f"step_wave_kernel<{ng}, 0, false, {occ}, {4 if S <= 4 else 8}>"}
     g = 2 if S <= 2 else (8 if B * 4 // 64 <= simds // 2 else 4) if S <= 4 else 8 if S <= 8 else 16
     return {0: f"dynamics_group_kernel<{g}, 0, 0, false", 1: "observe_kernel<"}
 
@@ -370,11 +367,11 @@ def test_configs1_default_dispatch_4096x4(lib, oracle_mod):
 
 
 @pytest.mark.parametrize("S,where", [(4, "2s"), (4, "2s+1"), (4, "4s"), (4, "4s+1"),
-                                     (8, "2s"), (8, "2s+1")])
+                                     (8, "2s"), (8, "2s+1"), (8, "4s"), (8, "4s+1")])
 def test_dispatch_boundaries_bit_exact(lib, oracle_mod, S, where):
     """Batches at the dispatch boundaries of the default step (in envs per SIMD of this device):
-    S = 4 at 2 and 4 envs per SIMD (step_wave_kernel OCC 2 -> OCC 4 -> server-per-lane groups),
-    S = 8 at 2 envs per SIMD (step_wave_kernel's two-chunk form -> groups).  The kernel that ran is checked by
+    S = 4 and S = 8 at 2 and 4 envs per SIMD (step_wave_kernel OCC 2 -> OCC 4 -> server-per-lane
+    groups; S = 8: the two-chunk forms).  The kernel that ran is checked by
     name (lbsim_launch_names), the results against the oracle on every env."""
     from marllb_amd import _lib
     simds = _simds()
@@ -391,16 +388,17 @@ def test_dispatch_boundaries_bit_exact(lib, oracle_mod, S, where):
 @pytest.mark.parametrize("occ", ["2", "4"])
 def test_step_wave_occupancy_forms_bit_exact(occ):
     """LBSIM_STEP_WAVE_OCC forces one occupancy form of the one-launch step_wave_kernel at every
-    batch size, so each simulator case the default dispatch sends to it (S <= 4, Q <= 32, not
+    batch size, so each simulator case the default dispatch sends to it (S <= 8, Q <= 32, not
     ALIAS, B <= 4 envs per SIMD: SED2, LSQ, LSQ2, trace arrivals, continuous and NaN actions, full
     rings, normalisation off) runs on the OCC-4 form that serves 2-4 envs per SIMD -- BASELINE
-    configs[1]'s 4096 x 4 -- and on the OCC-2 form.  Child process (read once per process)."""
+    configs[1]'s 4096 x 4 -- and on the OCC-2 form, the two-chunk S = 5-8 forms included.  Child
+    process (read once per process)."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     ks = [f"test_simulator_bit_exact_vs_oracle[{c}-{m}]" for c in range(len(CONFIGS))
           for m in ("server", "server-fused")
-          if CONFIGS[c]["S"] <= 4 and CONFIGS[c]["B"] <= 4096
+          if CONFIGS[c]["S"] <= 8 and CONFIGS[c]["B"] <= 4096
           and CONFIGS[c]["kw"].get("queue_capacity", 32) <= 32
           and CONFIGS[c]["kw"].get("assign_policy") != "alias"]
     assert len(ks) >= 20
