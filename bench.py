@@ -687,7 +687,7 @@ def main():
                            f"{S} servers (BASELINE configs[3] per GPU)",
                 "qmix": f"problem-05 QMIX: 4 agents x {S // 4} servers, per-agent GRU "
                         f"Q-networks (obs {4 * (S // 4) + 7 * S}) epsilon-greedy + mixing network "
-                        "(state 74) on the GPU each step (BASELINE configs[4] per GPU)"}[
+                        f"(state {4 * S + 10}) on the GPU each step (BASELINE configs[4] per GPU)"}[
                             args.workload]
             out["data"] = out["data"].replace("random discrete policy",
                                               "random-init network policy")

@@ -19,7 +19,7 @@
  *   ReservoirSampler.add / get_features       problem-01-reservoir-sampling/src/reservoir.py:50-196
  *   C twin reservoir_add / compute_stats      problem-01-reservoir-sampling/src/reservoir.h:118-268
  *   server assignment SED/SED2/LSQ/LSQ2       src/vpp/lb/node.c:388-441
- *   flow-completion samples (fct, duration)   src/vpp/lb/lbhash.h:87-172
+ *   flow-completion samples (fct, duration)   src/vpp/lb/lbhash.h:87-172 (duration: :129-136)
  * Full semantics: DESIGN.md §3 (the simulator spec the GPU kernels and oracle/ both implement).
  */
 #ifndef LBSIM_H
@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define LBSIM_ABI_VERSION 6
+#define LBSIM_ABI_VERSION 7
 #define LBSIM_MAX_SERVERS 64   /* S <= 64: BASELINE configs[4] read literally is 4 agents x 16 */
                                /* servers = 64 (S > 16: server-per-lane dynamics only)       */
 #define LBSIM_RESERVOIR_K 128  /* reservoir.py:31 capacity=128, reservoir.h:24               */
@@ -78,6 +78,15 @@ enum lbsim_assign_policy {
  * trace set with lbsim_set_trace (data/trace/poisson_for_loop/rate_N.csv). */
 enum lbsim_arrival_source { LBSIM_ARRIVAL_POISSON = 0, LBSIM_ARRIVAL_TRACE = 1 };
 
+/* The flow-duration sample of a completed flow (the reservoir behind obs columns 6-10 and the
+ * default reward field).  AGE (default): the flow's age at its last data packet, tc - t_arrival --
+ * VPP records time_now - t_init on every plain ACK after the first (src/vpp/lb/lbhash.h:129-136),
+ * the last one at the flow's completion, so the backlog wait is included (problem-01 README:
+ * "from first packet to last packet").  SERVICE: tc - max(t_arrival, predecessor's tc), the
+ * service time alone (the ABI-6 sample; independent of the queue, so a duration-based reward
+ * does not see the policy). */
+enum lbsim_duration_mode { LBSIM_DURATION_AGE = 0, LBSIM_DURATION_SERVICE = 1 };
+
 /* Dynamics-kernel mapping; every choice produces the same bits.  AUTO = SERVER_PER_LANE (faster
  * than one lane per env at every measured shape). */
 enum lbsim_dyn_mapping {
@@ -101,7 +110,7 @@ enum lbsim_dyn_kernel {
  * workgroups simulate their envs and then observe them: step_wave_kernel for
  * one-wave-per-env handles, fused_step_kernel for server-per-lane groups of <= 16 lanes (else
  * SPLIT); SPLIT: a dynamics launch and an observe launch.  AUTO: the one-launch step_wave_kernel
- * for one-wave-per-env handles with S <= 4 and at most 4 envs per SIMD (the single-env facade
+ * for one-wave-per-env handles with S <= 8 and at most 4 envs per SIMD (the single-env facade
  * and BASELINE configs[1]'s 4096 x 4 on 256 CUs; LBSIM_STEP_WAVE_MAX_B overrides the limit),
  * else SPLIT (the server-per-lane fused form measured slower).  The environment
  * variable LBSIM_STEP_KERNEL=split|fused overrides AUTO. */
@@ -160,6 +169,7 @@ typedef struct lbsim_config {
    * step needs no masked-reset launch; such a handle steps in two launches
    * (dynamics, observe), not the one-launch forms.  0 = off (the caller resets).             */
   int32_t next_step_reset;
+  int32_t duration_mode;     /* lbsim_duration_mode, default AGE            */
 } lbsim_config_t;
 
 typedef struct lbsim lbsim_t; /* opaque handle */

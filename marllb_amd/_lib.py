@@ -29,6 +29,7 @@ PROFILE_CLASSES = 5  # dynamics step, observe step, dynamics reset, observe rese
 DTYPE_I32, DTYPE_I64, DTYPE_F32 = 0, 1, 2
 METRICS = ["jain", "variance", "std", "cv", "max", "min", "product", "range", "gini"]
 POLICIES = ["sed", "sed2", "lsq", "lsq2", "alias"]
+DURATION_MODES = ("age", "service")  # lbsim_duration_mode
 
 
 class LbsimConfig(ctypes.Structure):
@@ -64,6 +65,7 @@ class LbsimConfig(ctypes.Structure):
         ("fail_prob", ctypes.c_float),
         ("recover_prob", ctypes.c_float),
         ("next_step_reset", ctypes.c_int32),
+        ("duration_mode", ctypes.c_int32),
     ]
 
 

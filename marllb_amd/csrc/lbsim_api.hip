@@ -33,6 +33,7 @@ constexpr int kLogMax = 8;
 thread_local const void* g_log_fn[kLogMax];
 thread_local int g_log_cls[kLogMax];
 thread_local int g_log_n = 0;
+thread_local int g_log_lost = 0;  // launches past kLogMax (reported, not dropped silently)
 thread_local int g_log_class = -1;
 }  // namespace
 
@@ -41,6 +42,8 @@ void lbk::note_launch(const void* host_fn) {
     g_log_fn[g_log_n] = host_fn;
     g_log_cls[g_log_n] = g_log_class;
     ++g_log_n;
+  } else {
+    ++g_log_lost;
   }
 }
 
@@ -72,6 +75,7 @@ struct lbsim {
   std::string err;
   // (class, host stub) of the kernels the last lbsim_step_ex / lbsim_reset_ex launched
   std::vector<std::pair<int, const void*>> launched[2];
+  int launched_lost[2] = {0, 0};  // launches of that call past the log's capacity
 };
 
 namespace {
@@ -161,9 +165,23 @@ int validate(const lbsim_config_t* c, char* msg, size_t n) {
       return bad("flow_timeout_s must be in [0, 3600]");
     if (c->flow_buckets < 1 || (double)c->flow_buckets / (double)c->arrival_rate > 100.0)
       return bad("flow_buckets must be >= 1 with flow_buckets / arrival_rate <= 100 s");
+    // the guess fct + (flow_timeout - 40 s) + wait is a signed int32 us sample: with the wait
+    // <= 16.7 x its mean (24-bit uniforms) and an fct of at most ~1,070 s (64 queued flows of
+    // <= 16.7 s service each at >= 1 flow/s), <= 1000 s for the other two terms keeps it below
+    // 2^31 us (lost_fct also saturates, for trace work beyond that bound)
+    if ((double)c->flow_timeout_s - 40.0 +
+            16.7 * (double)c->flow_buckets / (double)c->arrival_rate > 1000.0)
+      return bad("lost-FIN: flow_timeout_s - 40 + 16.7 * flow_buckets / arrival_rate must be "
+                 "<= 1000 s (the guessed fct is a signed 32-bit us sample)");
   }
+  if (c->lost_fin_prob > 0.0f && std::llround((double)c->lost_fin_prob * 16777216.0) == 0)
+    return bad("lost_fin_prob must be 0 or >= 2^-25 (a 24-bit threshold)");
   if (!(c->fail_prob >= 0.0f) || !(c->fail_prob <= 1.0f)) return bad("fail_prob must be in [0, 1]");
+  if (c->fail_prob > 0.0f && std::llround((double)c->fail_prob * 16777216.0) == 0)
+    return bad("fail_prob must be 0 or >= 2^-25 (a 24-bit threshold)");
   if (c->next_step_reset != 0 && c->next_step_reset != 1) return bad("next_step_reset must be 0 or 1");
+  if (c->duration_mode != LBSIM_DURATION_AGE && c->duration_mode != LBSIM_DURATION_SERVICE)
+    return bad("unknown duration_mode %d", c->duration_mode);
   if (!(c->recover_prob >= 0.0f) || !(c->recover_prob <= 1.0f))
     return bad("recover_prob must be in [0, 1]");
   if (c->dyn_mapping == LBSIM_DYN_ENV_PER_LANE && c->num_servers > 16)
@@ -207,6 +225,7 @@ void derive_params(const lbsim_config_t& c, SimParams& p) {
   p.rec_thr = (uint32_t)std::llround((double)c.recover_prob * 16777216.0);
   p.big_in_step = (p.dt_us >= (int32_t)kPackLimit || p.lf_thr != 0u) ? 1 : 0;
   p.next_reset = c.next_step_reset ? 1 : 0;
+  p.dur_service = c.duration_mode == LBSIM_DURATION_SERVICE ? 1 : 0;
 }
 
 // State sections in snapshot order.
@@ -295,6 +314,7 @@ struct ProfScope {
     if (rec) p.cls.push_back(cls);
   }
   ~ProfScope() {
+    g_log_class = -1;  // a launch outside any scope is logged with class -1, not a stale one
     if (!rec) return;
     Profiler& p = h->prof;
     (void)hipEventRecord(p.ev[p.used], s);
@@ -309,12 +329,17 @@ struct ProfScope {
 struct LaunchLog {
   lbsim_t* h;
   int which;
-  LaunchLog(lbsim_t* h_, int w) : h(h_), which(w) { g_log_n = 0; }
+  LaunchLog(lbsim_t* h_, int w) : h(h_), which(w) {
+    g_log_n = 0;
+    g_log_lost = 0;
+  }
   ~LaunchLog() {
     auto& v = h->launched[which];
     v.clear();
     for (int i = 0; i < g_log_n; ++i) v.emplace_back(g_log_cls[i], g_log_fn[i]);
+    h->launched_lost[which] = g_log_lost;
     g_log_n = 0;
+    g_log_lost = 0;
     g_log_class = -1;
   }
 };
@@ -486,6 +511,7 @@ int lbsim_config_default(lbsim_config_t* c) {
   c->flow_buckets = 1024;     // LB_DEFAULT_PER_CPU_STICKY_BUCKETS (lb.h:46)
   c->fail_prob = 0.0f;
   c->recover_prob = 0.1f;
+  c->duration_mode = LBSIM_DURATION_AGE;  // lbhash.h:129-136: the flow's age
   return LBSIM_OK;
 }
 
@@ -1065,6 +1091,10 @@ int lbsim_launch_names(lbsim_t* h, int which, char* buf, size_t buf_len) {
     if (!txt.empty()) txt += ';';
     txt += std::to_string(cls) + "=" + short_kernel_name(raw);
   }
+  // more launches than the log holds: a marker no counter file is keyed by
+  if (h->launched_lost[which] > 0)
+    txt += (txt.empty() ? "" : ";") + std::string("-1=truncated(") +
+           std::to_string(h->launched_lost[which]) + " more)";
   if (txt.size() + 1 > buf_len)
     return fail(h, LBSIM_ESHAPE, "launch names need %zu bytes", txt.size() + 1);
   memcpy(buf, txt.c_str(), txt.size() + 1);

@@ -309,8 +309,8 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
     if (ins && slot >= 0) {
       const uint32_t fct = lost_fct(p, (uint32_t)(tc_a - ta),
                                     gc.base_ms * 1000u + gc.base_rem + (uint32_t)ta, E.gid, E.episode);
-      my_res[(uint32_t)slot] =
-          make_uint3(fct, (uint32_t)svc, gc.base_ms + (gc.base_rem + (uint32_t)tc_a) / 1000u);
+      my_res[(uint32_t)slot] = make_uint3(fct, dur_sample(p, tc_a, ta, start_a),
+                                          gc.base_ms + (gc.base_rem + (uint32_t)tc_a) / 1000u);
       mark(slot);
     }
     if (mine) {
@@ -409,7 +409,7 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
       if (slot >= 0) {
         const uint32_t fct =
             lost_fct(p, (uint32_t)(etc - eta), (uint32_t)base_us + (uint32_t)eta, E.gid, E.episode);
-        const uint32_t dur = (uint32_t)(etc - (eta > prev ? eta : prev));
+        const uint32_t dur = dur_sample(p, etc, eta, eta > prev ? eta : prev);
         V.big |= big_record(fct, dur);
         my_res[(uint32_t)slot] = make_uint3(fct, dur, base_ms + (base_rem + (uint32_t)etc) / 1000u);
         mark(slot);

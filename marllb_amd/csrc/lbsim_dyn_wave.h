@@ -202,7 +202,9 @@ __device__ __forceinline__ void wave_flush(const SimParams& p, WaveSrv& V, WaveE
     svc = svc < 1 ? 1 : svc;
     const uint32_t fct = lost_fct(p, (uint32_t)(Bt.ltc - Bt.ta),
                                   base_ms * 1000u + base_rem + (uint32_t)Bt.ta, E.gid, E.episode);
-    res_b[key] = make_uint3(fct, (uint32_t)svc, base_ms + (base_rem + (uint32_t)Bt.ltc) / 1000u);
+    // duration (dur_sample): the age ltc - ta, or the service time svc = ltc - start
+    const uint32_t dur = p.dur_service ? (uint32_t)svc : (uint32_t)(Bt.ltc - Bt.ta);
+    res_b[key] = make_uint3(fct, dur, base_ms + (base_rem + (uint32_t)Bt.ltc) / 1000u);
   }
 }
 
@@ -456,7 +458,7 @@ __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParam
       if (slot >= 0) {
         const uint32_t fct =
             lost_fct(p, (uint32_t)(e.x - e.y), (uint32_t)base_us + (uint32_t)e.y, E.gid, E.episode);
-        const uint32_t dur = (uint32_t)(e.x - (e.y > prev ? e.y : prev));
+        const uint32_t dur = dur_sample(p, e.x, e.y, e.y > prev ? e.y : prev);
         if (big_record(fct, dur)) Ld.big[lane] = 1u;  // this lane's own server
         res_b[(uint32_t)lane * K + (uint32_t)slot] =
             make_uint3(fct, dur, base_ms + (base_rem + (uint32_t)e.x) / 1000u);

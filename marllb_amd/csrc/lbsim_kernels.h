@@ -116,6 +116,9 @@ struct SimParams {
   int32_t next_reset;
   // envs per wave of dynamics_group_kernel (0: 64 / G, every lane used); set by its launcher
   int32_t dyn_epw;
+  // lbsim_config_t::duration_mode == SERVICE (dur_sample): the duration sample is the service
+  // time, not the flow's age
+  int32_t dur_service;
 };
 
 constexpr uint32_t kStreamFailure = 5u;  // Philox stream of the failure / recovery draws
@@ -166,6 +169,14 @@ __device__ __forceinline__ uint32_t lf_mix(uint32_t h) {
   return h;
 }
 
+// fct + off + wait as a signed int32 us sample, saturated (the config bound keeps it in range for
+// Poisson work; trace work is unbounded).  oracle: the same.
+__device__ __forceinline__ uint32_t lf_guess(uint32_t fct, int32_t off, int32_t wait) {
+  int64_t g = (int64_t)(int32_t)fct + (int64_t)off + (int64_t)wait;
+  g = g > (int64_t)INT32_MAX ? (int64_t)INT32_MAX : (g < (int64_t)INT32_MIN ? (int64_t)INT32_MIN : g);
+  return (uint32_t)(int32_t)g;
+}
+
 // The fct sample of a completed flow, fct = tc - ta (lbhash.h:116-124, RSTACK: now - t_init), or,
 // for a flow whose FIN/RST the data plane missed (probability lost_fin_prob), VPP's timed-out guess
 // (lbhash.h:175-217): the entry expires flow_timeout after the flow's last packet (its completion),
@@ -184,7 +195,17 @@ __device__ __forceinline__ uint32_t lost_fct(const SimParams& p, uint32_t fct, u
   if ((h >> 8) >= p.lf_thr) return fct;
   const uint32_t h2 = lf_mix(h ^ 0x6A09E667u);
   const int32_t wait = (int32_t)(-lb_logf(u01_open0(h2)) * p.lf_wait_us);
-  return fct + (uint32_t)p.lf_off_us + (uint32_t)wait;
+  return lf_guess(fct, p.lf_off_us, wait);
+}
+
+// The flow-duration sample of a flow completing at tc that arrived at ta.  AGE
+// (default): the flow's age at its last data packet, tc - ta -- VPP records time_now - t_init on
+// every plain ACK after the first (lbhash.h:129-136), the last one at the completion -- so the
+// backlog wait is in it.  SERVICE (p.dur_service, a uniform branch): tc - start, start = max(ta,
+// the predecessor's tc), the service time alone.
+__device__ __forceinline__ uint32_t dur_sample(const SimParams& p, int32_t tc, int32_t ta,
+                                               int32_t start) {
+  return (uint32_t)(tc - (p.dur_service ? start : ta));
 }
 
 constexpr uint32_t kTraceEnvStride = 7919u;        // SURVEY §8d C3 per-env offset
@@ -744,7 +765,7 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
     int32_t svc = (int32_t)(L.next_work * c_scale);
     svc = svc < 1 ? 1 : svc;
     const int32_t tc_a = start_a + svc;
-    // completes in this step: its sample now (duration = tc - max(ta, predecessor's tc) = svc)
+    // completes in this step: its sample now (duration: age tc - ta, or svc = tc - start)
     const bool ins = push && tc_a <= dt;
 
     // ---- one Philox block, the next arrival's; the pushed flow's Algorithm R draw is this
@@ -755,8 +776,8 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
     if (ins && slot >= 0) {
       const uint32_t fct = lost_fct(p, (uint32_t)(tc_a - ta),
                                     ec.base_ms * 1000u + ec.base_rem + (uint32_t)ta, L.gid, L.episode);
-      my_res[(uint32_t)cs * (uint32_t)K + (uint32_t)slot] =
-          make_uint3(fct, (uint32_t)svc, ec.base_ms + (ec.base_rem + (uint32_t)tc_a) / 1000u);
+      my_res[(uint32_t)cs * (uint32_t)K + (uint32_t)slot] = make_uint3(
+          fct, dur_sample(p, tc_a, ta, start_a), ec.base_ms + (ec.base_rem + (uint32_t)tc_a) / 1000u);
       mark_slot<MAXS>(l, cs, slot);
     }
     // queue index < WL: the LDS window (a push that does not happen writes the lane's scratch
@@ -836,7 +857,7 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
 // One simulated step of dt_us with server weights w[] (env.py:230-259 with real dynamics).
 //
 // Arrival-driven, as the oracle: a FIFO server fixes a flow's completion time when the flow is
-// queued (tc = max(ta, tail) + svc), so its completion sample {fct = tc - ta, duration = svc,
+// queued (tc = max(ta, tail) + svc), so its completion sample {fct = tc - ta, duration (dur_sample),
 // ts(tc)} is known at the push, and a server's reservoir sees its samples in FIFO order whatever
 // the interleaving with other servers.  So:
 //   1. flows carried in from earlier steps that complete in this one are inserted first, server
@@ -935,7 +956,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
         if (slot >= 0) {
           const uint32_t fct =
               lost_fct(p, (uint32_t)(etc - eta), (uint32_t)base_us + (uint32_t)eta, L.gid, L.episode);
-          const uint32_t dur = (uint32_t)(etc - (eta > prev ? eta : prev));
+          const uint32_t dur = dur_sample(p, etc, eta, eta > prev ? eta : prev);
           L.bigm |= big_record(fct, dur) ? 1u << s : 0u;
           my_res[(uint32_t)s * (uint32_t)K + (uint32_t)slot] =
               make_uint3(fct, dur, base_ms + (base_rem + (uint32_t)etc) / 1000u);

@@ -43,8 +43,8 @@ __global__ void __launch_bounds__(64)
   }
 }
 
-// The small-batch step (dyn_wave_ok: S <= 4, at most 4 envs per SIMD): one wave per env steps it
-// (dyn_wave_env) and then observes it (observe_env_wave: S <= 4 is one chunk, one wave), so the
+// The small-batch step (dyn_wave_fits: S <= 8, at most 4 envs per SIMD): one wave per env steps it
+// (dyn_wave_env) and then observes it (observe_env_wave: one chunk for S <= 4, two for 5-8), so the
 // step is ONE launch and each env's observation runs as soon as its own event loop ends, while
 // slower envs still simulate.  Same routines, same order: the same bits as the two launches.
 // OCC waves per SIMD.  2: batches of at most 2 envs per SIMD, with the VALU queue counts (the

@@ -105,7 +105,8 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
                 dyn_mapping: str = "auto", step_kernel: str = "auto",
                 lost_fin_prob: float = 0.0, flow_timeout: float = 40.0, flow_buckets: int = 1024,
                 fail_prob: float = 0.0, recover_prob: float = 0.1,
-                next_step_reset: bool = False) -> _lib.LbsimConfig:
+                next_step_reset: bool = False,
+                duration_mode: str = "age") -> _lib.LbsimConfig:
     """Build and validate an lbsim_config_t from reference-style kwargs.
 
     server_rates defaults to identical servers at utilisation `load`: mu = rate / (load * S).
@@ -123,6 +124,10 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
     lost) and a down one recovers (THEORY.md §6.4 server_failure ~ Bernoulli(p_fail)).  0 = off.
     next_step_reset: lbsim_step resets, in place of stepping, the envs whose last step returned
     done (gymnasium's NEXT_STEP autoreset; VecLoadBalanceEnv(autoreset_mode="next_step")).
+    duration_mode: the flow-duration sample (obs columns 6-10, the default reward field): "age"
+    = the flow's age at its last data packet, completion - arrival, backlog wait included
+    (src/vpp/lb/lbhash.h:129-136 records time_now - t_init on every plain ACK after the first);
+    "service" = the service time alone.
     """
     if reward_metric not in _lib.METRICS:  # rewards.py:321-323
         raise ValueError(f"Unsupported metric: {reward_metric}. Supported: {_lib.METRICS}")
@@ -177,6 +182,9 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
     cfg.fail_prob = float(fail_prob)
     cfg.recover_prob = float(recover_prob)
     cfg.next_step_reset = 1 if next_step_reset else 0
+    if duration_mode not in _lib.DURATION_MODES:
+        raise ValueError(f"Unknown duration_mode: {duration_mode}. Supported: {_lib.DURATION_MODES}")
+    cfg.duration_mode = _lib.DURATION_MODES.index(duration_mode)
     _lib.validate(cfg)
     return cfg
 
@@ -627,7 +635,7 @@ class LoadBalanceEnv:
             v.reset()
         io = self._io if self._io is not None else self._io_buffers()
         cur = _torch().cuda.current_stream(v.device)
-        if cur.cuda_stream != io[7].value:
+        if cur.cuda_stream != (io[7].value or 0):  # c_void_p(0).value is None
             # the caller switched streams since the buffers were made: launch on the current one,
             # so the step stays ordered after a reset() / _upstream issued on it
             io = self._io = io[:6] + (cur, ctypes.c_void_p(cur.cuda_stream)) + io[8:]

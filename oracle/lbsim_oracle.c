@@ -16,7 +16,8 @@
  *   - _normalize_observation (float64)                env.py:450-470
  *   - step/reset bookkeeping (done, return)           env.py:186-286
  *   - SED/SED2/LSQ/LSQ2 server choice                 src/vpp/lb/node.c:388-441
- *   - completion samples fct / duration               src/vpp/lb/lbhash.h:116-135
+ *   - completion samples fct / duration               src/vpp/lb/lbhash.h:116-135 (duration
+ *     = the flow's age at its last data packet, :129-136)
  *   - lost-FIN flows' timed-out fct guess             src/vpp/lb/lbhash.h:175-217, stats.h:27
  *   - server failure / recovery (Bernoulli per step)  problem-03 THEORY.md §6.4 (:687-693)
  * plus the flow dynamics the reference does not have (Poisson arrivals, per-server
@@ -561,7 +562,10 @@ uint32_t oracle_lost_fin_fct(uint32_t fct, uint32_t abs_ta, uint32_t gid, uint32
   if ((h >> 8) >= thr) return fct;
   const uint32_t h2 = lf_mix(h ^ 0x6A09E667u);
   const int32_t wait = (int32_t)(-oracle_logf(u01(h2)) * wait_us);
-  return fct + (uint32_t)off_us + (uint32_t)wait;
+  /* signed int32 us, saturated (the config bound keeps Poisson work in range) */
+  int64_t g = (int64_t)(int32_t)fct + (int64_t)off_us + (int64_t)wait;
+  g = g > (int64_t)INT32_MAX ? (int64_t)INT32_MAX : (g < (int64_t)INT32_MIN ? (int64_t)INT32_MIN : g);
+  return (uint32_t)(int32_t)g;
 }
 
 /* Algorithm R slot for a flow that arrived in the step it completes in: the draw
@@ -639,7 +643,13 @@ static void pop_until(env_ctx* e, int s, int32_t t, uint64_t base_us, double den
     const uint32_t fct = oracle_lost_fin_fct((uint32_t)(tc - ta), (uint32_t)base_us + (uint32_t)ta,
                                              e->gid, o->episode[e->b], o->key[0], o->key[1],
                                              o->lf_thr, o->lf_off_us, o->lf_wait_us);
-    const uint32_t dur = (uint32_t)(tc - start);
+    /* the flow-duration sample: VPP records time_now - t_init on every plain ACK after the first
+     * (lbhash.h:129-136: states ACKed / PSHACKed), the last one at the flow's last data packet --
+     * its completion here -- so the sample is the flow's age tc - ta, queueing wait included
+     * (problem-01 README "from first packet to last packet"); duration_mode SERVICE keeps the
+     * service time tc - max(ta, predecessor's tc) */
+    const uint32_t dur =
+        (uint32_t)(tc - (o->cfg.duration_mode == LBSIM_DURATION_SERVICE ? start : ta));
     o->last_tc[sb] = tc;
     const uint32_t ts_ms = (uint32_t)((base_us + (uint64_t)(int64_t)tc) / 1000u);
     /* ta >= 0: arrived in this step (times are relative to the step start) */

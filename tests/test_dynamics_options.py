@@ -1,4 +1,4 @@
-"""The optional dynamics of DESIGN.md §3.4 / §3.9 on the CPU oracle (their GPU parity is in
+"""The duration sample and the optional dynamics of DESIGN.md §3.4 / §3.9 on the CPU oracle (their GPU parity is in
 tests/test_gpu_parity.py CONFIGS): lost-FIN flows (VPP's timed-out flow sample,
 src/vpp/lb/lbhash.h:175-217) and server failure / recovery (problem-03 THEORY.md §6.4).
 
@@ -164,3 +164,69 @@ def test_next_step_reset_equals_same_step_shifted(oracle_mod):
     np.testing.assert_array_equal(nxt.state_bytes(), same.state_bytes())
     nxt.close()
     same.close()
+
+
+def test_duration_sample_is_the_flow_age(oracle_mod):
+    """duration_mode="age" (default): the flow-duration sample is the flow's age at its last data
+    packet, completion - arrival (VPP records time_now - t_init on every plain ACK after the first,
+    src/vpp/lb/lbhash.h:129-136), so it includes the backlog wait: with lost-FIN off it equals the
+    fct sample slot for slot, it is >= the service time of duration_mode="service", and strictly
+    larger for flows that queued.  Everything else (queues, slots, counts, fct, timestamps) is the
+    same in both modes (the feature cache and the episode return follow the samples)."""
+    B, S, steps = 96, 4, 8
+    age, _ = _run(oracle_mod, B, S, steps, load=1.1)
+    svc, _ = _run(oracle_mod, B, S, steps, load=1.1, duration_mode="service")
+    for k in age:
+        if k not in ("res", "res_dur", "fcache", "ep_return"):
+            np.testing.assert_array_equal(age[k], svc[k], err_msg=k)
+    n = np.minimum(age["res_count"], 128).reshape(B, S)
+    valid = (np.arange(128)[None, None, :] < n[:, :, None]).reshape(-1)
+    a = age["res_dur"][valid].astype(np.int64)
+    s = svc["res_dur"][valid].astype(np.int64)
+    np.testing.assert_array_equal(a, age["res_fct"][valid].astype(np.int64))
+    assert (a >= s).all() and (s >= 1).all()
+    assert (a > s).mean() > 0.3, "at load 1.1 most flows wait behind another"
+
+
+def _reward_balanced_vs_skewed(oracle_mod, **kw):
+    """Mean default reward (Jain over column 10, flow_duration_avg_decay) of 512 envs x 4 servers
+    over 40 steps after 20, all weights 1.0 vs weights [2, 1, 1, 1] (discrete levels 0 / 2)."""
+    from marllb_amd.env import make_config
+    out = []
+    for row in ([0, 0, 0, 0], [2, 0, 0, 0]):
+        ora = oracle_mod.OracleEnv(make_config(512, 4, seed=7, **kw), threads=8)
+        ora.reset()
+        a = np.tile(np.array(row, np.int64), (512, 1))
+        for _ in range(20):
+            ora.step(a)
+        out.append(float(np.mean([ora.step(a)[1].mean() for _ in range(40)])))
+        ora.close()
+    return out
+
+
+def test_default_reward_sees_the_policy(oracle_mod):
+    """problem-03's reward is Jain fairness over flow_duration_avg_decay (THEORY.md:616, env.py:79).
+    With the duration sample as the flow's age the skewed weights [2, 1, 1, 1] -- server 0 carries
+    ~2.7x the flows in flight -- lower the reward by >= 0.03; with the service-time sample
+    (duration_mode="service") the reward cannot see the policy (the two differ by < 0.005)."""
+    bal, skew = _reward_balanced_vs_skewed(oracle_mod)
+    assert bal - skew >= 0.03, (bal, skew)
+    bal_s, skew_s = _reward_balanced_vs_skewed(oracle_mod, duration_mode="service")
+    assert abs(bal_s - skew_s) < 0.005, (bal_s, skew_s)
+
+
+def test_lost_fin_guess_at_the_accepted_limit(oracle_mod):
+    """The largest accepted lost-FIN offset (flow_timeout - 40 s + 16.7 x the mean bucket wait at
+    the 1000 s bound): every guessed sample stays a positive signed 32-bit us value equal to
+    fct + (flow_timeout - 40 s) + wait, wait >= 0 (no int32 wrap)."""
+    B, S, steps = 64, 4, 6
+    timeout = 40.0 + 1000.0 - 16.7 * 1024 / 400.0  # flow_buckets 1024 at 400 flows/s: 42.75 s
+    st0, _ = _run(oracle_mod, B, S, steps)
+    st, _ = _run(oracle_mod, B, S, steps, lost_fin_prob=1.0, flow_timeout=timeout)
+    n = np.minimum(st0["res_count"], 128).reshape(B, S)
+    valid = (np.arange(128)[None, None, :] < n[:, :, None]).reshape(-1)
+    f0 = st0["res_fct"].view(np.int32)[valid].astype(np.int64)
+    f1 = st["res_fct"].view(np.int32)[valid].astype(np.int64)
+    wait = f1 - f0 - (int(round(timeout * 1e6)) - 40_000_000)
+    assert (f1 > 0).all() and (wait >= 0).all()
+    assert f1.max() < 2 ** 31 - 1

@@ -84,8 +84,23 @@ def test_optional_dynamics_config():
                     ({"lost_fin_prob": 0.1, "flow_buckets": 0}, "flow_buckets"),
                     ({"lost_fin_prob": 0.1, "flow_buckets": 10 ** 6}, "flow_buckets"),
                     ({"fail_prob": -0.1}, "fail_prob"),
-                    ({"recover_prob": 2.0}, "recover_prob")]:
+                    ({"recover_prob": 2.0}, "recover_prob"),
+                    # a nonzero probability below the 24-bit threshold's resolution
+                    ({"fail_prob": 1e-9}, "fail_prob"),
+                    ({"lost_fin_prob": 1e-9}, "lost_fin_prob"),
+                    # the guessed fct must fit a signed 32-bit us sample
+                    ({"lost_fin_prob": 0.1, "flow_timeout": 3600.0}, "signed 32-bit"),
+                    ({"lost_fin_prob": 0.1, "flow_timeout": 600.0, "flow_buckets": 40000},
+                     "signed 32-bit"),
+                    ({"duration_mode": "wall"}, "duration_mode")]:
         with pytest.raises(ValueError, match=msg):
             E.make_config(8, 4, **kw)
     with pytest.raises(ValueError, match="autoreset_mode"):
         E.VecLoadBalanceEnv(8, 4, autoreset_mode="sometimes")
+
+
+def test_duration_mode_config():
+    """duration_mode (include/lbsim.h lbsim_duration_mode): the flow's age (lbhash.h:129-136) by
+    default, the service time on request."""
+    assert E.make_config(8, 4).duration_mode == 0
+    assert E.make_config(8, 4, duration_mode="service").duration_mode == 1

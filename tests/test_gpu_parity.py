@@ -243,6 +243,14 @@ CONFIGS = [
     dict(B=30, S=20, kw={"max_steps": 2, "next_step_reset": True, "fail_prob": 0.1,
                          "lost_fin_prob": 0.2}),
     dict(B=8256, S=4, kw={"max_steps": 5, "next_step_reset": True}),
+    # duration_mode="service" (the service-time duration sample; the default is the flow's age,
+    # lbhash.h:129-136): one-wave-per-env (full rings), server-per-lane groups (S = 20, B > the
+    # small-batch limit), lost-FIN guesses beside it
+    dict(B=64, S=3, kw={"duration_mode": "service", "queue_capacity": 6, "load": 1.3}),
+    dict(B=40, S=20, kw={"duration_mode": "service", "assign_policy": "sed2",
+                         "arrival_rate": 800.0}),
+    dict(B=48, S=8, kw={"duration_mode": "service", "lost_fin_prob": 0.2, "flow_timeout": 10.0}),
+    dict(B=8256, S=4, kw={"duration_mode": "service", "load": 1.1}),
 ]
 
 
@@ -509,6 +517,38 @@ def test_full_size_properties(lib, oracle_mod):
     np.testing.assert_array_equal(obs[off:off + n].cpu().numpy(), oo)
     np.testing.assert_array_equal(rew[off:off + n].cpu().numpy(), ro)
     assert st["dropped"].sum() == 0
+
+
+@pytest.mark.parametrize("B", [512, 65536])
+def test_default_reward_sees_the_policy(lib, oracle_mod, B):
+    """problem-03's default reward, Jain over flow_duration_avg_decay (THEORY.md:616, env.py:79),
+    with the duration sample as the flow's age (lbhash.h:129-136): weights
+    [2, 1, 1, 1] lower the mean reward by >= 0.03 against all-1.0 weights (40 steps after 20) on
+    the HIP path, at 512 x 4 bit-exact vs the oracle and at the headline 65536 x 4."""
+    from marllb_amd.env import VecLoadBalanceEnv, make_config
+    S = 4
+    means = []
+    for row in ([0, 0, 0, 0], [2, 0, 0, 0]):
+        env = VecLoadBalanceEnv(B, S, device="cuda:0", seed=7, autoreset=False)
+        ora = None
+        if B <= 512:
+            ora = oracle_mod.OracleEnv(make_config(B, S, seed=7), threads=8)
+            ora.reset()
+        env.reset()
+        a = torch.tensor(row, dtype=torch.int64).repeat(B, 1)
+        acc = []
+        for k in range(60):
+            _, rew, _, _ = env.step(a)
+            if ora is not None:
+                _, ro, _, _ = ora.step(a.numpy())
+                np.testing.assert_array_equal(rew.cpu().numpy(), ro)
+            if k >= 20:
+                acc.append(rew.double().mean().item())
+        means.append(float(np.mean(acc)))
+        env.close()
+        if ora is not None:
+            ora.close()
+    assert means[0] - means[1] >= 0.03, means
 
 
 def test_grid_above_four_waves_per_simd_s4(lib, oracle_mod):
