@@ -34,10 +34,12 @@ STEP_INTERVAL = 0.25   # simulated seconds per step
 K = 128
 
 
-def algorithmic_bytes(S: int, slots_per_env: float, inflight_per_env: float):
+def algorithmic_bytes(S: int, slots_per_env: float, inflight_per_env: float, paired: bool = False):
     """Bytes each kernel must move per env-step with the state layout of DESIGN.md §4.
 
-    observe : read the 128 slot records (fct, dur, ts: 12 B each) + hc + res_count per server,
+    observe : read the 128 slot records (fct, dur, ts: 12 B each; paired -- observe_pair_kernel,
+              records whose duration word equals the fct word -- needs fct and ts only, 8 B, though
+              the 12-B records put both words in the same 64-B segments) + hc + res_count per server,
               ep_step/ep_return read+write, obs 44 B/server, reward 4, done 1, ep outputs 12.
     dynamics: env header (8 x 4 B) and per-server hc/last_tc/res_count read+write, action 8 B and
               assign count 4 B per server, the reservoir slots actually written (12 B each,
@@ -47,12 +49,26 @@ def algorithmic_bytes(S: int, slots_per_env: float, inflight_per_env: float):
     fused   : one launch does both, so both (the observe reads of freshly written records are
               algorithmic traffic even when L2 serves them).
     """
-    obs = S * (K * 12 + 8 + 44) + 12 + 12 + 4 + 1 + 12
+    obs = S * (K * (8 if paired else 12) + 8 + 44) + 12 + 12 + 4 + 1 + 12
     dyn = 2 * 32 + S * (2 * 12 + 8 + 4) + 12 * slots_per_env + 16 * inflight_per_env
     return {"observe_kernel": obs, "dynamics_kernel": dyn, "fused_step_kernel": obs + dyn}
 
 
-def valu_roofline(B: int, S: int, avg: dict, sigs: dict):
+def phase_mismatch(workload, slots_per_env: float, name: str, tol: float = 0.10):
+    """None if a committed counter file was collected on the same work as this run -- the
+    reservoir slots written per env-step of its timed steps (the episode phase: early steps write
+    more slots) within `tol` of this run's -- else the reason its counters do not apply."""
+    if not workload or workload.get("slots_per_env_step") is None:
+        return f"profiles/{name} does not record the slots per env-step its counters were taken at"
+    ref = workload["slots_per_env_step"]
+    if abs(ref - slots_per_env) > tol * max(slots_per_env, 1e-9):
+        return (f"profiles/{name} was collected at {ref:.2f} reservoir slots per env-step "
+                f"(steps {workload.get('bench_steps')}, warm-up {workload.get('bench_warmup')}); "
+                f"this run wrote {slots_per_env:.2f}: another episode phase, counters not applied")
+    return None
+
+
+def valu_roofline(B: int, S: int, avg: dict, sigs: dict, slots_per_env: float = None):
     """The VALU side of each simulator kernel, from profiles/pmc_valu.json
     (tools/pmc_valu.py over rocprofv3 SQ counter passes of this workload, VALU issue costs measured
     by tools/ubench_valu.hip): VALU instructions per env-step and per class, the SIMD issue cycles
@@ -69,8 +85,13 @@ def valu_roofline(B: int, S: int, avg: dict, sigs: dict):
     if t.get("batch") != B or t.get("servers") != S:
         return None
     out = {"source": "profiles/pmc_valu.json", "simds": t["simds"], "clock_hz": t["clock_hz"],
-           "issue_costs_simd_cyc": t["ubench_simd_cyc_per_inst"]}
+           "issue_costs_simd_cyc": t["ubench_simd_cyc_per_inst"], "workload": t.get("workload")}
+    phase = phase_mismatch(t.get("workload"), slots_per_env, "pmc_valu.json") \
+        if slots_per_env is not None else None
     for name in avg:
+        if phase is not None:
+            out[name] = {"pmc_kernel": None, "ran": sigs.get(name), "stale_reason": phase}
+            continue
         full = sigs.get(name)
         rec = t["kernels"].get(full) if full else None
         if rec is None:
@@ -607,11 +628,14 @@ def main():
         ran = _lib.launch_names(handle, 0) if hasattr(lib, "lbsim_launch_names") else {}
         fused = ran.get(4, "").split("<")[0] or (
             "step_wave_kernel" if dyn == "dynamics_wave_kernel" else "fused_step_kernel")
-        names = {0: dyn, 1: "observe_kernel", 4: fused}
+        obs_name = ran.get(1, "observe_kernel").split("<")[0]
+        names = {0: dyn, 1: obs_name, 4: fused}
         avg = {names[i]: ms[i] / cnt[i] for i in names if cnt[i] > 0}
         rate = tr.rate if tr is not None else ARRIVAL_RATE
         slots, inflight = step_accounting(handle, lib, one_step, args.steps, replay)
-        abytes = algorithmic_bytes(S, slots / B, inflight / B)
+        abytes = algorithmic_bytes(S, slots / B, inflight / B,
+                                   paired=obs_name == "observe_pair_kernel")
+        abytes[obs_name] = abytes.pop("observe_kernel")
         abytes[dyn] = abytes.pop("dynamics_kernel")
         abytes[fused] = abytes.pop("fused_step_kernel")
         per_kernel = {}
@@ -626,19 +650,22 @@ def main():
         dom = max(avg, key=avg.get)
         ab = abytes[dom] * B
         achieved = ab / (avg[dom] * 1e-3) / 1e9
-        valu = valu_roofline(B, S, avg, sigs)
-        traffic, traffic_note = None, None
+        valu = valu_roofline(B, S, avg, sigs, slots / B)
+        traffic, traffic_note, traffic_workload = None, None, None
         tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tfile):
             t = json.load(open(tfile))
             held = t.get("bytes_per_launch", {})
+            traffic_workload = t.get("workload")
             if t.get("batch") != B or t.get("servers") != S:
                 traffic_note = f"profiles/pmc_traffic.json is for {t.get('batch')} x {t.get('servers')}"
-            elif sigs.get(dom) in held:
-                traffic = held[sigs[dom]]
-            else:
+            elif sigs.get(dom) not in held:
                 traffic_note = (f"profiles/pmc_traffic.json has no counters for {sigs.get(dom)!r} "
                                 f"(it holds {sorted(held)})")
+            else:
+                traffic_note = phase_mismatch(traffic_workload, slots / B, "pmc_traffic.json")
+                if traffic_note is None:
+                    traffic = held[sigs[dom]]
         out = {
             "metric": METRIC, "value": value, "unit": "env-steps/s",
             "n_gpus": dist.get_world_size() if world > 1 else 1,
@@ -664,6 +691,7 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "traffic_source": "profiles/pmc_traffic.json"
                          if traffic is not None else None, "stale_reason": traffic_note,
+                         "traffic_workload": traffic_workload,
                          "signature": sigs.get(dom), "algorithmic_bytes_per_launch": ab,
                          "avg_launch_ms": avg[dom],
                          "kernel_avg_ms": avg, "kernels": per_kernel, "valu": valu,

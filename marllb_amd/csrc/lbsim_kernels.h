@@ -2059,6 +2059,253 @@ __device__ double reward_of(const float* obs, int S, int metric, int field) {
                        [&](int i) { return (double)obs[nth_bit(act, i) * NF + field]; }, metric);
 }
 
+// ================================================================ paired observe (8 rows per wave)
+//
+// With the default duration sample (duration_mode AGE: both samples of a flow are tc - ta,
+// DESIGN.md §3.4) and lost-FIN off, every record the dynamics write holds dur == fct, so a
+// server's duration reservoir equals its fct reservoir slot for slot (same values, timestamps and
+// count) and its 5 duration features equal its 5 fct features bit for bit.  observe_pair_kernel
+// then computes each server's features once: one wave takes 8 consecutive (env, server) rows --
+// 8 / S envs, S in {1, 2, 4, 8} -- and lane (u, j) holds slots 8 e + j of row u (the fct word
+// and the timestamp of each record), so a wave does the work observe_kernel spreads over two.
+// Same operations in the same order as observe_chunk_regs' fct group: the same bits.
+
+// (uint64_t)(w * 2^48) for w in [0, 1], from the f32 weight: hi = floor(x / 2^32), lo = the
+// exact remainder x - hi 2^32 (x has <= 24 significant bits, so the remainder is a float), both
+// truncated as the conversion truncates.
+__device__ __forceinline__ uint64_t fixed48(float w) {
+  const float x = w * 281474976710656.0f;
+  const float hf = floorf(x * 2.3283064365386963e-10f);
+  const uint32_t hi = (uint32_t)hf;
+  const uint32_t lo = (uint32_t)fmaf(hf, -4294967296.0f, x);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+template <bool FULL>
+__device__ __forceinline__ void observe_rows_paired_regs(const DevState& st, const SimParams& p,
+                                                         size_t row0, int nrows, int n_in,
+                                                         ObsScratch& sc, float* obs_out, int lane) {
+  const int u = lane >> 3, j = lane & 7;
+  const bool act = u < nrows;
+  const size_t sb = row0 + (size_t)(act ? u : 0);
+  const int n = FULL ? K : n_in;  // this row's sample count
+  const int m8 = FULL ? K : n - (n & 7);
+  // the fct word and the timestamp of slots 8 e + j (the 12-B record is {fct, duration, ts})
+  const uint32_t* rec = reinterpret_cast<const uint32_t*>(st.res + sb * K + (size_t)j);
+  uint32_t key[16], th[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    key[e] = rec[24 * e];
+    th[e] = rec[24 * e + 2];
+    if constexpr (!FULL) th[e] = 8 * e + j < n ? th[e] : 0u;  // empty slots: stale words
+  }
+  uint32_t tmax = 0;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) tmax = th[e] > tmax ? th[e] : tmax;
+  uint32_t o = xor_lane_z<1>(tmax, lane);
+  tmax = o > tmax ? o : tmax;
+  o = xor_lane_z<2>(tmax, lane);
+  tmax = o > tmax ? o : tmax;
+  o = xor_lane_z<4>(tmax, lane);
+  tmax = o > tmax ? o : tmax;
+
+  // decay weights of the lane's 16 slots; f32 copies by slot in LDS for the gather after the sort
+  float w[16];
+  float* wf = reinterpret_cast<float*>(&sc.vals[0][0]) + u * K;  // [8][K] f32 (4 KiB)
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int slot = 8 * e + j;
+    w[e] = lb_exp2f((float)(tmax - th[e]) * p.decay_c);
+    if constexpr (!FULL) w[e] = slot < n ? w[e] : 0.0f;
+    if (act) wf[slot] = w[e];
+  }
+
+  // numpy-order sums, as observe_chunk_regs
+  float vf[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) vf[e] = sample_value<true>(key[e]);
+  auto in_acc = [&](int e) { return FULL || 8 * e + j < m8; };
+  float acc = vf[0];
+#pragma unroll
+  for (int e = 1; e < 16; ++e) acc += in_acc(e) ? vf[e] : 0.0f;
+  acc = acc + xor_f32_z<1>(acc, lane);
+  acc = acc + xor_f32_z<2>(acc, lane);
+  acc = acc + xor_f32_z<4>(acc, lane);
+  double svw = (double)vf[0] * (double)w[0], sw = (double)w[0];
+#pragma unroll
+  for (int e = 1; e < 16; ++e) {
+    const double wi = (double)w[e];
+    svw = in_acc(e) ? fma((double)vf[e], wi, svw) : svw;
+    sw += in_acc(e) ? wi : 0.0;
+  }
+  svw = svw + xor_f64_z<1>(svw, lane);
+  sw = sw + xor_f64_z<1>(sw, lane);
+  svw = svw + xor_f64_z<2>(svw, lane);
+  sw = sw + xor_f64_z<2>(sw, lane);
+  svw = svw + xor_f64_z<4>(svw, lane);
+  sw = sw + xor_f64_z<4>(sw, lane);
+  float* tail_v = reinterpret_cast<float*>(&sc.wts[0][0]) + u * 16;  // [8 rows][8] tail values
+  float* tail_w = reinterpret_cast<float*>(&sc.perm[0][0]) + u * 16;  // [8 rows][8] tail weights
+  int ntail = 0;
+  if constexpr (!FULL) {
+    ntail = n - m8;
+    const int et = m8 >> 3;
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+      if (e == et) {
+        tail_v[j] = vf[e];
+        tail_w[j] = w[e];
+      }
+    wave_sync();
+    for (int k = 0; k < ntail; ++k) {
+      const float tv = tail_v[k], tw = tail_w[k];
+      acc += tv;
+      svw = fma((double)tv, (double)tw, svw);
+      sw += (double)tw;
+    }
+  }
+  const float mean = acc / (float)n;
+  float ss;
+  {
+    float dv = vf[0] - mean;
+    ss = dv * dv;
+#pragma unroll
+    for (int e = 1; e < 16; ++e) {
+      dv = vf[e] - mean;
+      ss += in_acc(e) ? dv * dv : 0.0f;
+    }
+  }
+  ss = ss + xor_f32_z<1>(ss, lane);
+  ss = ss + xor_f32_z<2>(ss, lane);
+  ss = ss + xor_f32_z<4>(ss, lane);
+  if constexpr (!FULL) {
+    for (int k = 0; k < ntail; ++k) {
+      const float dv = tail_v[k] - mean;
+      ss += dv * dv;
+    }
+  }
+  const float sd = sqrtf(ss / (float)n);
+  const float md = (float)(svw / sw);
+
+  // order statistics: one key-only sort of (us << 7 | slot), empty slots last
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    key[e] = (key[e] << 7) | (uint32_t)(8 * e + j);
+    if constexpr (!FULL) key[e] = 8 * e + j < n ? key[e] : 0xFFFFFFFFu;
+  }
+  bitonic128_keys_g8(key, j);
+  wave_sync();  // wf complete
+  uint64_t incl[16];
+  uint64_t run = 0;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    run += fixed48(wf[key[e] & 127u]);
+    incl[e] = run;
+    key[e] >>= 7;
+  }
+  uint64_t excl = 0;
+#pragma unroll
+  for (int dd = 1; dd < 8; dd <<= 1) {
+    const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)(run + excl), (unsigned)dd, 8);
+    const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)((run + excl) >> 32), (unsigned)dd, 8);
+    if (j >= dd) excl += ((uint64_t)hi << 32) | lo;
+  }
+  const uint64_t tot_incl = run + excl;
+  const uint32_t tlo = (uint32_t)__shfl((int)(uint32_t)tot_incl, (lane & ~7) | 7, 64);
+  const uint32_t thi = (uint32_t)__shfl((int)(uint32_t)(tot_incl >> 32), (lane & ~7) | 7, 64);
+  const uint64_t thr = ((((uint64_t)thi << 32) | tlo) * 9u + 9u) / 10u;
+  const uint64_t thr_lane = thr > excl ? thr - excl : 0u;
+  uint32_t cand = 0xFFFFFFFFu;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const uint32_t c = incl[e] >= thr_lane ? key[e] : 0xFFFFFFFFu;
+    cand = c < cand ? c : cand;
+  }
+  const bool crosses = incl[15] >= thr_lane;
+  const uint64_t m = __ballot(crosses);
+  const uint32_t gm = (uint32_t)(m >> (lane & ~7)) & 0xFFu;
+  const int tstar = gm ? __builtin_ctz(gm) : 7;
+  cand = crosses ? cand : key[15];
+  const float p90d = sample_value<true>(shfl_u32(cand, (lane & ~7) | tstar));
+  float p90;
+  {
+    const float hidx = (float)(n - 1) * 0.9f;
+    const float fl = floorf(hidx);
+    const float gg = hidx - fl;
+    float va, vb;
+    if constexpr (FULL) {
+      va = sample_value<true>(key[kP90Lo & 15]);
+      vb = sample_value<true>(key[(kP90Lo & 15) + 1]);
+    } else {
+      wave_sync();  // every gather from wf done: reuse sc.vals for the sorted keys
+      uint32_t* srt = &sc.vals[u][0];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) srt[16 * j + e] = key[e];
+      wave_sync();
+      const int lo = (int)fl;
+      va = sample_value<true>(srt[lo]);
+      vb = sample_value<true>(srt[lo + 1 < n ? lo + 1 : lo]);
+    }
+    const float diff = vb - va;
+    p90 = (gg >= 0.5f) ? (vb - diff * (1.0f - gg)) : (va + diff * gg);
+    if constexpr (FULL) p90 = __uint_as_float(shfl_u32(__float_as_uint(p90), (lane & ~7) | 7));
+  }
+  // row u: lane j < 5 writes feature j to both column groups (fct 1-5, duration 6-10); lane 5
+  // writes n_flow_on
+  if (act) {
+    if (j < 5) {
+      const float v = j == 0 ? mean : j == 1 ? p90 : j == 2 ? sd : j == 3 ? md : p90d;
+      obs_out[u * NF + 1 + j] = v;
+      obs_out[u * NF + 6 + j] = v;
+      st.fcache[sb * 10 + (size_t)j] = v;
+      st.fcache[sb * 10 + (size_t)(5 + j)] = v;
+    } else if (j == 5) {
+      obs_out[u * NF] = (float)(st.hc[sb] >> 16);
+    }
+  }
+  wave_sync();
+}
+
+// Rows of envs [b0, b0 + nenv) (nenv * S <= 8) into obs_out (their (S, 11) rows back to back).
+// INC: unchanged rows take their cached features (fresh: some env was reset by this step); rows
+// the register path cannot take (n < 8, a sample >= kPackLimit) go through observe_chunk per env.
+template <bool INC>
+__device__ __forceinline__ void observe_rows_paired(const DevState& st, const SimParams& p,
+                                                    size_t b0, int nenv, ObsScratch& sc,
+                                                    float* obs_out, int lane, bool fresh) {
+  const int S = p.S, nrows = nenv * S;
+  const size_t row0 = b0 * (size_t)S;
+  const int u = lane >> 3;
+  const bool act = u < nrows;
+  const size_t usb = row0 + (size_t)(act ? u : 0);
+  const uint32_t rc = st.res_count[usb];
+  const uint32_t hcw = st.hc[usb];
+  if constexpr (INC) {
+    const uint32_t w = lane < 4 * nrows ? st.chg[(row0 + (size_t)(lane >> 2)) * 4 + (lane & 3)] : 0u;
+    if (!fresh && !__any(w != 0u)) {  // no reservoir of the rows changed: the cached features
+      for (int e = lane; e < nrows * NF; e += 64) {
+        const int s = e / NF, c = e - s * NF;
+        obs_out[e] = c == 0 ? (float)(st.hc[row0 + (size_t)s] >> 16)
+                            : st.fcache[(row0 + (size_t)s) * 10 + (size_t)(c - 1)];
+      }
+      wave_sync();
+      return;
+    }
+  }
+  const int n = rc < (uint32_t)K ? (int)rc : K;
+  if (!__any(act && (n < 8 || (hcw & kHcBig) != 0u))) {
+    if (!__any(act && n < K)) observe_rows_paired_regs<true>(st, p, row0, nrows, K, sc, obs_out, lane);
+    else observe_rows_paired_regs<false>(st, p, row0, nrows, n, sc, obs_out, lane);
+    return;
+  }
+  for (int e = 0; e < nenv; ++e) {
+    const bool fe = fresh && p.next_reset && st.ep_step[b0 + (size_t)e] < 0;
+    for (int s0 = 0; s0 < S; s0 += kObsChunk)
+      observe_chunk<true, INC>(st, p, b0 + (size_t)e, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk,
+                               sc, obs_out + e * S * NF, lane, fe);
+  }
+}
+
 // ================================================================ observe (one wave = one env)
 
 struct ObsOutputs {
@@ -2201,6 +2448,31 @@ __global__ void __launch_bounds__(64 * kObsWavesPerEnv<MAXS>, 5)
   }
   __syncthreads();
   observe_outputs<MAXS, MODE, FAC>(st, p, out, b, s_obs, s_act, tid, nthr);
+}
+
+// Step-mode observation when every record pairs dur == fct (observe_rows_paired): one wave per
+// 8 consecutive (env, server) rows, S in {1, 2, 4, 8}, then each of its 8 / S envs' reward,
+// episode words and outputs (observe_outputs, in env order).
+#ifndef LBSIM_OBS_PAIR_WAVES
+#define LBSIM_OBS_PAIR_WAVES 5
+#endif
+template <int MODE, bool FAC>
+__global__ void __launch_bounds__(64, LBSIM_OBS_PAIR_WAVES)
+    observe_pair_kernel(DevState st, SimParams p, ObsOutputs out) {
+  __shared__ ObsScratch sc;
+  __shared__ float s_obs[8 * NF];
+  __shared__ float s_act[8];
+  const int S = p.S, epw = 8 / S, lane = (int)threadIdx.x;
+  const size_t b0 = (size_t)blockIdx.x * (size_t)epw;
+  const int nenv = (size_t)p.B - b0 < (size_t)epw ? (int)((size_t)p.B - b0) : epw;
+  bool fresh = false;
+  if (MODE == kModeStep && p.next_reset)
+    for (int e = 0; e < nenv; ++e) fresh |= st.ep_step[b0 + (size_t)e] < 0;
+  observe_rows_paired<MODE == kModeStep>(st, p, b0, nenv, sc, s_obs, lane, fresh);
+  for (int e = 0; e < nenv; ++e) {
+    observe_outputs<8, MODE, FAC>(st, p, out, b0 + (size_t)e, s_obs + e * S * NF, s_act, lane, 64);
+    wave_sync();  // s_act reused by the next env
+  }
 }
 
 // Wide envs (S > 16: configs[4] read literally, 4 agents x 16 servers), in two launches instead of

@@ -1,5 +1,8 @@
 // lbsim_obs.hip — observe launchers: one wave per 4-server chunk, the chunks of an
 // env in one workgroup, each with its own ObsScratch in dynamic LDS.
+#include <cstdlib>
+#include <cstring>
+
 #include "lbsim_internal.h"
 
 namespace lbk {
@@ -56,11 +59,32 @@ void launch_observe_split(const LaunchCtx& L, const ObsOutputs& o, const uint8_t
     LBSIM_LAUNCH((observe_rows_kernel<64, MODE, FAC>), grid, block, 0, stream, L.st, L.prm, o, mask);
 }
 
+// The paired step observe (observe_pair_kernel): records whose duration word equals the fct word
+// by construction (duration_mode AGE, lost-FIN off) and S dividing 8.  LBSIM_OBSERVE_PAIRED=0
+// turns it off (A/B; the same bits either way).
+bool observe_paired(const LaunchCtx& L) {
+  static const bool on = [] {
+    const char* e = std::getenv("LBSIM_OBSERVE_PAIRED");
+    return !(e != nullptr && std::strcmp(e, "0") == 0);
+  }();
+  return on && L.prm.dur_service == 0 && L.prm.lf_thr == 0u &&
+         (L.S == 1 || L.S == 2 || L.S == 4 || L.S == 8);
+}
+
 // the problem-05 facade rows (agent_obs / state) come from their own instantiation
 template <int MODE>
 void launch_observe_m(const LaunchCtx& L, const ObsOutputs& o, const uint8_t* mask,
                       hipStream_t stream) {
   const bool fac = o.agent_obs != nullptr || o.state != nullptr;
+  if (MODE == kModeStep && observe_paired(L)) {  // 8 rows per wave: 8 / S envs
+    const int epw = 8 / L.S;
+    const dim3 grid((unsigned)((L.B + epw - 1) / epw)), block(64);
+    if (fac)
+      LBSIM_LAUNCH((observe_pair_kernel<MODE, true>), grid, block, 0, stream, L.st, L.prm, o);
+    else
+      LBSIM_LAUNCH((observe_pair_kernel<MODE, false>), grid, block, 0, stream, L.st, L.prm, o);
+    return;
+  }
   if (L.S > kObsChunk && L.S > observe_split_s()) {
     if (fac) launch_observe_split<MODE, true>(L, o, mask, stream);
     else launch_observe_split<MODE, false>(L, o, mask, stream);

@@ -72,12 +72,14 @@ def test_shard_arithmetic():
     assert lbdist.gather_over_ranks(1.5) == [1.5]
 
 
-def test_two_rank_oracle_shards_equal_single_process(tmp_path, oracle_mod):
-    res = run_ranks("oracle", 2, str(tmp_path / "r.npz"))
-    assert list(res["offsets"]) == [0, B]
-    assert float(res["slowest"]) == 2.0 and float(res["rate"]) == 2 * B * T / 2.0
-    assert list(res["per_rank"]) == [1.0, 2.0]  # gather_over_ranks: rank order
-    obs, rew = single_process_reference(oracle_mod, 2)
+@pytest.mark.parametrize("world", [2, 4])
+def test_rank_oracle_shards_equal_single_process(tmp_path, oracle_mod, world):
+    res = run_ranks("oracle", world, str(tmp_path / "r.npz"))
+    assert list(res["offsets"]) == [r * B for r in range(world)]
+    assert float(res["slowest"]) == float(world)
+    assert float(res["rate"]) == world * B * T / float(world)
+    assert list(res["per_rank"]) == [float(r + 1) for r in range(world)]  # rank order
+    obs, rew = single_process_reference(oracle_mod, world)
     np.testing.assert_array_equal(res["obs"], obs)
     np.testing.assert_array_equal(res["rew"], rew)
 
@@ -91,22 +93,26 @@ def test_two_rank_gpu_shards_equal_single_process_oracle(tmp_path, oracle_mod):
 
 
 @pytest.mark.gpu
-def test_bench_self_launches_ranks():
-    """`bench.py --gpus 2` without torchrun starts its own two rank processes (the driver's
-    multi-GPU contract); gloo for the measurement collectives so both ranks may share one card.
-    Rank 0 prints exactly one JSON line with n_gpus = 2 and the global batch of both shards."""
+@pytest.mark.parametrize("world,batch", [(2, 2048), (8, 512)])
+def test_bench_self_launches_ranks(world, batch):
+    """`bench.py --gpus N` without torchrun starts its own N rank processes (the driver's
+    multi-GPU contract, rehearsed up to the 8 ranks of one node); gloo for the measurement
+    collectives so every rank may share one card.  Rank 0 prints exactly one JSON line with
+    n_gpus = N and the global batch of all shards."""
     import json
     root = os.path.dirname(HERE)
     env = dict(os.environ, LBSIM_DIST_BACKEND="gloo")
-    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps",
-                        "3", "--warmup", "1", "--batch", "2048"], cwd=root, env=env,
-                       capture_output=True, text=True, timeout=240)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world),
+                        "--steps", "3", "--warmup", "1", "--batch", str(batch),
+                        "--no-cpu-baseline", "--no-graph", "--prewarm-ms", "0"], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 4096 and out["value"] > 0
+    assert out["n_gpus"] == world and out["config"]["global_batch"] == world * batch
+    assert out["value"] > 0
     ranks = out["ranks"]
-    assert ranks["world_size"] == 2 and len(ranks["elapsed_s"]) == 2
+    assert ranks["world_size"] == world and len(ranks["elapsed_s"]) == world
     assert ranks["elapsed_min_s"] <= ranks["elapsed_max_s"]
     assert abs(ranks["elapsed_max_s"] - out["ms_per_step"] * 3 / 1e3) < 1e-9

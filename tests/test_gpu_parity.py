@@ -356,7 +356,9 @@ def _expected_step_kernels(B, S, simds):
         occ = 2 if B <= 2 * simds else 4
         return {4: f"step_wave_kernel<{ng}, 0, false, {occ}, {4 if S <= 4 else 8}>"}
     g = 2 if S <= 2 else (8 if B * 4 // 64 <= simds // 2 else 4) if S <= 4 else 8 if S <= 8 else 16
-    return {0: f"dynamics_group_kernel<{g}, 0, 0, false", 1: "observe_kernel<"}
+    # paired records (duration = the flow's age, lost-FIN off) with S dividing 8: 8 rows per wave
+    obs = "observe_pair_kernel<0, " if S in (1, 2, 4, 8) else "observe_kernel<"
+    return {0: f"dynamics_group_kernel<{g}, 0, 0, false", 1: obs}
 
 
 def test_configs1_default_dispatch_4096x4(lib, oracle_mod):
@@ -466,23 +468,56 @@ def test_wave_kernel_bit_exact(step):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
 
 
-def test_sharding_invariance(lib):
-    """Global env ids key the RNG: two shards reproduce the monolithic run exactly."""
+@pytest.mark.parametrize("S,world,B", [(4, 2, 200), (8, 4, 1003), (8, 8, 8400), (16, 8, 777)])
+def test_sharding_invariance(lib, S, world, B):
+    """Global env ids key the RNG: `world` uneven shards (each its own handle with its
+    env_id_offset, as one rank per GPU runs them) reproduce the monolithic run exactly (SURVEY
+    §8e), whatever kernel each shard's size dispatches to (8400 x 8 whole: server-per-lane groups;
+    its ~1k-env shards: one wave per env) -- observations, rewards, done and assignment counts."""
     from marllb_amd.env import VecLoadBalanceEnv
-    B, S = 200, 4
+    rng = np.random.default_rng(S * 100 + world)
+    cuts = np.sort(rng.choice(np.arange(1, B), world - 1, replace=False))
+    bounds = [0, *cuts.tolist(), B]
     full = VecLoadBalanceEnv(B, S, device="cuda:0", seed=9, autoreset=False)
-    parts = [VecLoadBalanceEnv(n, S, device="cuda:0", seed=9, autoreset=False, env_id_offset=o)
-             for o, n in ((0, 120), (120, 80))]
+    parts = [VecLoadBalanceEnv(hi - lo, S, device="cuda:0", seed=9, autoreset=False,
+                               env_id_offset=lo) for lo, hi in zip(bounds[:-1], bounds[1:])]
     f = full.reset()
     p = torch.cat([e.reset() for e in parts])
     assert torch.equal(f, p)
-    rng = np.random.default_rng(5)
     for _ in range(5):
         a = torch.from_numpy(rng.integers(0, 3, (B, S)))
-        fo, fr, _, _ = full.step(a)
-        po = [e.step(a[o:o + e.num_envs]) for e, o in zip(parts, (0, 120))]
+        fo, fr, fd, fi = full.step(a, assign_counts=True)
+        po = [e.step(a[lo:hi], assign_counts=True) for e, lo, hi in zip(parts, bounds[:-1], bounds[1:])]
         assert torch.equal(fo, torch.cat([x[0] for x in po]))
         assert torch.equal(fr, torch.cat([x[1] for x in po]))
+        assert torch.equal(fd, torch.cat([x[2] for x in po]))
+        assert torch.equal(fi["assign_counts"], torch.cat([x[3]["assign_counts"] for x in po]))
+    for e in [full, *parts]:
+        e.close()
+
+
+def test_sharding_invariance_qmix_shape(lib):
+    """configs[4]'s env shape (4 agents x 4 servers, problem-05 facade) split over 8 uneven
+    shards equals one handle: agent observations, rewards, done and the global state."""
+    from marllb_amd.multi_agent import VecMultiAgentLoadBalanceEnv
+    B, world = 1000, 8
+    rng = np.random.default_rng(44)
+    bounds = [0, *np.sort(rng.choice(np.arange(1, B), world - 1, replace=False)).tolist(), B]
+    full = VecMultiAgentLoadBalanceEnv(B, 4, 4, device="cuda:0", seed=21, action_type="discrete")
+    parts = [VecMultiAgentLoadBalanceEnv(hi - lo, 4, 4, device="cuda:0", seed=21,
+                                         action_type="discrete", env_id_offset=lo)
+             for lo, hi in zip(bounds[:-1], bounds[1:])]
+    assert torch.equal(full.reset(), torch.cat([e.reset() for e in parts]))
+    for _ in range(4):
+        a = torch.from_numpy(rng.integers(0, 3, (B, 4)))
+        fo, fr, fd, _ = full.step(a)
+        po = [e.step(a[lo:hi]) for e, lo, hi in zip(parts, bounds[:-1], bounds[1:])]
+        assert torch.equal(fo, torch.cat([x[0] for x in po]))
+        assert torch.equal(fr, torch.cat([x[1] for x in po]))
+        assert torch.equal(fd, torch.cat([x[2] for x in po]))
+        assert torch.equal(full.get_state(), torch.cat([e.get_state() for e in parts]))
+    for e in [full, *parts]:
+        e.close()
 
 
 def test_full_size_properties(lib, oracle_mod):

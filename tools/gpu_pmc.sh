@@ -9,7 +9,10 @@ mkdir -p $O
 cd $R
 timeout -k 10 300 ./tools/ubench_valu > $O/ubench_valu.jsonl 2> $O/ubench_valu.err || exit 9
 cd /tmp && export TMPDIR=/tmp
-B="$R/bench.py --no-cpu-baseline --no-graph --prewarm-ms 0 --steps 20 --warmup 5 $@"
+# the driver's bench command (--steps 20 --warmup 5, pre-warm on) without the graph leg and the CPU
+# baseline, which run after the timed region; tools/pmc_traffic.py / pmc_valu.py --steps 20
+# --warmup 5 keep the timed launches (and their exact accounting replay) only
+B="$R/bench.py --no-cpu-baseline --no-graph --steps 20 --warmup 5 $@"
 P="timeout -s KILL 240 rocprofv3"
 $P --pmc FETCH_SIZE -d $O/fetch -o run --output-format csv -- python3 $B > $O/fetch.log 2>&1 &&
 $P --pmc WRITE_SIZE -d $O/write -o run --output-format csv -- python3 $B > $O/write.log 2>&1 &&

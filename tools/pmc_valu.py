@@ -20,14 +20,12 @@ the VALU issue micro-benchmark (ubench_valu.jsonl: SIMD cycles per instruction o
     python tools/pmc_valu.py gpurun_out/<tag> --batch 65536 --servers 4 [--out profiles/pmc_valu.json]
 """
 import argparse
-import collections
-import csv
 import json
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from pmc_traffic import is_step_kernel, kernel_key  # noqa: E402
+from pmc_traffic import bench_workload, is_step_kernel, load  # noqa: E402
 
 CLOCK_HZ = 2.4e9  # MI355X peak engine clock (MI355X_MICROARCH.md)
 SIMDS = 1024      # 256 CUs x 4
@@ -42,16 +40,6 @@ PRICE = {"SQ_INSTS_VALU_INT32": "v_add_u32", "SQ_INSTS_VALU_ADD_F32": "v_fma_f32
          "other": "v_add_u32"}
 # ops of the micro-benchmark that issue two VALU instructions per counted step
 PAIRS = {"v_mad_u64_u32+xor", "v_mov_dpp+add", "v_cvt_f64_f32+v_cvt_f32_f64", "v_lshlrev_b64+pack"}
-
-
-def load(d, sub):
-    agg = collections.defaultdict(list)
-    path = os.path.join(d, sub, "run_counter_collection.csv")
-    if not os.path.exists(path):
-        return agg
-    for r in csv.DictReader(open(path)):
-        agg[(kernel_key(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
-    return agg
 
 
 def mean(v):
@@ -76,15 +64,19 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--servers", type=int, default=4)
     ap.add_argument("--waves", type=int, default=4, help="ubench occupancy used for the prices")
+    ap.add_argument("--steps", type=int, default=20, help="bench --steps of the passes (K)")
+    ap.add_argument("--warmup", type=int, default=5, help="bench --warmup of the passes (W)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     cost = ubench_costs(a.dir, a.waves)
     cost["v_cvt"] = cost.get("v_cvt_f64_f32+v_cvt_f32_f64")
     agg = {}
     for sub in ("sq1", "sq2", "vc1", "vc2"):
-        agg.update(load(a.dir, sub))
+        agg.update(load(a.dir, sub, a.steps, a.warmup))
     kernels = sorted({k for k, _ in agg if is_step_kernel(k)})
-    out = {"batch": a.batch, "servers": a.servers, "clock_hz": CLOCK_HZ, "simds": SIMDS,
+    out = {"batch": a.batch, "servers": a.servers,
+           "workload": bench_workload(a.dir, "sq1", a.steps, a.warmup),
+           "clock_hz": CLOCK_HZ, "simds": SIMDS,
            "ubench_waves_per_simd": a.waves, "ubench_simd_cyc_per_inst": cost, "kernels": {}}
     for k in kernels:  # keyed by the full template signature (lbsim_launch_names)
         c = {cn: mean(v) for (kn, cn), v in agg.items() if kn == k}
