@@ -1684,7 +1684,11 @@ __device__ __forceinline__ bool observe_chunk_full(const DevState& st, const Sim
 // every computed chunk refreshes the cache (US: reset and step modes).
 // fresh: the env was reset by this step (next-step auto-reset): every chunk is recomputed (the
 // cached features are the previous episode's).
-template <bool US, bool INC>
+// REGS = false: the general path only -- observe_rows_paired's fallback for rows the register
+// path cannot take (one copy of the code instead of two more register-path instantiations: fewer
+// SGPR / VGPR spills in observe_pair_kernel, 131 -> 125 us at 65536 x 4, 241 -> 229 us at
+// 65536 x 8, profiles/r05f/; LBSIM_OBS_PAIR_FALLBACK_REGS=1 restores the full observe_chunk).
+template <bool US, bool INC, bool REGS = true>
 __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParams& p, size_t b,
                                               int s_base, int S, ObsScratch& sc, float* obs_out,
                                               int lane, bool fresh = false) {
@@ -1711,7 +1715,7 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
       return;
     }
   }
-  if constexpr (US) {
+  if constexpr (US && REGS) {
     if (observe_chunk_full<INC>(st, p, b, s_base, S, sc, obs_out, lane, rc, hcw)) return;
   }
   // ---- phase 1: reservoirs into LDS, decay weights relative to each server's newest sample.
@@ -2269,6 +2273,9 @@ __device__ __forceinline__ void observe_rows_paired_regs(const DevState& st, con
 // Rows of envs [b0, b0 + nenv) (nenv * S <= 8) into obs_out (their (S, 11) rows back to back).
 // INC: unchanged rows take their cached features (fresh: some env was reset by this step); rows
 // the register path cannot take (n < 8, a sample >= kPackLimit) go through observe_chunk per env.
+#ifndef LBSIM_OBS_PAIR_FALLBACK_REGS
+#define LBSIM_OBS_PAIR_FALLBACK_REGS 0
+#endif
 template <bool INC>
 __device__ __forceinline__ void observe_rows_paired(const DevState& st, const SimParams& p,
                                                     size_t b0, int nenv, ObsScratch& sc,
@@ -2301,8 +2308,9 @@ __device__ __forceinline__ void observe_rows_paired(const DevState& st, const Si
   for (int e = 0; e < nenv; ++e) {
     const bool fe = fresh && p.next_reset && st.ep_step[b0 + (size_t)e] < 0;
     for (int s0 = 0; s0 < S; s0 += kObsChunk)
-      observe_chunk<true, INC>(st, p, b0 + (size_t)e, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk,
-                               sc, obs_out + e * S * NF, lane, fe);
+      observe_chunk<true, INC, LBSIM_OBS_PAIR_FALLBACK_REGS != 0>(
+          st, p, b0 + (size_t)e, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk, sc,
+          obs_out + e * S * NF, lane, fe);
   }
 }
 
@@ -2453,8 +2461,10 @@ __global__ void __launch_bounds__(64 * kObsWavesPerEnv<MAXS>, 5)
 // Step-mode observation when every record pairs dur == fct (observe_rows_paired): one wave per
 // 8 consecutive (env, server) rows, S in {1, 2, 4, 8}, then each of its 8 / S envs' reward,
 // episode words and outputs (observe_outputs, in env order).
+// 4 waves per SIMD (128 VGPRs): with 5 (96 VGPRs) the register path spilled and the kernel ran
+// 140 us against 130 us at 65536 x 4, 255 against 236 us at 65536 x 8 (profiles/r05d/).
 #ifndef LBSIM_OBS_PAIR_WAVES
-#define LBSIM_OBS_PAIR_WAVES 5
+#define LBSIM_OBS_PAIR_WAVES 4
 #endif
 template <int MODE, bool FAC>
 __global__ void __launch_bounds__(64, LBSIM_OBS_PAIR_WAVES)
