@@ -2069,9 +2069,10 @@ __device__ double reward_of(const float* obs, int S, int metric, int field) {
 // DESIGN.md §3.4) and lost-FIN off, every record the dynamics write holds dur == fct, so a
 // server's duration reservoir equals its fct reservoir slot for slot (same values, timestamps and
 // count) and its 5 duration features equal its 5 fct features bit for bit.  observe_pair_kernel
-// then computes each server's features once: one wave takes 8 consecutive (env, server) rows --
-// 8 / S envs, S in {1, 2, 4, 8} -- and lane (u, j) holds slots 8 e + j of row u (the fct word
-// and the timestamp of each record), so a wave does the work observe_kernel spreads over two.
+// then computes each server's features once: one wave takes up to 8 consecutive (env, server)
+// rows -- the 8 / S whole envs of S <= 8 servers -- and lane (u, j) holds slots 8 e + j of row u
+// (the fct word and the timestamp of each record), so a wave does the work observe_kernel
+// spreads over two.  step_wave_kernel's S = 5-8 observe phase takes the same path for its env.
 // Same operations in the same order as observe_chunk_regs' fct group: the same bits.
 
 // (uint64_t)(w * 2^48) for w in [0, 1], from the f32 weight: hi = floor(x / 2^32), lo = the
@@ -2459,7 +2460,7 @@ __global__ void __launch_bounds__(64 * kObsWavesPerEnv<MAXS>, 5)
 }
 
 // Step-mode observation when every record pairs dur == fct (observe_rows_paired): one wave per
-// 8 consecutive (env, server) rows, S in {1, 2, 4, 8}, then each of its 8 / S envs' reward,
+// 8 / S whole envs (S <= 8: their 8 / S * S <= 8 consecutive rows), then each env's reward,
 // episode words and outputs (observe_outputs, in env order).
 // 4 waves per SIMD (128 VGPRs): with 5 (96 VGPRs) the register path spilled and the kernel ran
 // 140 us against 130 us at 65536 x 4, 255 against 236 us at 65536 x 8 (profiles/r05d/).
@@ -2521,6 +2522,9 @@ __global__ void __launch_bounds__(64)
 
 // observe_kernel's work for env b by ONE wave, its chunks in sequence (fused_step_kernel's second
 // phase).  Same routines, same order: the same bits.
+#ifndef LBSIM_STEP_WAVE_PAIRED
+#define LBSIM_STEP_WAVE_PAIRED 1
+#endif
 template <int MAXS>
 __device__ __forceinline__ void observe_env_wave(const DevState& st, const SimParams& p,
                                                  const ObsOutputs& out, size_t b, ObsScratch& sc,
@@ -2529,6 +2533,9 @@ __device__ __forceinline__ void observe_env_wave(const DevState& st, const SimPa
   const bool fresh = p.next_reset && st.ep_step[b] < 0;
   if constexpr (MAXS <= kObsChunk) {  // one chunk: straight-line code, no loop-carried s0
     observe_chunk<true, true>(st, p, b, 0, S, sc, s_obs, lane, fresh);
+  } else if (LBSIM_STEP_WAVE_PAIRED && MAXS <= 8 && p.dur_service == 0 && p.lf_thr == 0u) {
+    // paired records: the env's S <= 8 rows in one pass (observe_rows_paired)
+    observe_rows_paired<true>(st, p, b, 1, sc, s_obs, lane, fresh);
   } else {
     // rolled, with b and lane opaque per chunk: nothing derived from them is hoisted and held
     // across both chunks (step_wave_kernel<4, ..., 8>: 124 VGPRs instead of 184 B of spills/lane)

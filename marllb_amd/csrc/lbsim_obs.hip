@@ -60,7 +60,7 @@ void launch_observe_split(const LaunchCtx& L, const ObsOutputs& o, const uint8_t
 }
 
 // The paired step observe (observe_pair_kernel): records whose duration word equals the fct word
-// by construction (duration_mode AGE, lost-FIN off) and S dividing 8.  LBSIM_OBSERVE_PAIRED=0
+// by construction (duration_mode AGE, lost-FIN off) and S <= 8 (8 / S whole envs per wave).  LBSIM_OBSERVE_PAIRED=0
 // turns it off (A/B; the same bits either way).
 bool observe_paired(const LaunchCtx& L) {
   static const bool on = [] {
@@ -68,7 +68,7 @@ bool observe_paired(const LaunchCtx& L) {
     return !(e != nullptr && std::strcmp(e, "0") == 0);
   }();
   return on && L.prm.dur_service == 0 && L.prm.lf_thr == 0u &&
-         (L.S == 1 || L.S == 2 || L.S == 4 || L.S == 8);
+         L.S <= 8;
 }
 
 // the problem-05 facade rows (agent_obs / state) come from their own instantiation

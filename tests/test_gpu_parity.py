@@ -356,8 +356,8 @@ def _expected_step_kernels(B, S, simds):
         occ = 2 if B <= 2 * simds else 4
         return {4: f"step_wave_kernel<{ng}, 0, false, {occ}, {4 if S <= 4 else 8}>"}
     g = 2 if S <= 2 else (8 if B * 4 // 64 <= simds // 2 else 4) if S <= 4 else 8 if S <= 8 else 16
-    # paired records (duration = the flow's age, lost-FIN off) with S dividing 8: 8 rows per wave
-    obs = "observe_pair_kernel<0, " if S in (1, 2, 4, 8) else "observe_kernel<"
+    # paired records (duration = the flow's age, lost-FIN off), S <= 8: 8 // S envs per wave
+    obs = "observe_pair_kernel<0, " if S <= 8 else "observe_kernel<"
     return {0: f"dynamics_group_kernel<{g}, 0, 0, false", 1: obs}
 
 
