@@ -193,6 +193,10 @@ def parse():
                          "shape for at least this long (GPU clocks and caches ramp up); the "
                          "measured env's trajectory, warm-up and timed steps are unchanged.  "
                          "Reported as prewarm_ms; 0 disables")
+    ap.add_argument("--autoreset-mode", choices=["same_step", "next_step"], default="same_step",
+                    help="rollout workload: the env's auto-reset mode (same_step: SB3 / gym; "
+                         "next_step: gymnasium >= 1.0's NEXT_STEP, the reset inside the step "
+                         "launches -- the mode the graph leg always captures)")
     ap.add_argument("--late-episode", default="",
                     help="rollout workload at N=1: after the headline measurement, keep stepping the "
                          "same envs and also time --steps steps from these episode steps (comma "
@@ -359,6 +363,7 @@ def graph_leg(args, dev, shard, B, S, common, kernel_ms):
     import torch
     from marllb_amd.env import VecLoadBalanceEnv
     common = dict(common, graph_mode=True)
+    common.pop("autoreset_mode", None)
     autoreset = "same_step"
     k = max(1, args.graph_steps)  # steps per captured graph (one replay = k steps)
     if args.workload == "rollout":
@@ -543,6 +548,8 @@ def main():
         tr = trace.builtin(args.trace)
     common = dict(device=dev, seed=args.seed, env_id_offset=shard.env_id_offset, autoreset=True,
                   assign_policy=args.policy, trace=tr, dyn_mapping=args.dyn_mapping)
+    if args.workload == "rollout":
+        common["autoreset_mode"] = args.autoreset_mode
     prewarm = prewarm_scratch(args, dev, B, S, common)
     torch.manual_seed(args.seed)  # network init (random weights of the reference architecture)
     if args.workload == "rollout":
@@ -614,6 +621,18 @@ def main():
     cdev = dev if backend == "nccl" else None
     elapsed = lbdist.max_over_ranks(t1 - t0, cdev)
     per_rank = lbdist.gather_over_ranks(t1 - t0, cdev)
+    # the graph leg right after the timed region (before the accounting replay and everything
+    # else), so both legs run on the GPU in the same state: sustained load lowers the kernels'
+    # speed over the following seconds (profiles/r05k/)
+    graph_res = None
+    if world == 1 and not args.no_graph:
+        kms = sum(ms[i] / cnt[i] for i in (0, 1, 4) if cnt[i] > 0)
+        if pol_events:
+            kms += sum(a.elapsed_time(b) for a, b in pol_events) / len(pol_events)
+        try:
+            graph_res = graph_leg(args, dev, shard, B, S, common, kms)
+        except Exception as e:  # reported, never fatal to the headline line
+            graph_res = {"error": f"{type(e).__name__}: {e}"}
 
     if rank == 0:
         value = lbdist.throughput(shard, args.steps, elapsed)
@@ -686,6 +705,8 @@ def main():
                        "assign_policy": args.policy,
                        "envs_per_gpu": B, "servers": S, "global_batch": world * B,
                        "step_interval_s": 0.25, "autoreset": True,
+                       "autoreset_mode": args.autoreset_mode if args.workload == "rollout"
+                       else "same_step",
                        "parallelism": f"env-shard x{world}", "dyn_mapping": args.dyn_mapping},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
@@ -732,14 +753,8 @@ def main():
                     "frac": tf / MFMA_F32_PEAK_TFLOPS}
                 # host + torch work between the launches (<= 10 us)
                 out["policy_glue_ms_per_step"] = out["policy_ms_per_step"] - pms
-        if world == 1 and not args.no_graph:
-            kms = sum(avg.values()) + (out["roofline"]["kernels"].get(
-                {"sac-gru": "sac_actor_kernel", "qmix": "qmix_policy_kernel"}.get(
-                    args.workload, ""), {}).get("avg_launch_ms", 0.0))
-            try:
-                out["graph"] = graph_leg(args, dev, shard, B, S, common, kms)
-            except Exception as e:  # reported, never fatal to the headline line
-                out["graph"] = {"error": f"{type(e).__name__}: {e}"}
+        if graph_res is not None:
+            out["graph"] = graph_res
         if world == 1 and args.workload == "rollout" and args.late_episode:
             out["late_episode"] = late_episode(args, env, handle, lib, one_step, rate, B, S,
                                                args.warmup + args.steps)

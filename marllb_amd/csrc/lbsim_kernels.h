@@ -2272,7 +2272,8 @@ __device__ __forceinline__ void observe_rows_paired_regs(const DevState& st, con
 }
 
 // Rows of envs [b0, b0 + nenv) (nenv * S <= 8) into obs_out (their (S, 11) rows back to back).
-// INC: unchanged rows take their cached features (fresh: some env was reset by this step); rows
+// INC: unchanged rows take their cached features unless some env was reset by this step (nr:
+// next-step auto-reset is on; its ep_step words are loaded with the decision words); rows
 // the register path cannot take (n < 8, a sample >= kPackLimit) go through observe_chunk per env.
 #ifndef LBSIM_OBS_PAIR_FALLBACK_REGS
 #define LBSIM_OBS_PAIR_FALLBACK_REGS 0
@@ -2280,7 +2281,7 @@ __device__ __forceinline__ void observe_rows_paired_regs(const DevState& st, con
 template <bool INC>
 __device__ __forceinline__ void observe_rows_paired(const DevState& st, const SimParams& p,
                                                     size_t b0, int nenv, ObsScratch& sc,
-                                                    float* obs_out, int lane, bool fresh) {
+                                                    float* obs_out, int lane, bool nr) {
   const int S = p.S, nrows = nenv * S;
   const size_t row0 = b0 * (size_t)S;
   const int u = lane >> 3;
@@ -2290,6 +2291,8 @@ __device__ __forceinline__ void observe_rows_paired(const DevState& st, const Si
   const uint32_t hcw = st.hc[usb];
   if constexpr (INC) {
     const uint32_t w = lane < 4 * nrows ? st.chg[(row0 + (size_t)(lane >> 2)) * 4 + (lane & 3)] : 0u;
+    // one round trip for the decision words and the reset flags: every load is issued first
+    const bool fresh = nr && __any(lane < nenv && st.ep_step[b0 + (size_t)lane] < 0);
     if (!fresh && !__any(w != 0u)) {  // no reservoir of the rows changed: the cached features
       for (int e = lane; e < nrows * NF; e += 64) {
         const int s = e / NF, c = e - s * NF;
@@ -2307,7 +2310,7 @@ __device__ __forceinline__ void observe_rows_paired(const DevState& st, const Si
     return;
   }
   for (int e = 0; e < nenv; ++e) {
-    const bool fe = fresh && p.next_reset && st.ep_step[b0 + (size_t)e] < 0;
+    const bool fe = nr && st.ep_step[b0 + (size_t)e] < 0;
     for (int s0 = 0; s0 < S; s0 += kObsChunk)
       observe_chunk<true, INC, LBSIM_OBS_PAIR_FALLBACK_REGS != 0>(
           st, p, b0 + (size_t)e, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk, sc,
@@ -2476,10 +2479,8 @@ __global__ void __launch_bounds__(64, LBSIM_OBS_PAIR_WAVES)
   const int S = p.S, epw = 8 / S, lane = (int)threadIdx.x;
   const size_t b0 = (size_t)blockIdx.x * (size_t)epw;
   const int nenv = (size_t)p.B - b0 < (size_t)epw ? (int)((size_t)p.B - b0) : epw;
-  bool fresh = false;
-  if (MODE == kModeStep && p.next_reset)
-    for (int e = 0; e < nenv; ++e) fresh |= st.ep_step[b0 + (size_t)e] < 0;
-  observe_rows_paired<MODE == kModeStep>(st, p, b0, nenv, sc, s_obs, lane, fresh);
+  observe_rows_paired<MODE == kModeStep>(st, p, b0, nenv, sc, s_obs, lane,
+                                         MODE == kModeStep && p.next_reset != 0);
   for (int e = 0; e < nenv; ++e) {
     observe_outputs<8, MODE, FAC>(st, p, out, b0 + (size_t)e, s_obs + e * S * NF, s_act, lane, 64);
     wave_sync();  // s_act reused by the next env
@@ -2535,7 +2536,7 @@ __device__ __forceinline__ void observe_env_wave(const DevState& st, const SimPa
     observe_chunk<true, true>(st, p, b, 0, S, sc, s_obs, lane, fresh);
   } else if (LBSIM_STEP_WAVE_PAIRED && MAXS <= 8 && p.dur_service == 0 && p.lf_thr == 0u) {
     // paired records: the env's S <= 8 rows in one pass (observe_rows_paired)
-    observe_rows_paired<true>(st, p, b, 1, sc, s_obs, lane, fresh);
+    observe_rows_paired<true>(st, p, b, 1, sc, s_obs, lane, p.next_reset != 0);
   } else {
     // rolled, with b and lane opaque per chunk: nothing derived from them is hoisted and held
     // across both chunks (step_wave_kernel<4, ..., 8>: 124 VGPRs instead of 184 B of spills/lane)
