@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
-"""Does a captured step run slower than the eager one because of the launches, or because the
-GPU runs the kernels back to back?  The random-policy rollout (65536 x 4, next-step auto-reset)
-captured K steps per torch.cuda.CUDAGraph; each replay timed with HIP events (a) back to back,
-(b) with the GPU idle for --idle-ms between replays, and (c) the same K steps eager with events
-around them, both ways.  JSON line per mode: ms per step of the replays / eager groups.
+"""Captured vs eager steps of the random-policy rollout on the same GPU state.
 
-    python tools/graph_gap_exp.py [--batch 65536] [--k 5] [--reps 40] [--idle-ms 2]
+Fresh envs (65536 x 4, same seed) are stepped, in the order given by --order, through W warm-up
+steps and then K timed steps (groups of --k steps; a group is one graph replay in graph mode),
+each group bracketed by HIP events, plus the wall time over the timed steps.  Repeating the
+sequence (--rounds) shows whether a mode is slower by itself or by its place in the run (GPU
+state after sustained load).  One JSON line per (round, mode).
+
+    python tools/graph_gap_exp.py [--order eager_same,eager_next,graph_next] [--rounds 2]
 """
 import argparse
 import json
@@ -16,67 +18,69 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main():
+def run(mode, B, S, k, warmup, steps, seed):
     import torch
     from marllb_amd.env import VecLoadBalanceEnv
+    dev = torch.device("cuda", 0)
+    graph = mode.startswith("graph")
+    ar = "next_step" if mode.endswith("next") else "same_step"
+    env = VecLoadBalanceEnv(B, S, device=dev, seed=seed, max_steps=10000, autoreset=True,
+                            autoreset_mode=ar, graph_mode=graph)
+    env.reset()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed + 1)
+    if graph:
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                env.step(torch.randint(0, 3, (B, S), device=dev, dtype=torch.int64))
+        torch.cuda.current_stream(dev).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(k):
+                env.step(torch.randint(0, 3, (B, S), device=dev, dtype=torch.int64))
+        group = g.replay
+    else:
+        def group():
+            for _ in range(k):
+                env.step(torch.randint(0, 3, (B, S), device=dev, dtype=torch.int64,
+                                       generator=gen))
+    for _ in range(max(1, warmup // k)):
+        group()
+    torch.cuda.synchronize()
+    n = max(1, steps // k)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(n)]
+    t0 = time.perf_counter()
+    for e0, e1 in ev:
+        e0.record()
+        group()
+        e1.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ms = sorted(e0.elapsed_time(e1) / k for e0, e1 in ev)
+    env.close()
+    torch.cuda.synchronize()
+    return {"mode": mode, "median_ms_per_step": ms[len(ms) // 2], "min_ms_per_step": ms[0],
+            "wall_ms_per_step": wall / (n * k) * 1e3}
+
+
+def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--servers", type=int, default=4)
     ap.add_argument("--k", type=int, default=5)
-    ap.add_argument("--reps", type=int, default=40)
-    ap.add_argument("--idle-ms", type=float, default=2.0)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--order", default="eager_same,eager_next,graph_next")
     a = ap.parse_args()
-    dev = torch.device("cuda", 0)
-    B, S, k = a.batch, a.servers, a.k
-    out = {}
-    for mode in ("graph", "eager"):
-        env = VecLoadBalanceEnv(B, S, device=dev, seed=7, max_steps=10000, autoreset=True,
-                                autoreset_mode="next_step", graph_mode=(mode == "graph"))
-        env.reset()
-        gen = torch.Generator(device=dev)
-        gen.manual_seed(11)
-
-        def step():
-            env.step(torch.randint(0, 3, (B, S), device=dev, dtype=torch.int64, generator=gen))
-        if mode == "graph":
-            side = torch.cuda.Stream(dev)
-            side.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.stream(side):
-                for _ in range(2):
-                    env.step(torch.randint(0, 3, (B, S), device=dev, dtype=torch.int64))
-            torch.cuda.current_stream(dev).wait_stream(side)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for _ in range(k):
-                    env.step(torch.randint(0, 3, (B, S), device=dev, dtype=torch.int64))
-            group = g.replay
-        else:
-            def group():
-                for _ in range(k):
-                    step()
-        for _ in range(4):
-            group()
-        torch.cuda.synchronize()
-        for idle in (0.0, a.idle_ms):
-            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                  for _ in range(a.reps)]
-            t0 = time.perf_counter()
-            for e0, e1 in ev:
-                e0.record()
-                group()
-                e1.record()
-                if idle > 0:
-                    torch.cuda.synchronize()
-                    time.sleep(idle * 1e-3)
-            torch.cuda.synchronize()
-            wall = time.perf_counter() - t0
-            ms = sorted(e0.elapsed_time(e1) / k for e0, e1 in ev)
-            out[f"{mode}_idle{idle:g}ms"] = {"median_ms_per_step": ms[len(ms) // 2],
-                                            "min_ms_per_step": ms[0],
-                                            "wall_ms_per_step": wall / (a.reps * k) * 1e3}
-        env.close()
-    print(json.dumps({"batch": B, "servers": S, "steps_per_group": k, "reps": a.reps,
-                      "idle_ms": a.idle_ms, "modes": out}))
+    for r in range(a.rounds):
+        for mode in a.order.split(","):
+            res = run(mode, a.batch, a.servers, a.k, a.warmup, a.steps, 20260109)
+            print(json.dumps({"round": r, "batch": a.batch, "servers": a.servers, **res}),
+                  flush=True)
 
 
 if __name__ == "__main__":
