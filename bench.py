@@ -390,6 +390,11 @@ def graph_leg(args, dev, shard, B, S, common, kernel_ms):
         env = VecMultiAgentLoadBalanceEnv(B, 4, S // 4, action_type="discrete", max_steps=100,
                                           **common)
         g = QMIXRollout(env, seed=args.seed + shard.rank).capture(steps=k)
+    # the kernels the captured step launches (next-step handles: the kModeStepNR dynamics), so
+    # gap_ms_per_step is read against the right eager kernels
+    from marllb_amd import _lib
+    h = env.handle if hasattr(env, "handle") else getattr(getattr(env, "vec", None), "handle", None)
+    ran = _lib.launch_names(h, 0) if h is not None else {}
     reps = max(1, -(-args.steps // k))  # replays covering at least --steps steps
     for _ in range(max(1, -(-args.warmup // k))):
         g.replay()
@@ -405,7 +410,10 @@ def graph_leg(args, dev, shard, B, S, common, kernel_ms):
     return {"value": B * n / el, "unit": "env-steps/s", "ms_per_step": ms, "steps": n,
             "kernels_ms_per_step": kernel_ms, "gap_ms_per_step": ms - kernel_ms,
             "form": f"{k} steps captured in one torch.cuda.CUDAGraph, replayed",
-            "steps_per_graph": k, "autoreset": autoreset}
+            "steps_per_graph": k, "autoreset": autoreset, "kernels": ran,
+            "note": "kernels_ms_per_step are the eager leg's HIP-event averages; the graph leg "
+                    "runs the kernels in `kernels` (compare with the eager line's signatures when "
+                    "the auto-reset modes differ)"}
 
 
 def late_episode(args, env, handle, lib, one_step, rate, B, S, done_steps):

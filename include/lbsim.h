@@ -87,6 +87,14 @@ enum lbsim_arrival_source { LBSIM_ARRIVAL_POISSON = 0, LBSIM_ARRIVAL_TRACE = 1 }
  * does not see the policy). */
 enum lbsim_duration_mode { LBSIM_DURATION_AGE = 0, LBSIM_DURATION_SERVICE = 1 };
 
+/* Observation column 0 (n_flow_on).  QUEUE (default): the flows in flight at the server.  VPP:
+ * the data plane's as_stat_t n_flow_on, +1 at a flow's first ACK and -1 at its RSTACK
+ * (src/vpp/lb/lbhash.h:116-120,138-142,167): a lost-FIN flow is never decremented (the decrement
+ * is commented out, lbhash.h:193,214), so the column is the flows in flight plus the server's
+ * lost-FIN flows completed since the episode start (or its last failure).  Only differs from
+ * QUEUE with lost_fin_prob > 0. */
+enum lbsim_n_flow_on_mode { LBSIM_NFLOW_QUEUE = 0, LBSIM_NFLOW_VPP = 1 };
+
 /* Dynamics-kernel mapping; every choice produces the same bits.  AUTO = SERVER_PER_LANE (faster
  * than one lane per env at every measured shape). */
 enum lbsim_dyn_mapping {
@@ -170,6 +178,7 @@ typedef struct lbsim_config {
    * (dynamics, observe), not the one-launch forms.  0 = off (the caller resets).             */
   int32_t next_step_reset;
   int32_t duration_mode;     /* lbsim_duration_mode, default AGE            */
+  int32_t n_flow_on_mode;    /* lbsim_n_flow_on_mode, default QUEUE         */
 } lbsim_config_t;
 
 typedef struct lbsim lbsim_t; /* opaque handle */

@@ -30,6 +30,7 @@ DTYPE_I32, DTYPE_I64, DTYPE_F32 = 0, 1, 2
 METRICS = ["jain", "variance", "std", "cv", "max", "min", "product", "range", "gini"]
 POLICIES = ["sed", "sed2", "lsq", "lsq2", "alias"]
 DURATION_MODES = ("age", "service")  # lbsim_duration_mode
+N_FLOW_ON_MODES = ("queue", "vpp")  # lbsim_n_flow_on_mode
 
 
 class LbsimConfig(ctypes.Structure):
@@ -66,6 +67,7 @@ class LbsimConfig(ctypes.Structure):
         ("recover_prob", ctypes.c_float),
         ("next_step_reset", ctypes.c_int32),
         ("duration_mode", ctypes.c_int32),
+        ("n_flow_on_mode", ctypes.c_int32),
     ]
 
 

@@ -182,6 +182,8 @@ int validate(const lbsim_config_t* c, char* msg, size_t n) {
   if (c->next_step_reset != 0 && c->next_step_reset != 1) return bad("next_step_reset must be 0 or 1");
   if (c->duration_mode != LBSIM_DURATION_AGE && c->duration_mode != LBSIM_DURATION_SERVICE)
     return bad("unknown duration_mode %d", c->duration_mode);
+  if (c->n_flow_on_mode != LBSIM_NFLOW_QUEUE && c->n_flow_on_mode != LBSIM_NFLOW_VPP)
+    return bad("unknown n_flow_on_mode %d", c->n_flow_on_mode);
   if (!(c->recover_prob >= 0.0f) || !(c->recover_prob <= 1.0f))
     return bad("recover_prob must be in [0, 1]");
   if (c->dyn_mapping == LBSIM_DYN_ENV_PER_LANE && c->num_servers > 16)
@@ -226,6 +228,7 @@ void derive_params(const lbsim_config_t& c, SimParams& p) {
   p.big_in_step = (p.dt_us >= (int32_t)kPackLimit || p.lf_thr != 0u) ? 1 : 0;
   p.next_reset = c.next_step_reset ? 1 : 0;
   p.dur_service = c.duration_mode == LBSIM_DURATION_SERVICE ? 1 : 0;
+  p.leak = (c.n_flow_on_mode == LBSIM_NFLOW_VPP && p.lf_thr != 0u) ? 1 : 0;
 }
 
 // State sections in snapshot order.
@@ -250,6 +253,7 @@ std::vector<Section> sections(lbsim_t* h) {
     v.push_back({(void**)&s.norm_std, BS * NF * 8});
   }
   if (h->cfg.fail_prob > 0.0f) v.push_back({(void**)&s.down, BS * 4});
+  if (h->prm.leak) v.push_back({(void**)&s.lost_on, BS * 4});
   return v;
 }
 

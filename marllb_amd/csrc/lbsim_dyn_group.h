@@ -164,7 +164,7 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
                                                  LaneState<1>& E, SrvLane& V, int s, int gbase,
                                                  int n_alias, const GroupConst& gc, int2* win,
                                                  int32_t* atab, int4* acache, uint3* const my_res,
-                                                 int2* const my_ring) {
+                                                 int2* const my_ring, uint32_t* const my_lost) {
   constexpr int WL = kGroupWL;
   constexpr bool two_choice = (POLICY == 1 || POLICY == 3);
   constexpr bool alias = POLICY == kPolicyAlias;
@@ -306,11 +306,19 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
 
     // ---- the pushed flow's Algorithm R draw is this arrival's word r (E.u3)
     const int slot = reservoir_slot_r32(V.rcnt, E.u3);
+    // n_flow_on_mode VPP: a lost-FIN flow completing in this step (only in the general loop:
+    // sim_step_group sends leak handles there, so the FAST loop carries none of this code)
+    if constexpr (!FAST) {
+      if (p.leak && ins)
+        count_lost(p, my_lost, gc.base_ms * 1000u + gc.base_rem + (uint32_t)ta, E.gid, E.episode);
+    }
     if (ins && slot >= 0) {
       const uint32_t fct = lost_fct(p, (uint32_t)(tc_a - ta),
                                     gc.base_ms * 1000u + gc.base_rem + (uint32_t)ta, E.gid, E.episode);
-      my_res[(uint32_t)slot] = make_uint3(fct, dur_sample(p, tc_a, ta, start_a),
-                                          gc.base_ms + (gc.base_rem + (uint32_t)tc_a) / 1000u);
+      // duration (dur_sample): the age tc - ta, or the service time svc = tc - start
+      const uint32_t dur = p.dur_service ? (uint32_t)svc : (uint32_t)(tc_a - ta);
+      my_res[(uint32_t)slot] =
+          make_uint3(fct, dur, gc.base_ms + (gc.base_rem + (uint32_t)tc_a) / 1000u);
       mark(slot);
     }
     if (mine) {
@@ -360,6 +368,7 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
   const uint32_t sb = b * (uint32_t)S + (uint32_t)s;  // valid when V.act
   uint3* const my_res = st.res + (size_t)sb * K;
   int2* const my_ring = st.ring + (size_t)sb * (size_t)Q;
+  uint32_t* const my_lost = st.lost_on + sb;  // used only when p.leak (lost_on allocated)
   const GroupAliasTab tab{atab, gbase};
   const int lane = gbase + s;
   int n_alias = 0;
@@ -391,6 +400,7 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
       V.rcnt = 0u;
       V.big = false;
       mark(0);  // emptied: the next observe recomputes the (zero) features
+      if (p.leak) *my_lost = 0u;
     }
     V.qcap = fails ? 0 : (recovers ? Q : V.qcap);
   }
@@ -406,6 +416,7 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
       const u32x4 d = philox4x32_10(
           u32x4{rc >> 1, E.gid, E.episode, (kStreamReservoir << 24) | (uint32_t)s}, p.key0, p.key1);
       const int slot = reservoir_slot(rc, d);
+      count_lost(p, my_lost, (uint32_t)base_us + (uint32_t)eta, E.gid, E.episode);
       if (slot >= 0) {
         const uint32_t fct =
             lost_fct(p, (uint32_t)(etc - eta), (uint32_t)base_us + (uint32_t)eta, E.gid, E.episode);
@@ -438,12 +449,12 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
   const GroupConst gc = group_const(p, base_ms, base_rem);
   const bool finite = lsq || alias || !V.act ||
                       (fabs(V.den) >= 1e-30 && fabs(V.den) <= 1e300);  // false for NaN
-  if (__all(finite))
+  if (__all(finite) && !p.leak)
     group_event_loop<G, POLICY, TRACE, true>(st, p, E, V, s, gbase, n_alias, gc, win, atab, acache, my_res,
-                                             my_ring);
+                                             my_ring, my_lost);
   else
     group_event_loop<G, POLICY, TRACE, false>(st, p, E, V, s, gbase, n_alias, gc, win, atab, acache, my_res,
-                                              my_ring);
+                                              my_ring, my_lost);
 
   // ---- rebase to the next step's start (this lane's server)
   E.next_arr -= dt;
@@ -539,6 +550,7 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
     V.rcnt = 0u;
     V.qcap = Q;  // every server is up at the episode start
     V.big = false;
+    if (p.leak && V.act) st.lost_on[sb] = 0u;  // n_flow_on_mode VPP: no lost flows yet
 #pragma unroll
     for (int k = 0; k < G; ++k) wall[k] = 1.0f;
   };

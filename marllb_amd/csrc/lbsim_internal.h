@@ -82,7 +82,8 @@ inline bool dyn_wave_fits(const LaunchCtx& L) {
   static const bool forced_lanes = std::getenv("LBSIM_DYN_GROUP_LANES") != nullptr;
   if (dyn_wave_mode() == 0 || forced_lanes || L.dyn_mapping == LBSIM_DYN_ENV_PER_LANE) return false;
   if (L.S > 8 || L.prm.Q > 32 || L.prm.policy == LBSIM_POLICY_ALIAS) return false;
-  return L.prm.fail_thr == 0u;  // server failures: the group / env-lane kernels
+  // server failures, n_flow_on_mode VPP's lost-flow counts: the group / env-lane kernels
+  return L.prm.fail_thr == 0u && L.prm.leak == 0;
 }
 
 inline bool dyn_wave_ok(const LaunchCtx& L) {

@@ -68,6 +68,10 @@ struct DevState {
   float* fcache;
   // server failures (only if fail_prob > 0, else nullptr): down[b*S + s] = 1 while server s is down
   uint32_t* down;
+  // n_flow_on_mode VPP with lost-FIN (SimParams::leak, else nullptr): lost_on[b*S + s] = lost-FIN
+  // flows of server s completed since the episode start / its last failure, never decremented
+  // (lbhash.h:193,214); observation column 0 adds it (n_flow_on)
+  uint32_t* lost_on;
   // stateless features API only: caller's separate value / timestamp arrays [n*K]
   const uint32_t* feat_vals;
   const uint32_t* feat_ts;
@@ -119,6 +123,8 @@ struct SimParams {
   // lbsim_config_t::duration_mode == SERVICE (dur_sample): the duration sample is the service
   // time, not the flow's age
   int32_t dur_service;
+  // n_flow_on_mode VPP and lost-FIN on: count the lost flows per server (DevState::lost_on)
+  int32_t leak;
 };
 
 constexpr uint32_t kStreamFailure = 5u;  // Philox stream of the failure / recovery draws
@@ -171,10 +177,12 @@ __device__ __forceinline__ uint32_t lf_mix(uint32_t h) {
 
 // fct + off + wait as a signed int32 us sample, saturated (the config bound keeps it in range for
 // Poisson work; trace work is unbounded).  oracle: the same.
+// With fct in [0, 2^31), |off| <= 1000 s (lbsim_config_validate) and wait >= 0, fct + off cannot
+// overflow and the sum can only pass INT32_MAX: two saturating 32-bit adds (v_add_i32 clamp)
+// give the 64-bit sum clamped, without 64-bit registers in the event loop.
 __device__ __forceinline__ uint32_t lf_guess(uint32_t fct, int32_t off, int32_t wait) {
-  int64_t g = (int64_t)(int32_t)fct + (int64_t)off + (int64_t)wait;
-  g = g > (int64_t)INT32_MAX ? (int64_t)INT32_MAX : (g < (int64_t)INT32_MIN ? (int64_t)INT32_MIN : g);
-  return (uint32_t)(int32_t)g;
+  const int32_t a = __builtin_elementwise_add_sat((int32_t)fct, off);
+  return (uint32_t)__builtin_elementwise_add_sat(a, wait);
 }
 
 // The fct sample of a completed flow, fct = tc - ta (lbhash.h:116-124, RSTACK: now - t_init), or,
@@ -206,6 +214,31 @@ __device__ __forceinline__ uint32_t lost_fct(const SimParams& p, uint32_t fct, u
 __device__ __forceinline__ uint32_t dur_sample(const SimParams& p, int32_t tc, int32_t ta,
                                                int32_t start) {
   return (uint32_t)(tc - (p.dur_service ? start : ta));
+}
+
+// Whether the flow that arrived at abs_ta is a lost-FIN flow (the test of lost_fct).
+__device__ __forceinline__ bool lf_lost(const SimParams& p, uint32_t abs_ta, uint32_t gid,
+                                        uint32_t episode) {
+  const uint32_t salt =
+      lf_mix(lf_mix(p.key0 ^ (episode * 0x9E3779B9u)) ^ gid ^ (p.key1 * 0x85EBCA6Bu));
+  return (lf_mix(abs_ta ^ salt) >> 8) < p.lf_thr;
+}
+
+// n_flow_on_mode VPP (p.leak, a uniform branch): a completing flow that is lost-FIN adds one to
+// its server's lost_on count (a device atomic: every completion point of every kernel counts,
+// whether or not Algorithm R keeps its sample; the count is order-free).
+__device__ __forceinline__ void count_lost(const SimParams& p, uint32_t* ctr, uint32_t abs_ta,
+                                           uint32_t gid, uint32_t episode) {
+  if (p.leak && lf_lost(p, abs_ta, gid, episode)) atomicAdd(ctr, 1u);
+}
+
+// Observation column 0: the server's flows in flight, plus its lost-FIN flows under n_flow_on_mode
+// VPP (read device-coherent: the one-launch forms observe right after their own dynamics).
+__device__ __forceinline__ float n_flow_on(const DevState& st, size_t sb) {
+  uint32_t n = st.hc[sb] >> 16;
+  if (st.lost_on != nullptr)
+    n += __hip_atomic_load(st.lost_on + sb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return (float)n;
 }
 
 constexpr uint32_t kTraceEnvStride = 7919u;        // SURVEY §8d C3 per-env offset
@@ -773,6 +806,11 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
     const u32x4 d = philox_rk(u32x4{L.arr_idx + 1u, L.gid, L.episode, kStreamArrival << 24},
                               ec.rk0, ec.rk1);
     const int slot = reservoir_slot_r32(cres, L.u3);
+    if constexpr (!FAST) {  // n_flow_on_mode VPP (sim_step sends leak handles to this loop)
+      if (p.leak && ins)  // this env's lost_on row: its reservoirs' row (my_res) over K
+        count_lost(p, st.lost_on + (size_t)(my_res - st.res) / K + (size_t)cs,
+                   ec.base_ms * 1000u + ec.base_rem + (uint32_t)ta, L.gid, L.episode);
+    }
     if (ins && slot >= 0) {
       const uint32_t fct = lost_fct(p, (uint32_t)(tc_a - ta),
                                     ec.base_ms * 1000u + ec.base_rem + (uint32_t)ta, L.gid, L.episode);
@@ -935,6 +973,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
         }
         fld<MAXS>(l, F_RCNT, s) = 0;
         mark_slot<MAXS>(l, s, 0);  // emptied: the next observe recomputes the (zero) features
+        if (p.leak) st.lost_on[b0 + (uint32_t)s] = 0u;
       }
     }
   }
@@ -953,6 +992,8 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
         const u32x4 d = philox4x32_10(
             u32x4{rc >> 1, L.gid, L.episode, (kStreamReservoir << 24) | (uint32_t)s}, p.key0, p.key1);
         const int slot = reservoir_slot(rc, d);
+        count_lost(p, st.lost_on + b0 + (uint32_t)s, (uint32_t)base_us + (uint32_t)eta, L.gid,
+                   L.episode);
         if (slot >= 0) {
           const uint32_t fct =
               lost_fct(p, (uint32_t)(etc - eta), (uint32_t)base_us + (uint32_t)eta, L.gid, L.episode);
@@ -987,7 +1028,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
   //      SED/SED2 scores can only be NaN when some den is 0 / inf / NaN: a wave whose envs all
   //      have finite scores runs the loop without the NaN fallbacks (a wave-uniform choice).
   const EvConst<MAXS> ec = ev_const<MAXS>(p, base_ms, base_rem);
-  if (lsq || alias || __all(finite_scores))
+  if ((lsq || alias || __all(finite_scores)) && !p.leak)
     event_loop<MAXS, POLICY, TRACE, true>(st, p, L, l, ec, den, rcp, n_alias, my_res, my_ring);
   else
     event_loop<MAXS, POLICY, TRACE, false>(st, p, L, l, ec, den, rcp, n_alias, my_res, my_ring);
@@ -1117,6 +1158,8 @@ __global__ void __launch_bounds__(64 * kDynWaves<MAXS>)
     draw_arrival<MAXS>(st, p, L, 0);
     trace_prefetch<MAXS>(st, p, L);
     clear_servers<MAXS>(p, L, l);
+    if (p.leak)  // a new episode: no lost flows yet (n_flow_on_mode VPP)
+      for (int s = 0; s < S; ++s) st.lost_on[b * (uint32_t)S + (uint32_t)s] = 0u;
 #pragma unroll
     for (int s = 0; s < MAXS; ++s) w[s] = 1.0f;
   };
@@ -1648,7 +1691,7 @@ __device__ __forceinline__ void observe_chunk_regs(const DevState& st, const Sim
       obs_out[(s_base + u) * NF + 1 + 5 * r + j] = v;
       st.fcache[so * 10 + (size_t)(5 * r + j)] = v;
     } else if (j == 5 && r == 0) {
-      obs_out[(s_base + u) * NF] = (float)(st.hc[so] >> 16);
+      obs_out[(s_base + u) * NF] = n_flow_on(st, so);
     }
   }
   wave_sync();
@@ -1708,7 +1751,7 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
     if (!fresh && !__any(w != 0u)) {  // no reservoir of the chunk changed: the cached features
       for (int e = lane; e < S * NF; e += 64) {
         const int s = e / NF, c = e - s * NF;
-        obs_out[s_base * NF + e] = c == 0 ? (float)(st.hc[srow + (size_t)s] >> 16)
+        obs_out[s_base * NF + e] = c == 0 ? n_flow_on(st, srow + (size_t)s)
                                           : st.fcache[(srow + (size_t)s) * 10 + (size_t)(c - 1)];
       }
       wave_sync();
@@ -1927,7 +1970,7 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
     const int s = e / NF, c = e - s * NF;
     float v;
     if (c == 0) {
-      v = (float)(st.hc[srow + (size_t)s] >> 16);
+      v = n_flow_on(st, srow + (size_t)s);
     } else {
       const int r = 2 * s + (c >= 6 ? 1 : 0);
       const int f = (c - 1) % 5;
@@ -2114,9 +2157,11 @@ __device__ __forceinline__ void observe_rows_paired_regs(const DevState& st, con
   o = xor_lane_z<4>(tmax, lane);
   tmax = o > tmax ? o : tmax;
 
-  // decay weights of the lane's 16 slots; f32 copies by slot in LDS for the gather after the sort
+  // decay weights of the lane's 16 slots; f32 copies by slot in LDS for the gather after the sort.
+  // Row u at stride KP = 136 dwords: the 32 lanes of a ds_write_b32 half (rows u, u + 1, u + 2,
+  // u + 3, slots 8 e + j) hit 32 distinct banks (a stride of 128 put 4 rows on every bank)
   float w[16];
-  float* wf = reinterpret_cast<float*>(&sc.vals[0][0]) + u * K;  // [8][K] f32 (4 KiB)
+  float* wf = reinterpret_cast<float*>(&sc.vals[u][0]);  // [8][KP] f32
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const int slot = 8 * e + j;
@@ -2265,7 +2310,7 @@ __device__ __forceinline__ void observe_rows_paired_regs(const DevState& st, con
       st.fcache[sb * 10 + (size_t)j] = v;
       st.fcache[sb * 10 + (size_t)(5 + j)] = v;
     } else if (j == 5) {
-      obs_out[u * NF] = (float)(st.hc[sb] >> 16);
+      obs_out[u * NF] = n_flow_on(st, sb);
     }
   }
   wave_sync();
@@ -2296,7 +2341,7 @@ __device__ __forceinline__ void observe_rows_paired(const DevState& st, const Si
     if (!fresh && !__any(w != 0u)) {  // no reservoir of the rows changed: the cached features
       for (int e = lane; e < nrows * NF; e += 64) {
         const int s = e / NF, c = e - s * NF;
-        obs_out[e] = c == 0 ? (float)(st.hc[row0 + (size_t)s] >> 16)
+        obs_out[e] = c == 0 ? n_flow_on(st, row0 + (size_t)s)
                             : st.fcache[(row0 + (size_t)s) * 10 + (size_t)(c - 1)];
       }
       wave_sync();

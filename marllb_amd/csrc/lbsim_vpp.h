@@ -131,7 +131,7 @@ __global__ void __launch_bounds__(64)
     tv_out[(pair * 2 + 1) * kVppN + i] = make_float2(t, dv);
   }
   if (lane == 0) {
-    if (nflow_out != nullptr) nflow_out[pair] = (int32_t)(st.hc[sb] >> 16);
+    if (nflow_out != nullptr) nflow_out[pair] = (int32_t)n_flow_on(st, sb);
     if (s == 0 && ts_out != nullptr)
       ts_out[e] = (float)((double)st.clock[b] * (double)p.dt_us * 1e-6);
   }

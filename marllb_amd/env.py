@@ -106,7 +106,7 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
                 lost_fin_prob: float = 0.0, flow_timeout: float = 40.0, flow_buckets: int = 1024,
                 fail_prob: float = 0.0, recover_prob: float = 0.1,
                 next_step_reset: bool = False,
-                duration_mode: str = "age") -> _lib.LbsimConfig:
+                duration_mode: str = "age", n_flow_on_mode: str = "queue") -> _lib.LbsimConfig:
     """Build and validate an lbsim_config_t from reference-style kwargs.
 
     server_rates defaults to identical servers at utilisation `load`: mu = rate / (load * S).
@@ -128,6 +128,9 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
     = the flow's age at its last data packet, completion - arrival, backlog wait included
     (src/vpp/lb/lbhash.h:129-136 records time_now - t_init on every plain ACK after the first);
     "service" = the service time alone.
+    n_flow_on_mode: observation column 0: "queue" = the flows in flight at the server; "vpp" =
+    the data plane's n_flow_on, which never decrements a lost-FIN flow (lbhash.h:193,214): the
+    flows in flight plus the server's lost-FIN flows since the episode start.
     """
     if reward_metric not in _lib.METRICS:  # rewards.py:321-323
         raise ValueError(f"Unsupported metric: {reward_metric}. Supported: {_lib.METRICS}")
@@ -185,6 +188,9 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
     if duration_mode not in _lib.DURATION_MODES:
         raise ValueError(f"Unknown duration_mode: {duration_mode}. Supported: {_lib.DURATION_MODES}")
     cfg.duration_mode = _lib.DURATION_MODES.index(duration_mode)
+    if n_flow_on_mode not in _lib.N_FLOW_ON_MODES:
+        raise ValueError(f"Unknown n_flow_on_mode: {n_flow_on_mode}. Supported: {_lib.N_FLOW_ON_MODES}")
+    cfg.n_flow_on_mode = _lib.N_FLOW_ON_MODES.index(n_flow_on_mode)
     _lib.validate(cfg)
     return cfg
 

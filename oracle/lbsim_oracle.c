@@ -323,6 +323,10 @@ typedef struct oracle {
   double* norm_mean; double* norm_std;
   /* server failures (only if fail_prob > 0): 1 = the server is down, per (env, server) */
   uint32_t* down;
+  /* n_flow_on_mode VPP with lost-FIN (leak): lost-FIN flows completed per (env, server) since the
+   * episode start / the server's last failure, never decremented (lbhash.h:193,214) */
+  int leak;
+  uint32_t* lost_on;
   /* TRACE arrivals (lbsim_set_trace semantics): us gap before each row, mean-1 work */
   uint32_t* trace_gap; float* trace_work; uint32_t trace_rows;
   /* not state: the Algorithm R draw word of each queued flow that arrived in the current step,
@@ -345,6 +349,7 @@ static void derive(oracle_t* o) {
   o->fail_thr = (uint32_t)llround((double)c->fail_prob * 16777216.0);
   o->rec_thr = (uint32_t)llround((double)c->recover_prob * 16777216.0);
   o->big_in_step = (o->dt_us >= (int32_t)((1u << 25) - 1u)) || o->lf_thr != 0u;
+  o->leak = c->n_flow_on_mode == LBSIM_NFLOW_VPP && o->lf_thr != 0u;
   o->key[0] = (uint32_t)(c->seed & 0xFFFFFFFFull);
   o->key[1] = (uint32_t)(c->seed >> 32);
 }
@@ -359,7 +364,7 @@ oracle_t* oracle_create(const lbsim_config_t* cfg) {
   const size_t sz[] = {B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4,
                        B * 8, BS * 4, BS * 4, BS * 4, BSQ * 8, BSK * 12, BS * 16, BS * 40,
                        cfg->normalize_obs ? BS * NF * 8 : 0, cfg->normalize_obs ? BS * NF * 8 : 0,
-                       cfg->fail_prob > 0.0f ? BS * 4 : 0};
+                       cfg->fail_prob > 0.0f ? BS * 4 : 0, o->leak ? BS * 4 : 0};
   size_t total = 0;
   for (size_t i = 0; i < sizeof(sz) / sizeof(sz[0]); ++i) total += sz[i];
   o->bytes = total;
@@ -372,7 +377,7 @@ oracle_t* oracle_create(const lbsim_config_t* cfg) {
                    (void**)&o->norm_count, (void**)&o->ep_return, (void**)&o->hc,
                    (void**)&o->last_tc, (void**)&o->res_count, (void**)&o->ring,
                    (void**)&o->res, (void**)&o->chg, (void**)&o->fcache, (void**)&o->norm_mean,
-                   (void**)&o->norm_std, (void**)&o->down};
+                   (void**)&o->norm_std, (void**)&o->down, (void**)&o->lost_on};
   for (size_t i = 0; i < sizeof(sz) / sizeof(sz[0]); ++i) {
     *ptrs[i] = sz[i] ? (void*)p : NULL;
     p += sz[i];
@@ -640,6 +645,11 @@ static void pop_until(env_ctx* e, int s, int32_t t, uint64_t base_us, double den
     if (tc > t) break;
     const int32_t start = ta > o->last_tc[sb] ? ta : o->last_tc[sb];
     /* the sample is (float)(int32_t)fct * 1e-6f seconds */
+    /* n_flow_on_mode VPP: a lost-FIN flow (the test of oracle_lost_fin_fct) is counted at its
+     * completion, sampled or not */
+    if (o->leak && oracle_lost_fin_fct(0u, (uint32_t)base_us + (uint32_t)ta, e->gid,
+                                       o->episode[e->b], o->key[0], o->key[1], o->lf_thr, 1, 0.0f) != 0u)
+      o->lost_on[sb] += 1u;
     const uint32_t fct = oracle_lost_fin_fct((uint32_t)(tc - ta), (uint32_t)base_us + (uint32_t)ta,
                                              e->gid, o->episode[e->b], o->key[0], o->key[1],
                                              o->lf_thr, o->lf_off_us, o->lf_wait_us);
@@ -723,6 +733,7 @@ static void sim_step(env_ctx* e, const float* w) {
         o->hc[sb] = (uint32_t)ring_head(o, sb); /* empty queue, reservoirs emptied: no HC_BIG */
         o->last_tc[sb] = LAST_NONE;
         o->res_count[sb] = 0u;
+        if (o->lost_on) o->lost_on[sb] = 0u;
         o->chg[sb * 4] |= 1u; /* emptied: the next observe recomputes the (zero) features */
       }
       if (o->down[sb]) qcap[s] = 0;
@@ -868,7 +879,9 @@ static void observe(oracle_t* o, size_t b, float* obs_out, float* reward_out, ui
     features_one(vf, w, wq, n, ff);
     features_one(vd, w, wq, n, fd);
     for (int f = 0; f < 5; ++f) { o->fcache[sb * 10 + (size_t)f] = ff[f]; o->fcache[sb * 10 + 5 + (size_t)f] = fd[f]; }
-    raw[s * NF + 0] = (float)ring_count(o, sb);
+    /* n_flow_on: flows in flight, plus the lost-FIN flows VPP never decrements (n_flow_on_mode
+     * VPP, lbhash.h:193,214) */
+    raw[s * NF + 0] = (float)((uint32_t)ring_count(o, sb) + (o->lost_on ? o->lost_on[sb] : 0u));
     for (int f = 0; f < 5; ++f) { raw[s * NF + 1 + f] = ff[f]; raw[s * NF + 6 + f] = fd[f]; }
   }
   if (step_mode) {
@@ -904,6 +917,7 @@ static void reset_env(oracle_t* o, size_t b) {
     o->res_count[sb] = 0u;
     for (int w = 0; w < 4; ++w) o->chg[sb * 4 + (size_t)w] = 0u;
     if (o->down) o->down[sb] = 0u; /* every server is up at the episode start */
+    if (o->lost_on) o->lost_on[sb] = 0u;
   }
   float w1[LBSIM_MAX_SERVERS];
   for (int s = 0; s < LBSIM_MAX_SERVERS; ++s) w1[s] = 1.0f;

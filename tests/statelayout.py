@@ -4,7 +4,7 @@ import numpy as np
 K, NF = 128, 11
 
 
-def sections(B, S, Q, normalize, failures=False):
+def sections(B, S, Q, normalize, failures=False, leak=False):
     BS = B * S
     out = [("next_arr", np.int32, B), ("next_work", np.float32, B), ("next_u2", np.uint32, B),
            ("next_u3", np.uint32, B), ("arr_idx", np.uint32, B), ("episode", np.uint32, B),
@@ -16,12 +16,18 @@ def sections(B, S, Q, normalize, failures=False):
         out += [("norm_mean", np.float64, BS * NF), ("norm_std", np.float64, BS * NF)]
     if failures:
         out += [("down", np.uint32, BS)]
+    if leak:  # n_flow_on_mode "vpp" with lost-FIN: lost flows per server
+        out += [("lost_on", np.uint32, BS)]
     return out
 
 
-def parse(buf: bytes, B, S, Q, normalize, failures=False):
+def has_leak(cfg) -> bool:
+    return cfg.n_flow_on_mode == 1 and cfg.lost_fin_prob > 0
+
+
+def parse(buf: bytes, B, S, Q, normalize, failures=False, leak=False):
     d, off = {}, 0
-    for name, dt, n in sections(B, S, Q, normalize, failures):
+    for name, dt, n in sections(B, S, Q, normalize, failures, leak):
         nb = np.dtype(dt).itemsize * n
         d[name] = np.frombuffer(buf[off:off + nb], dtype=dt)
         off += nb

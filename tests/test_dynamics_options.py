@@ -230,3 +230,45 @@ def test_lost_fin_guess_at_the_accepted_limit(oracle_mod):
     wait = f1 - f0 - (int(round(timeout * 1e6)) - 40_000_000)
     assert (f1 > 0).all() and (wait >= 0).all()
     assert f1.max() < 2 ** 31 - 1
+
+
+def test_n_flow_on_vpp_counts_lost_flows(oracle_mod):
+    """n_flow_on_mode="vpp": VPP's n_flow_on is +1 at a flow's first ACK and -1 at its RSTACK
+    (lbhash.h:116-120,138-142,167) and a lost-FIN flow is never decremented (lbhash.h:193,214):
+    column 0 = the flows in flight + the server's lost-FIN flows since the episode start.  The
+    simulation itself is unchanged (every other column, the queues and reservoirs equal the
+    "queue" run); the leak grows step by step at about lost_fin_prob x the completions; off
+    without lost-FIN (no state section, bit-identical)."""
+    from marllb_amd.env import make_config
+    B, S, steps = 64, 4, 6
+    outs = {}
+    for mode in ("queue", "vpp"):
+        cfg = make_config(B, S, seed=5, lost_fin_prob=0.25, n_flow_on_mode=mode)
+        ora = oracle_mod.OracleEnv(cfg, threads=4)
+        ora.reset()
+        rng = np.random.default_rng(5)
+        outs[mode] = [ora.step(rng.integers(0, 3, (B, S)).astype(np.int64)) for _ in range(steps)]
+        outs[mode + "_st"] = statelayout.parse(ora.state_bytes(), B, S, cfg.queue_capacity, False,
+                                               False, statelayout.has_leak(cfg))
+        ora.close()
+    st_q, st_v = outs["queue_st"], outs["vpp_st"]
+    for k in st_q:
+        if k not in ("fcache", "ep_return"):
+            np.testing.assert_array_equal(st_q[k], st_v[k], err_msg=k)
+    leak = st_v["lost_on"].reshape(B, S).astype(np.float32)
+    o_q, o_v = outs["queue"][-1][0], outs["vpp"][-1][0]
+    np.testing.assert_array_equal(o_v[:, :, 1:], o_q[:, :, 1:])
+    np.testing.assert_array_equal(o_v[:, :, 0], o_q[:, :, 0] + leak)
+    prev = None
+    for (ov, *_), (oq, *_) in zip(outs["vpp"], outs["queue"]):
+        d = (ov[:, :, 0] - oq[:, :, 0])
+        assert (d >= 0).all()
+        if prev is not None:
+            assert (d >= prev).all(), "the leak never decreases within an episode"
+        prev = d
+    # completions per server-step ~ arrivals (100 per env-step over 4 servers) at 25 % lost
+    per_step = leak.mean() / (steps + 8)  # 8 warm-up steps
+    assert 0.15 * 25 < per_step < 0.35 * 25, per_step
+    # without lost-FIN the mode changes nothing (no section)
+    a = make_config(B, S, seed=5, n_flow_on_mode="vpp")
+    assert not statelayout.has_leak(a)

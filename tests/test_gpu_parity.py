@@ -251,6 +251,14 @@ CONFIGS = [
                          "arrival_rate": 800.0}),
     dict(B=48, S=8, kw={"duration_mode": "service", "lost_fin_prob": 0.2, "flow_timeout": 10.0}),
     dict(B=8256, S=4, kw={"duration_mode": "service", "load": 1.1}),
+    # n_flow_on_mode "vpp" (column 0 never drops a lost-FIN flow, lbhash.h:193,214): with
+    # failures (counts cleared), on 3 servers, on 20 servers, and the headline group shape
+    dict(B=64, S=4, kw={"n_flow_on_mode": "vpp", "lost_fin_prob": 0.3, "fail_prob": 0.1}),
+    dict(B=50, S=3, kw={"n_flow_on_mode": "vpp", "lost_fin_prob": 0.5, "flow_timeout": 10.0,
+                        "assign_policy": "lsq"}),
+    dict(B=40, S=20, kw={"n_flow_on_mode": "vpp", "lost_fin_prob": 0.2, "assign_policy": "sed2"}),
+    dict(B=8256, S=4, kw={"n_flow_on_mode": "vpp", "lost_fin_prob": 0.2, "max_steps": 5,
+                          "next_step_reset": True}),
 ]
 
 
@@ -275,9 +283,9 @@ def _actions(rng, B, S, cfgkw):
     return rng.integers(-n, n, (B, S)).astype(np.int64)
 
 
-def _compare_state(h_gpu, ora, B, S, Q, norm, fail=False):
-    g = statelayout.parse(h_gpu.state_bytes(), B, S, Q, norm, fail)
-    o = statelayout.parse(ora.state_bytes(), B, S, Q, norm, fail)
+def _compare_state(h_gpu, ora, B, S, Q, norm, fail=False, leak=False):
+    g = statelayout.parse(h_gpu.state_bytes(), B, S, Q, norm, fail, leak)
+    o = statelayout.parse(ora.state_bytes(), B, S, Q, norm, fail, leak)
     for name in g:
         if name == "ring":
             continue
@@ -295,6 +303,7 @@ def _run_vs_oracle(oracle_mod, B, S, kw, akw, case, mapping="auto", steps=12, po
     env = VecLoadBalanceEnv(B, S, device="cuda:0", autoreset=autoreset, dyn_mapping=mapping, **kw)
     ora = oracle_mod.OracleEnv(make_config(B, S, **kw), threads=threads, trace=kw.get("trace"))
     Q, norm, fail = env.cfg.queue_capacity, bool(env.cfg.normalize_obs), env.cfg.fail_prob > 0
+    leak = statelayout.has_leak(env.cfg)
     obs_g = env.reset().cpu().numpy()
     obs_o = ora.reset()
     np.testing.assert_array_equal(obs_g, obs_o)
@@ -307,7 +316,7 @@ def _run_vs_oracle(oracle_mod, B, S, kw, akw, case, mapping="auto", steps=12, po
         np.testing.assert_array_equal(og.cpu().numpy(), oo, err_msg=f"obs step {k}")
         np.testing.assert_array_equal(rg.cpu().numpy(), ro, err_msg=f"reward step {k}")
         np.testing.assert_array_equal(dg.cpu().numpy().astype(np.uint8), do)
-    _compare_state(env.handle, ora, B, S, Q, norm, fail)
+    _compare_state(env.handle, ora, B, S, Q, norm, fail, leak)
     # masked reset of every third env, then more steps
     mask = (np.arange(B) % 3 == 0).astype(np.uint8)
     og = env.reset(mask=torch.from_numpy(mask)).cpu().numpy()
@@ -319,7 +328,7 @@ def _run_vs_oracle(oracle_mod, B, S, kw, akw, case, mapping="auto", steps=12, po
         oo, ro, do, _ = ora.step(a)
         np.testing.assert_array_equal(og.cpu().numpy(), oo)
         np.testing.assert_array_equal(rg.cpu().numpy(), ro)
-    _compare_state(env.handle, ora, B, S, Q, norm, fail)
+    _compare_state(env.handle, ora, B, S, Q, norm, fail, leak)
     ora.close()
     return env
 
