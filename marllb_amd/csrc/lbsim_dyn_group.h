@@ -210,7 +210,7 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
         while (r >= rows) r -= rows;
         gap = (int32_t)st.trace_gap[r];
         wk = st.trace_work[r];
-      } else {
+      } else {  // (the two logs as one packed-f32 polynomial measured 2 % slower: r05t)
         gap = (int32_t)(-lb_logf(u01_open0(d.x)) * gc.mean_gap);
         wk = -lb_logf(u01_open0(d.y));
       }
