@@ -19,7 +19,8 @@ from collections import defaultdict
 def short(name: str) -> str:
     name = name.replace("(anonymous namespace)::", "")
     for key in ("dynamics_kernel", "dynamics_group_kernel", "dynamics_wave_kernel",
-                "observe_kernel", "features_kernel", "reward_kernel", "fused_step_kernel",
+                "observe_kernel", "observe_pair_kernel", "features_kernel", "reward_kernel",
+                "fused_step_kernel",
                 "step_wave_kernel", "step_stats_kernel", "vpp_"):
         if key in name:
             return (name.split("(")[0].replace("void ", "").replace("lbk::", "")
@@ -33,11 +34,14 @@ def is_reset(k: str) -> bool:
         return False
     name, args = k.split("<", 1)
     a = [x.strip() for x in args.rstrip(">").split(",")]
+    if name == "observe_pair_kernel":  # observe_pair_kernel<MODE, FAC>
+        return a[0] == "1"
     return name.startswith(("dynamics", "observe_kernel")) and len(a) > 1 and a[1] == "1"
 
 
 def is_step(k: str) -> bool:
-    return (k.startswith(("dynamics", "observe_kernel", "step_wave_kernel", "fused_step_kernel"))
+    return (k.startswith(("dynamics", "observe_kernel", "observe_pair_kernel", "step_wave_kernel",
+                          "fused_step_kernel"))
             and not is_reset(k))
 
 
