@@ -707,8 +707,10 @@ def main():
                      "mu=lambda/(0.8 S) per server, random discrete policy") if tr is None else
                     (f"trace replay {tr.name} ({tr.rows} rows, {tr.rate:.1f}/s; per-env offset "
                      "gid*7919), mu=rate/(0.8 S), random discrete policy"),
-            "config": {"workload": ("LB env random-policy rollout, 4 servers (BASELINE configs[1] "
-                                    "rollout at the north-star batch)") if tr is None else
+            "config": {"workload": (f"LB env random-policy rollout, {S} servers (BASELINE "
+                                    "configs[1] rollout at the north-star batch)" if S == 4
+                                    and B == 65536 else f"LB env random-policy rollout, {B} x "
+                                    f"{S} (BASELINE configs[1] shape family)") if tr is None else
                                    f"LB env trace replay, {S} servers (BASELINE configs[2])",
                        "assign_policy": args.policy,
                        "envs_per_gpu": B, "servers": S, "global_batch": world * B,

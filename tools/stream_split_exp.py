@@ -20,12 +20,17 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--parts", default="1,2,4")
+    ap.add_argument("--join", default="none,step",
+                    help="none: the parts run free on their streams; step: one randint on the "
+                         "main stream per step, every part waits for it and the main stream "
+                         "waits for every part (the join a single batched step() would need)")
     args = ap.parse_args()
     import torch
     from marllb_amd.env import VecLoadBalanceEnv
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
-    for P in [int(x) for x in args.parts.split(",")]:
+    main_s = torch.cuda.current_stream(dev)
+    for join, P in [(j, int(x)) for j in args.join.split(",") for x in args.parts.split(",")]:
         b = args.batch // P
         S = args.servers
         streams = [torch.cuda.Stream(dev) for _ in range(P)]
@@ -41,13 +46,30 @@ def main():
             gens.append(g)
         torch.cuda.synchronize()
 
-        def one_step():
+        def one_step_join():
+            a = torch.randint(0, 3, (args.batch, S), device=dev, dtype=torch.int64,
+                              generator=gens[0])
+            ev = torch.cuda.Event()
+            ev.record(main_s)
+            done = []
+            for i in range(P):
+                streams[i].wait_event(ev)
+                with torch.cuda.stream(streams[i]):
+                    envs[i].step(a[i * b:(i + 1) * b])
+                    e = torch.cuda.Event()
+                    e.record(streams[i])
+                    done.append(e)
+            for e in done:
+                main_s.wait_event(e)
+
+        def one_step_free():
             for i in range(P):
                 with torch.cuda.stream(streams[i]):
                     a = torch.randint(0, 3, (b, S), device=dev, dtype=torch.int64,
                                       generator=gens[i])
                     envs[i].step(a)
 
+        one_step = one_step_join if join == "step" else one_step_free
         for _ in range(args.warmup):
             one_step()
         torch.cuda.synchronize()
@@ -56,7 +78,7 @@ def main():
             one_step()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        print(json.dumps({"parts": P, "batch": args.batch, "servers": S, "steps": args.steps,
+        print(json.dumps({"parts": P, "join": join, "batch": args.batch, "servers": S, "steps": args.steps,
                           "ms_per_step": dt / args.steps * 1e3,
                           "env_steps_per_s": args.batch * args.steps / dt}), flush=True)
         del envs
