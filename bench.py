@@ -661,7 +661,7 @@ def main():
         rate = tr.rate if tr is not None else ARRIVAL_RATE
         slots, inflight = step_accounting(handle, lib, one_step, args.steps, replay)
         abytes = algorithmic_bytes(S, slots / B, inflight / B,
-                                   paired=obs_name == "observe_pair_kernel")
+                                   paired=obs_name.startswith("observe_pair"))
         abytes[obs_name] = abytes.pop("observe_kernel")
         abytes[dyn] = abytes.pop("dynamics_kernel")
         abytes[fused] = abytes.pop("fused_step_kernel")

@@ -857,8 +857,10 @@ int lbsim_sac_actor_step(const lbsim_sac_actor_t* n, const float* state, float* 
   a.step = step;
   a.step_dev = n->step_dev;
   int mt = fused_mt(B);
-  // the [R][ld] tile + split-K scratch of the heads ([4][2][R][16])
-  auto lds_of = [&](int m) { return (size_t)16 * m * (a.ld + 128) * 4; };
+  // the [R][ld] tile + split-K scratch of the heads ([4][nt][R][16], nt = ceil(2A / 16)): at A = 8
+  // 20.6 KB per 16-env tile, 7 tiles per CU
+  const int nt_heads = (2 * a.A + 15) / 16;
+  auto lds_of = [&](int m) { return (size_t)16 * m * (a.ld + 64 * nt_heads) * 4; };
   while (mt > 1 && lds_of(mt) > kFusedLdsMax) mt >>= 1;
   const size_t lds = lds_of(mt);
   const hipStream_t s = (hipStream_t)stream;

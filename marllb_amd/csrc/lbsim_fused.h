@@ -308,16 +308,47 @@ struct SacActorArgs {
   const uint32_t* step_dev;  // when set, the Philox step counter is *step_dev (graph replays)
 };
 
+// The SAC tile's input rows in one pass with no index division: thread t < kxp stages state
+// column t, kxp <= t < kxp + H hidden column t - kxp, each for all R rows (R independent loads in
+// flight per thread; a row's loads are contiguous across the threads).
+template <int R, int H>
+__device__ __forceinline__ void stage_sac_rows(float* lds, const SacActorArgs& p, int64_t row0) {
+  const int t = threadIdx.x, kxp = p.kxp, ld = p.ld;
+  for (int c = t; c < kxp + H; c += blockDim.x) {
+    const bool st = c < kxp;
+    const float* src = st ? p.state + c : p.hidden + (c - kxp);
+    const int64_t stride = st ? p.I : H;
+    const bool col_ok = !st || c < p.I;
+    float v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int64_t b = row0 + r;
+      const bool live = col_ok && b < p.B && (st || !(p.reset && p.reset[b]));
+      v[r] = live ? src[b * stride] : 0.0f;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) lds[r * ld + c] = v[r];
+  }
+}
+
+#ifndef LBSIM_SAC_WPE
+#define LBSIM_SAC_WPE 1
+#endif
+
 template <int MT, int H, int F>
-__global__ void __launch_bounds__(256) sac_actor_kernel(SacActorArgs p) {
+__global__ void __launch_bounds__(256, LBSIM_SAC_WPE) sac_actor_kernel(SacActorArgs p) {
   const uint32_t step = p.step_dev != nullptr ? *p.step_dev : p.step;
   extern __shared__ float lds[];
   constexpr int R = 16 * MT;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t row0 = (int64_t)blockIdx.x * R;
   const int ld = p.ld, kxp = p.kxp;
+#if LBSIM_SAC_OLD_STAGE
   stage_rows(lds, ld, 0, p.state, p.I, p.I, kxp, R, row0, p.B, nullptr);
   stage_rows(lds, ld, kxp, p.hidden, H, H, H, R, row0, p.B, p.reset);
+#else
+  stage_sac_rows<R, H>(lds, p, row0);
+#endif
   __syncthreads();
   {
     f4 hn[(H / 16 + 3) / 4][MT];

@@ -2363,6 +2363,42 @@ __device__ __forceinline__ void observe_rows_paired(const DevState& st, const Si
   }
 }
 
+// Rows [s0, s0 + 8) of env b of a wide env (S a multiple of 8, S >= 16): the paired register
+// path of observe_rows_paired over one wave's 8 rows, written to obs_env + s0 * NF; the rows the
+// register path cannot take go through the two 4-server observe_chunk calls.  fresh: env b was
+// reset by this step (no cached features).
+template <bool INC>
+__device__ __forceinline__ void observe_rows_paired_wide(const DevState& st, const SimParams& p,
+                                                         size_t b, int s0, ObsScratch& sc,
+                                                         float* obs_env, int lane, bool fresh) {
+  const size_t row0 = b * (size_t)p.S + (size_t)s0;
+  const size_t usb = row0 + (size_t)(lane >> 3);
+  float* obs_out = obs_env + s0 * NF;
+  const uint32_t rc = st.res_count[usb];
+  const uint32_t hcw = st.hc[usb];
+  if constexpr (INC) {
+    const uint32_t w = lane < 32 ? st.chg[(row0 + (size_t)(lane >> 2)) * 4 + (lane & 3)] : 0u;
+    if (!fresh && !__any(w != 0u)) {  // none of the 8 reservoirs changed: the cached features
+      for (int e = lane; e < 8 * NF; e += 64) {
+        const int s = e / NF, c = e - s * NF;
+        obs_out[e] = c == 0 ? n_flow_on(st, row0 + (size_t)s)
+                            : st.fcache[(row0 + (size_t)s) * 10 + (size_t)(c - 1)];
+      }
+      wave_sync();
+      return;
+    }
+  }
+  const int n = rc < (uint32_t)K ? (int)rc : K;
+  if (!__any(n < 8 || (hcw & kHcBig) != 0u)) {
+    if (!__any(n < K)) observe_rows_paired_regs<true>(st, p, row0, 8, K, sc, obs_out, lane);
+    else observe_rows_paired_regs<false>(st, p, row0, 8, n, sc, obs_out, lane);
+    return;
+  }
+  for (int c = s0; c < s0 + 8; c += kObsChunk)
+    observe_chunk<true, INC, LBSIM_OBS_PAIR_FALLBACK_REGS != 0>(st, p, b, c, kObsChunk, sc,
+                                                                 obs_env, lane, fresh);
+}
+
 // ================================================================ observe (one wave = one env)
 
 struct ObsOutputs {
@@ -2530,6 +2566,41 @@ __global__ void __launch_bounds__(64, LBSIM_OBS_PAIR_WAVES)
     observe_outputs<8, MODE, FAC>(st, p, out, b0 + (size_t)e, s_obs + e * S * NF, s_act, lane, 64);
     wave_sync();  // s_act reused by the next env
   }
+}
+
+// Step-mode observation of paired records for S = 16 (configs[4]'s 4 agents x 4 servers): one
+// workgroup of two waves per env, wave w observing rows [8 w, 8 w + 8) (observe_rows_paired_wide),
+// then the env's reward, episode words and outputs (observe_outputs) -- the work of
+// observe_kernel<16>'s four chunk waves in two.
+#ifndef LBSIM_OBS_PAIR16_WAVES
+#define LBSIM_OBS_PAIR16_WAVES LBSIM_OBS_PAIR_WAVES
+#endif
+template <int MODE, bool FAC>
+__global__ void __launch_bounds__(128, LBSIM_OBS_PAIR16_WAVES)
+    observe_pair16_kernel(DevState st, SimParams p, ObsOutputs out) {
+  __shared__ ObsScratch sc[2];
+  __shared__ float s_obs[16 * NF];
+  __shared__ float s_act[16];
+  const size_t b = blockIdx.x;
+  const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const bool fresh = MODE == kModeStep && p.next_reset && st.ep_step[b] < 0;
+  observe_rows_paired_wide<MODE == kModeStep>(st, p, b, 8 * wv, sc[wv], s_obs, lane, fresh);
+  __syncthreads();
+  observe_outputs<16, MODE, FAC>(st, p, out, b, s_obs, s_act, tid, 128);
+}
+
+// The raw rows of paired-record wide envs (S > 16, a multiple of 8) for observe_rows_kernel: one
+// single-wave workgroup per (env, 8-row group), as observe_chunks_kernel per 4-server chunk.
+template <int MODE>
+__global__ void __launch_bounds__(64, LBSIM_OBS_PAIR_WAVES)
+    observe_pair_chunks_kernel(DevState st, SimParams p, ObsOutputs out, int ngroups) {
+  const size_t b = blockIdx.x / (unsigned)ngroups;
+  const int c = (int)(blockIdx.x - b * (unsigned)ngroups);
+  __shared__ ObsScratch sc;
+  const bool fresh = MODE == kModeStep && p.next_reset && st.ep_step[b] < 0;
+  observe_rows_paired_wide<MODE == kModeStep>(st, p, b, 8 * c, sc,
+                                              out.obs + b * (size_t)p.S * NF, (int)threadIdx.x,
+                                              fresh);
 }
 
 // Wide envs (S > 16: configs[4] read literally, 4 agents x 16 servers), in two launches instead of

@@ -60,7 +60,8 @@ void launch_observe_split(const LaunchCtx& L, const ObsOutputs& o, const uint8_t
 }
 
 // The paired step observe (observe_pair_kernel): records whose duration word equals the fct word
-// by construction (duration_mode AGE, lost-FIN off) and S <= 8 (8 / S whole envs per wave).  LBSIM_OBSERVE_PAIRED=0
+// by construction (duration_mode AGE, lost-FIN off) and S <= 8 (8 / S whole envs per wave), or S a
+// multiple of 8 (S / 8 waves per env: observe_pair16_kernel, observe_pair_chunks_kernel).  LBSIM_OBSERVE_PAIRED=0
 // turns it off (A/B; the same bits either way).
 bool observe_paired(const LaunchCtx& L) {
   static const bool on = [] {
@@ -68,7 +69,7 @@ bool observe_paired(const LaunchCtx& L) {
     return !(e != nullptr && std::strcmp(e, "0") == 0);
   }();
   return on && L.prm.dur_service == 0 && L.prm.lf_thr == 0u &&
-         L.S <= 8;
+         (L.S <= 8 || L.S % 8 == 0);
 }
 
 // the problem-05 facade rows (agent_obs / state) come from their own instantiation
@@ -76,6 +77,29 @@ template <int MODE>
 void launch_observe_m(const LaunchCtx& L, const ObsOutputs& o, const uint8_t* mask,
                       hipStream_t stream) {
   const bool fac = o.agent_obs != nullptr || o.state != nullptr;
+  if constexpr (MODE == kModeStep) {
+  if (observe_paired(L) && L.S > 8) {  // 8 rows per wave, S / 8 per env
+    if (L.S == 16) {
+      const dim3 grid((unsigned)L.B), block(128);
+      if (fac)
+        LBSIM_LAUNCH((observe_pair16_kernel<MODE, true>), grid, block, 0, stream, L.st, L.prm, o);
+      else
+        LBSIM_LAUNCH((observe_pair16_kernel<MODE, false>), grid, block, 0, stream, L.st, L.prm, o);
+      return;
+    }
+    const int ng = L.S / 8;
+    LBSIM_LAUNCH(observe_pair_chunks_kernel<MODE>, dim3((unsigned)((int64_t)L.B * ng)), dim3(64), 0,
+                 stream, L.st, L.prm, o, ng);
+    const dim3 grid((unsigned)L.B), block(64);
+    if (fac)
+      LBSIM_LAUNCH((observe_rows_kernel<64, MODE, true>), grid, block, 0, stream, L.st, L.prm, o,
+                   nullptr);
+    else
+      LBSIM_LAUNCH((observe_rows_kernel<64, MODE, false>), grid, block, 0, stream, L.st, L.prm, o,
+                   nullptr);
+    return;
+  }
+  }
   if (MODE == kModeStep && observe_paired(L)) {  // 8 rows per wave: 8 / S envs
     const int epw = 8 / L.S;
     const dim3 grid((unsigned)((L.B + epw - 1) / epw)), block(64);

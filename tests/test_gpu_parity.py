@@ -251,6 +251,16 @@ CONFIGS = [
                          "arrival_rate": 800.0}),
     dict(B=48, S=8, kw={"duration_mode": "service", "lost_fin_prob": 0.2, "flow_timeout": 10.0}),
     dict(B=8256, S=4, kw={"duration_mode": "service", "load": 1.1}),
+    # paired observe of wide envs (S = 16: two waves per env, observe_pair16_kernel; S = 32:
+    # one wave per 8-row group + the rows kernel): next-step auto-reset with normalisation,
+    # sparse arrivals (unchanged groups keep cached features, rows with n < 8 take the chunk
+    # fallback), waits > 33 s (the fallback's two-pass sort)
+    dict(B=50, S=16, kw={"max_steps": 3, "next_step_reset": True, "normalize_obs": True}),
+    dict(B=40, S=16, kw={"arrival_rate": 12.0, "server_rates": [1.0, 1.2] * 8,
+                         "assign_policy": "sed2"}),
+    dict(B=32, S=16, kw={"server_rates": [1.0, 1.5, 2.0, 2.5] * 4, "arrival_rate": 20.0,
+                         "step_interval": 5.0, "queue_capacity": 64}),
+    dict(B=24, S=32, kw={"max_steps": 2, "next_step_reset": True, "arrival_rate": 900.0}),
     # n_flow_on_mode "vpp" (column 0 never drops a lost-FIN flow, lbhash.h:193,214): with
     # failures (counts cleared), on 3 servers, on 20 servers, and the headline group shape
     dict(B=64, S=4, kw={"n_flow_on_mode": "vpp", "lost_fin_prob": 0.3, "fail_prob": 0.1}),
@@ -365,8 +375,10 @@ def _expected_step_kernels(B, S, simds):
         occ = 2 if B <= 2 * simds else 4
         return {4: f"step_wave_kernel<{ng}, 0, false, {occ}, {4 if S <= 4 else 8}>"}
     g = 2 if S <= 2 else (8 if B * 4 // 64 <= simds // 2 else 4) if S <= 4 else 8 if S <= 8 else 16
-    # paired records (duration = the flow's age, lost-FIN off), S <= 8: 8 // S envs per wave
-    obs = "observe_pair_kernel<0, " if S <= 8 else "observe_kernel<"
+    # paired records (duration = the flow's age, lost-FIN off), S <= 8: 8 // S envs per wave;
+    # S = 16: two waves per env
+    obs = ("observe_pair_kernel<0, " if S <= 8 else "observe_pair16_kernel<0, " if S == 16
+           else "observe_pair_chunks_kernel<0>" if S % 8 == 0 else "observe_kernel<")
     return {0: f"dynamics_group_kernel<{g}, 0, 0, false", 1: obs}
 
 

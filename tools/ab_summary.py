@@ -12,4 +12,6 @@ for line in open(sys.argv[1]):
         continue
     r = d["roofline"]
     ks = " ".join(f"{k}={v * 1e3:.1f}us" for k, v in r["kernel_avg_ms"].items())
+    pol = d.get("policy_ms_per_step")
+    ks += f" policy={pol * 1e3:.1f}us" if pol is not None else ""
     print(f"  {d['value'] / 1e6:.1f} M/s  {d['ms_per_step'] * 1e3:.1f} us/step  {ks}")

@@ -45,8 +45,8 @@ def is_step_kernel(k: str) -> bool:
     name = k.split("<", 1)[0]
     if name in ("step_wave_kernel", "fused_step_kernel"):
         return True
-    if name == "observe_pair_kernel":  # observe_pair_kernel<MODE, FAC>
-        return k.split("<", 1)[1].split(",")[0].strip() == "0"
+    if name.startswith("observe_pair"):  # observe_pair*_kernel<MODE, ...>
+        return k.split("<", 1)[1].split(",")[0].rstrip(">").strip() == "0"
     if name not in ("dynamics_group_kernel", "dynamics_kernel", "dynamics_wave_kernel",
                     "observe_kernel"):
         return False

@@ -34,13 +34,13 @@ def is_reset(k: str) -> bool:
         return False
     name, args = k.split("<", 1)
     a = [x.strip() for x in args.rstrip(">").split(",")]
-    if name == "observe_pair_kernel":  # observe_pair_kernel<MODE, FAC>
+    if name.startswith("observe_pair"):  # observe_pair*_kernel<MODE, ...>
         return a[0] == "1"
     return name.startswith(("dynamics", "observe_kernel")) and len(a) > 1 and a[1] == "1"
 
 
 def is_step(k: str) -> bool:
-    return (k.startswith(("dynamics", "observe_kernel", "observe_pair_kernel", "step_wave_kernel",
+    return (k.startswith(("dynamics", "observe_kernel", "observe_pair", "step_wave_kernel",
                           "fused_step_kernel"))
             and not is_reset(k))
 
