@@ -275,16 +275,29 @@ __device__ __forceinline__ void gru_store(const f4 (&hn)[(H / 16 + 3) / 4][MT], 
 }
 
 // Stage rows [row0, row0 + R) of a [B, n] matrix (row stride src_ld) into LDS cols [col0, col0 +
-// npad), zero past n, past B and (if reset_mask) for rows whose mask byte is set.
+// npad), zero past n, past B and (if reset_mask) for rows whose mask byte is set.  Eight elements
+// per thread per pass, all eight loads issued before the LDS stores: the policy kernels' staging
+// sits on their critical path (QMIX runs one round of workgroups), so its HBM latency is paid once
+// per eight elements, not once per element.
 __device__ __forceinline__ void stage_rows(float* lds, int ld, int col0, const float* src,
                                            int64_t src_ld, int n, int npad, int R, int64_t row0,
                                            int64_t B, const uint8_t* reset_mask) {
-  for (int e = threadIdx.x; e < R * npad; e += blockDim.x) {
-    const int r = e / npad, c = e - r * npad;
-    const int64_t b = row0 + r;
-    float v = 0.0f;
-    if (c < n && b < B && !(reset_mask && reset_mask[b])) v = src[b * src_ld + c];
-    lds[r * ld + col0 + c] = v;
+  const int total = R * npad, nthr = (int)blockDim.x;
+  for (int e0 = (int)threadIdx.x; e0 < total; e0 += 8 * nthr) {
+    float v[8];
+    int at[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = e0 + i * nthr;
+      const int r = e / npad, c = e - r * npad;
+      const int64_t b = row0 + r;
+      at[i] = e < total ? r * ld + col0 + c : -1;
+      v[i] = (e < total && c < n && b < B && !(reset_mask && reset_mask[b])) ? src[b * src_ld + c]
+                                                                               : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (at[i] >= 0) lds[at[i]] = v[i];
   }
 }
 
@@ -757,17 +770,33 @@ __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
   if (h == 0 && lane < R)
     eps_d = philox4x32_10(u32x4{(uint32_t)(row0 + lane), step, (uint32_t)a, 4u << 24}, p.key0,
                           p.key1);
+  // one round of 512 workgroups: the staging's HBM latency is exposed, so every thread issues all
+  // its loads before its LDS stores (column-owner form, no index division): obs column c = t2 (+
+  // 128 k) of the 16 rows, hidden column t2 mod H of 16 H / 128 rows
   if (p.sld > 0) stage_rows(pre, p.sld, 0, p.state, p.Ds, p.Ds, p.ksp, R, row0, p.B, nullptr);
-  for (int e = t2; e < R * kxp; e += 128) {  // obs rows of agent a, zero padded
-    const int r = e / kxp, c = e - r * kxp;
-    const int64_t b = row0 + r;
-    mine[r * lda + c] = (c < p.I && b < p.B) ? p.obs[(b * A + a) * p.I + c] : 0.0f;
+  for (int c = t2; c < kxp; c += 128) {  // obs rows of agent a, zero padded
+    float v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int64_t b = row0 + r;
+      v[r] = (c < p.I && b < p.B) ? p.obs[(b * A + a) * p.I + c] : 0.0f;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) mine[r * lda + c] = v[r];
   }
-  for (int e = t2; e < R * H; e += 128) {  // hidden rows (zeros for reset envs)
-    const int r = e / H, c = e - r * H;
-    const int64_t b = row0 + r;
-    const bool live = b < p.B && !(p.reset && p.reset[b]);
-    mine[r * lda + kxp + c] = live ? p.hidden[(b * A + a) * H + c] : 0.0f;
+  {
+    static_assert(128 % H == 0 && R * H % 128 == 0, "hidden staging: whole rows per thread group");
+    constexpr int RH = R * H / 128;  // rows per thread
+    const int c = t2 % H, rh0 = (t2 / H) * RH;
+    float v[RH];
+#pragma unroll
+    for (int i = 0; i < RH; ++i) {  // hidden rows (zeros for reset envs)
+      const int64_t b = row0 + rh0 + i;
+      const bool live = b < p.B && !(p.reset && p.reset[b]);
+      v[i] = live ? p.hidden[(b * A + a) * H + c] : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < RH; ++i) mine[(rh0 + i) * lda + kxp + c] = v[i];
   }
   __syncthreads();
   const float* bi = p.b_ih + a * 3 * H;
