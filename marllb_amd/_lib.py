@@ -215,6 +215,37 @@ def load() -> ctypes.CDLL:
     return lib
 
 
+class TimingEvent:
+    """A HIP timing event created with hipEventDisableSystemFence, for bench.py's per-launch times
+    of the policy kernels (lbsim_profile_begin's events are made the same way): a default event's
+    record writes back and invalidates the caches between the launches it brackets.  Resolved
+    through liblbsim.so's own HIP runtime (the one torch shares).  Read elapsed_time only after the
+    device is synchronised."""
+
+    _DISABLE_SYSTEM_FENCE = 0x20000000
+
+    def __init__(self):
+        self._lib = load()
+        self.ev = ctypes.c_void_p()
+        if self._lib.hipEventCreateWithFlags(ctypes.byref(self.ev),
+                                             ctypes.c_uint(self._DISABLE_SYSTEM_FENCE)) != 0:
+            raise RuntimeError("hipEventCreateWithFlags failed")
+
+    def record(self, stream: int = 0) -> None:
+        if self._lib.hipEventRecord(self.ev, ctypes.c_void_p(stream or None)) != 0:
+            raise RuntimeError("hipEventRecord failed")
+
+    def elapsed_time(self, end: "TimingEvent") -> float:
+        ms = ctypes.c_float()
+        if self._lib.hipEventElapsedTime(ctypes.byref(ms), self.ev, end.ev) != 0:
+            raise RuntimeError("hipEventElapsedTime failed (events not complete?)")
+        return ms.value
+
+    def __del__(self):
+        if getattr(self, "ev", None) and self.ev.value:
+            self._lib.hipEventDestroy(self.ev)
+
+
 def launch_names(handle, which: int = 0) -> dict:
     """{profile class: kernel signature} of the last step (which=0) / reset (1) of a Handle
     (lbsim_launch_names), e.g. {0: 'dynamics_group_kernel<4, 0, 0, false, 1>', 1: ...}."""

@@ -1039,9 +1039,19 @@ int lbsim_profile_begin(lbsim_t* h, int max_launches) {
   DeviceGuard g(h->device);
   Profiler& p = h->prof;
   const size_t need = 2 * (size_t)max_launches;
+  // Timing-only events: no system-scope fence when they are recorded.  A default event's record
+  // writes back and invalidates the caches between the launches it brackets, which costs the
+  // timed step itself (the caller synchronises the device before reading the times, so nothing
+  // needs the fence).  LBSIM_PROFILE_FENCE=1 keeps the default events (A/B).
+  static const unsigned flags = [] {
+    const char* e = std::getenv("LBSIM_PROFILE_FENCE");
+    return (e != nullptr && std::strcmp(e, "1") == 0) ? (unsigned)hipEventDefault
+                                                       : (unsigned)hipEventDisableSystemFence;
+  }();
   while (p.ev.size() < need) {
     hipEvent_t e;
-    if (hipEventCreate(&e) != hipSuccess) return fail(h, LBSIM_EDEVICE, "hipEventCreate failed");
+    if (hipEventCreateWithFlags(&e, flags) != hipSuccess)
+      return fail(h, LBSIM_EDEVICE, "hipEventCreateWithFlags failed");
     p.ev.push_back(e);
   }
   p.used = 0;

@@ -216,10 +216,13 @@ def _copy_into(dst, src):
 def _timed(launch):
     if profile_events is None:
         return launch()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
+    # fence-free HIP events (_lib.TimingEvent) on the stream the policy kernel is launched on
+    from . import _lib
+    stream = torch.cuda.current_stream().cuda_stream
+    e0, e1 = _lib.TimingEvent(), _lib.TimingEvent()
+    e0.record(stream)
     rc = launch()
-    e1.record()
+    e1.record(stream)
     profile_events.append((e0, e1))
     return rc
 
