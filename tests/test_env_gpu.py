@@ -405,3 +405,28 @@ def test_profiler_counts_and_times_every_launch():
     assert list(cnt5) == [0, 0, 0, 0, 5] and ms5[4] > 0
     assert lib.lbsim_profile_end_ex(h.h, ms5, cnt5, 6) == _lib.EINVAL
     env.close()
+
+
+def test_timing_event_times_a_launch_on_torch_stream():
+    """_lib.TimingEvent (the fence-free HIP event bench.py times the policy launches with) brackets
+    work on torch's current stream: positive, below the wall time, and ordered like torch's own
+    events around the same work."""
+    import time
+    from marllb_amd import _lib
+    x = torch.randn(4096, 4096, device="cuda:0")
+    stream = torch.cuda.current_stream().cuda_stream
+    e0, e1 = _lib.TimingEvent(), _lib.TimingEvent()
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    w0 = time.perf_counter()
+    e0.record(stream)
+    t0.record()
+    for _ in range(4):
+        x = x @ x * 1e-3
+    t1.record()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    wall_ms = (time.perf_counter() - w0) * 1e3
+    ms, ref = e0.elapsed_time(e1), t0.elapsed_time(t1)
+    assert 0.0 < ms < wall_ms
+    assert ms >= 0.5 * ref  # the fence-free pair encloses torch's pair
