@@ -443,7 +443,9 @@ int lbsim_vpp_features(const float* tv, const float* ts, int64_t res_per_ts, int
  * {0: dynamics step, 1: observe step, 2: dynamics reset, 3: observe reset} the summed event time
  * in ms (ms_out[4]) and the number of timed launches (count_out[4]).  lbsim_profile_end_ex
  * returns the first n_classes (<= LBSIM_PROFILE_CLASSES) classes, class 4 being the fused step
- * kernel.  Used by bench.py.
+ * kernel.  Used by bench.py.  The events are created with hipEventDisableSystemFence (no cache
+ * writeback / invalidate between the bracketed launches; LBSIM_PROFILE_FENCE=1 restores default
+ * events): read the times only after synchronising the device, as lbsim_profile_end's callers do.
  */
 #define LBSIM_PROFILE_CLASSES 5
 /* (lbsim_profile_end reports the first 4 classes only: a handle whose steps are one launch --
