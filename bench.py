@@ -37,20 +37,22 @@ K = 128
 def algorithmic_bytes(S: int, slots_per_env: float, inflight_per_env: float, paired: bool = False):
     """Bytes each kernel must move per env-step with the state layout of DESIGN.md §4.
 
-    observe : read the 128 slot records (fct, dur, ts: 12 B each; paired -- observe_pair_kernel,
-              records whose duration word equals the fct word -- needs fct and ts only, 8 B, though
-              the 12-B records put both words in the same 64-B segments) + hc + res_count per server,
-              ep_step/ep_return read+write, obs 44 B/server, reward 4, done 1, ep outputs 12.
+    observe : read the 128 slot records ({fct, ts}: 8 B each, + the 4-B duration word of the
+              duration plane when the handle has one -- paired = no plane, observe_pair_kernel)
+              + hc + res_count per server, ep_step/ep_return read+write, obs 44 B/server,
+              reward 4, done 1, ep outputs 12.
     dynamics: env header (8 x 4 B) and per-server hc/last_tc/res_count read+write, action 8 B and
-              assign count 4 B per server, the reservoir slots actually written (12 B each,
-              slots_per_env = lbsim_step_stats' popcount of the written-slot masks, measured on
-              the timed steps), and the flows carried into the next step (8-B ring entry written
-              at the end of the step and read at the start of the next: inflight_per_env).
+              assign count 4 B per server, the reservoir slots actually written (8 B each, 12 with
+              a duration plane; slots_per_env = lbsim_step_stats' popcount of the written-slot
+              masks, measured on the timed steps), and the flows carried into the next step (8-B
+              ring entry written at the end of the step and read at the start of the next:
+              inflight_per_env).
     fused   : one launch does both, so both (the observe reads of freshly written records are
               algorithmic traffic even when L2 serves them).
     """
-    obs = S * (K * (8 if paired else 12) + 8 + 44) + 12 + 12 + 4 + 1 + 12
-    dyn = 2 * 32 + S * (2 * 12 + 8 + 4) + 12 * slots_per_env + 16 * inflight_per_env
+    rec = 8 if paired else 12
+    obs = S * (K * rec + 8 + 44) + 12 + 12 + 4 + 1 + 12
+    dyn = 2 * 32 + S * (2 * 12 + 8 + 4) + rec * slots_per_env + 16 * inflight_per_env
     return {"observe_kernel": obs, "dynamics_kernel": dyn, "fused_step_kernel": obs + dyn}
 
 
@@ -197,6 +199,7 @@ def parse():
                     help="rollout workload: the env's auto-reset mode (same_step: SB3 / gym; "
                          "next_step: gymnasium >= 1.0's NEXT_STEP, the reset inside the step "
                          "launches -- the mode the graph leg always captures)")
+    ap.add_argument("--graph-child", type=float, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--late-episode", default="",
                     help="rollout workload at N=1: after the headline measurement, keep stepping the "
                          "same envs and also time --steps steps from these episode steps (comma "
@@ -416,6 +419,31 @@ def graph_leg(args, dev, shard, B, S, common, kernel_ms):
                     "the auto-reset modes differ)"}
 
 
+def graph_leg_child(args, kernel_ms, timeout_s: float = 420.0):
+    """Runs graph_leg in a fresh child process (this script with --graph-child) and returns its
+    dict: a fault or abort inside the HIP runtime during graph capture / replay ends the child, not
+    the headline process, whose JSON line is then printed with graph = {"error": ...} (VERDICT r05
+    item 6: a runtime abort there used to lose the headline).  The child starts as a new program
+    (fork + exec of python by subprocess, no exec of this process) and initialises its own GPU
+    context; it builds the same workload from the same arguments."""
+    import subprocess
+    argv = [sys.executable, os.path.abspath(__file__)] + [a for a in sys.argv[1:]] + \
+        ["--graph-child", repr(kernel_ms), "--no-cpu-baseline", "--prewarm-ms", "0"]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK")}
+    try:
+        r = subprocess.run(argv, env=env, capture_output=True, text=True, timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return {"error": f"graph-leg child timed out after {timeout_s:.0f} s"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        tail = " | ".join(r.stderr.strip().splitlines()[-4:])
+        return {"error": f"graph-leg child exited {r.returncode}: {tail}"}
+    res = json.loads(lines[-1])
+    res["process"] = "child (fresh process and GPU context; the headline process never captures)"
+    return res
+
+
 def late_episode(args, env, handle, lib, one_step, rate, B, S, done_steps):
     """The same rollout later in its episodes (max_steps 10000, the reference default): every
     reservoir is full and most servers' reservoirs take no new sample in a step (Algorithm R
@@ -543,7 +571,11 @@ def main():
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # a process group whenever a launcher gave this process a rank (torchrun's contract), N = 1
+    # included: the timing barrier and the max / gather of the elapsed times then run as RCCL
+    # collectives on the GPU at every N (tests/test_dist.py::test_bench_torchrun_rccl_world1)
+    dist_on = world > 1 or ("RANK" in os.environ and args.graph_child is None)
+    if dist_on:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -558,6 +590,10 @@ def main():
                   assign_policy=args.policy, trace=tr, dyn_mapping=args.dyn_mapping)
     if args.workload == "rollout":
         common["autoreset_mode"] = args.autoreset_mode
+    if args.graph_child is not None:  # the graph leg alone, in its own process (graph_leg_child)
+        res = graph_leg(args, dev, shard, B, S, dict(common), args.graph_child)
+        print(json.dumps(res), flush=True)
+        return
     prewarm = prewarm_scratch(args, dev, B, S, common)
     torch.manual_seed(args.seed)  # network init (random weights of the reference architecture)
     if args.workload == "rollout":
@@ -607,7 +643,7 @@ def main():
     for _ in range(args.warmup):
         one_step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     lib = _lib.load()
     from marllb_amd import policies
@@ -619,7 +655,7 @@ def main():
         one_step()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     NC = _lib.PROFILE_CLASSES
     ms = (ctypes.c_double * NC)()
@@ -630,17 +666,15 @@ def main():
     elapsed = lbdist.max_over_ranks(t1 - t0, cdev)
     per_rank = lbdist.gather_over_ranks(t1 - t0, cdev)
     # the graph leg right after the timed region (before the accounting replay and everything
-    # else), so both legs run on the GPU in the same state: sustained load lowers the kernels'
-    # speed over the following seconds (profiles/r05k/)
+    # else), so both legs run on the GPU in a similar state: sustained load lowers the kernels'
+    # speed over the following seconds (profiles/r05k/).  In a child process: nothing the capture
+    # or the replays do can abort this one (graph_leg_child).
     graph_res = None
     if world == 1 and not args.no_graph:
         kms = sum(ms[i] / cnt[i] for i in (0, 1, 4) if cnt[i] > 0)
         if pol_events:
             kms += sum(a.elapsed_time(b) for a, b in pol_events) / len(pol_events)
-        try:
-            graph_res = graph_leg(args, dev, shard, B, S, common, kms)
-        except Exception as e:  # reported, never fatal to the headline line
-            graph_res = {"error": f"{type(e).__name__}: {e}"}
+        graph_res = graph_leg_child(args, kms)
 
     if rank == 0:
         value = lbdist.throughput(shard, args.steps, elapsed)
@@ -661,7 +695,7 @@ def main():
         rate = tr.rate if tr is not None else ARRIVAL_RATE
         slots, inflight = step_accounting(handle, lib, one_step, args.steps, replay)
         abytes = algorithmic_bytes(S, slots / B, inflight / B,
-                                   paired=obs_name.startswith("observe_pair"))
+                                   paired=True)  # duration "age", lost-FIN off: no plane
         abytes[obs_name] = abytes.pop("observe_kernel")
         abytes[dyn] = abytes.pop("dynamics_kernel")
         abytes[fused] = abytes.pop("fused_step_kernel")
@@ -699,7 +733,7 @@ def main():
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             # every rank's timed-region wall time (value uses the max): imbalance shows here
-            "ranks": {"world_size": world, "backend": backend if world > 1 else None,
+            "ranks": {"world_size": world, "backend": backend if dist_on else None,
                       "elapsed_s": per_rank, "elapsed_min_s": min(per_rank),
                       "elapsed_max_s": elapsed},
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32/int32 (f64 reward)",
@@ -774,7 +808,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
         print(json.dumps(out), flush=True)
     env.close()
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

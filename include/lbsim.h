@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define LBSIM_ABI_VERSION 7
+#define LBSIM_ABI_VERSION 8  /* 8: snapshot layout -- 8-B {fct, ts} records + duration plane */
 #define LBSIM_MAX_SERVERS 64   /* S <= 64: BASELINE configs[4] read literally is 4 agents x 16 */
                                /* servers = 64 (S > 16: server-per-lane dynamics only)       */
 #define LBSIM_RESERVOIR_K 128  /* reservoir.py:31 capacity=128, reservoir.h:24               */
@@ -266,7 +266,7 @@ int lbsim_episode_stats(lbsim_t* h, int32_t* length_out, double* return_out, voi
 
 /* Accounting of the last step (bench.py's algorithmic bytes; synchronises the device): HOST
  * stats_out[0] = reservoir slots the last dynamics launch wrote (popcount of the written-slot
- * masks: each a 12-B record store), stats_out[1] = flows in flight after it (sum of the queue
+ * masks: each an 8-B record store, + 4 B with a duration plane), stats_out[1] = flows in flight after it (sum of the queue
  * counts: ring entries carried into the next step). */
 int lbsim_step_stats(lbsim_t* h, int64_t* stats_out);
 
@@ -464,7 +464,10 @@ int lbsim_profile_end_ex(lbsim_t* h, double* ms_out, int64_t* count_out, int n_c
 int lbsim_launch_names(lbsim_t* h, int which, char* buf, size_t buf_len);
 
 /* Snapshot: total bytes of the device state, and copies to/from a HOST buffer of that size.
- * Layout: DESIGN.md §4 (used by the parity tests to compare every state word with oracle/). */
+ * Layout: DESIGN.md §4 (used by the parity tests to compare every state word with oracle/).  A
+ * handle whose duration samples can differ from its fct samples (duration_mode SERVICE, or
+ * lost_fin_prob > 0) keeps a duration plane and has a larger snapshot: lbsim_set_state rejects a
+ * snapshot of the other record format by its size (LBSIM_ESHAPE). */
 int lbsim_state_size(const lbsim_t* h, size_t* bytes_out);
 int lbsim_get_state(lbsim_t* h, void* host_buf, size_t bytes);
 int lbsim_set_state(lbsim_t* h, const void* host_buf, size_t bytes);

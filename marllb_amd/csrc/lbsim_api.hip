@@ -231,6 +231,11 @@ void derive_params(const lbsim_config_t& c, SimParams& p) {
   p.leak = (c.n_flow_on_mode == LBSIM_NFLOW_VPP && p.lf_thr != 0u) ? 1 : 0;
 }
 
+// Whether a handle keeps a duration plane (DevState::res_dur): duration_mode SERVICE (the service
+// time differs from the age) or lost-FIN guesses (their fct differs from the duration).  Otherwise
+// every duration sample equals its fct sample, and the duration reservoir is the fct reservoir.
+bool dur_plane(const SimParams& p) { return p.dur_service != 0 || p.lf_thr != 0u; }
+
 // State sections in snapshot order.
 struct Section {
   void** ptr;
@@ -246,7 +251,7 @@ std::vector<Section> sections(lbsim_t* h) {
       {(void**)&s.clock, B * 4},      {(void**)&s.ep_step, B * 4},   {(void**)&s.dropped, B * 4},
       {(void**)&s.norm_count, B * 4}, {(void**)&s.ep_return, B * 8}, {(void**)&s.hc, BS * 4},
       {(void**)&s.last_tc, BS * 4},   {(void**)&s.res_count, BS * 4}, {(void**)&s.ring, BSQ * 8},
-      {(void**)&s.res, BSK * 12},     {(void**)&s.chg, BS * 16},      {(void**)&s.fcache, BS * 40},
+      {(void**)&s.res, BSK * 8},      {(void**)&s.chg, BS * 16},      {(void**)&s.fcache, BS * 40},
   };
   if (h->cfg.normalize_obs) {
     v.push_back({(void**)&s.norm_mean, BS * NF * 8});
@@ -254,6 +259,8 @@ std::vector<Section> sections(lbsim_t* h) {
   }
   if (h->cfg.fail_prob > 0.0f) v.push_back({(void**)&s.down, BS * 4});
   if (h->prm.leak) v.push_back({(void**)&s.lost_on, BS * 4});
+  // the duration plane: only when a flow's duration sample can differ from its fct
+  if (dur_plane(h->prm)) v.push_back({(void**)&s.res_dur, BSK * 4});
   return v;
 }
 

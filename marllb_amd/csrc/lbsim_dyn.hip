@@ -41,6 +41,18 @@ void launch_dyn_group(const LaunchCtx& L, const void* action, int dtype, int32_t
   SimParams prm = L.prm;
   prm.dyn_epw = epw;
   const dim3 block(64), grid((unsigned)((L.B + epw - 1) / epw));
+  // the step of a next-step auto-reset handle inlines the event loop twice (the reset's warm-up
+  // and the step): unconstrained it took 133-137 VGPRs, 3 waves per SIMD, and ran 190 us against
+  // the plain step's 149 at 65536 x 4 (profiles/r06b/modes): held to the 4-wave budget
+  if constexpr (MODE == kModeStepNR) {
+    if (L.prm.trace)
+      LBSIM_LAUNCH((dynamics_group_kernel<G, MODE, POLICY, true, 4>), grid, block, 0, stream,
+                   L.st, prm, action, dtype, assign, mask);
+    else
+      LBSIM_LAUNCH((dynamics_group_kernel<G, MODE, POLICY, false, 4>), grid, block, 0, stream,
+                   L.st, prm, action, dtype, assign, mask);
+    return;
+  }
   // a step grid of more than 4 waves per SIMD: the 5-wave register budget (SED, 4 / 8 lanes)
   if constexpr (MODE == kModeStep && POLICY == 0 && (G == 4 || G == 8)) {
     if ((int64_t)grid.x > 4 * (int64_t)L.simds) {

@@ -31,6 +31,14 @@
 namespace lbk {
 
 constexpr int kGroupWL = 8;  // LDS queue window per server: 64 lanes x 8 x 8 B = 4 KiB per wave
+// 1: the entry after the queue head is read one iteration ahead (SrvLane::nt), so an iteration's
+// pop waits on no LDS round trip; 0: read at the pop (A/B)
+#ifndef LBSIM_DYN_NT_AHEAD
+#define LBSIM_DYN_NT_AHEAD 1
+#endif
+#ifndef LBSIM_DYN_KEYS_IN_BLOCK
+#define LBSIM_DYN_KEYS_IN_BLOCK 1
+#endif
 
 // Reductions over the aligned G-lane group (G <= 16: one DPP row).  Lanes read only within their
 // group, so groups that left the event loop (inactive lanes) are never read.  mov_dpp with
@@ -116,9 +124,14 @@ __device__ __forceinline__ uint64_t group_bits(uint64_t m, int gbase) {
 // The server this lane owns (fields of DESIGN.md §4, in registers).
 struct SrvLane {
   int32_t cnt, head_tc, head, lh, tail, last, assigned;
+  int32_t nt;       // t_complete of the entry after the head (valid if cnt > 1): the next pop's
+                    // new head_tc from a register, refreshed from LDS one iteration ahead
   int32_t qcap;     // Q, or 0 while the server is down (fail_prob > 0): not eligible, as full
   bool big;         // the server's sticky kHcBig flag
   uint32_t rcnt;
+  int32_t lost;     // n_flow_on_mode VPP (p.leak): the server's lost-FIN flows completed so far
+                    // (DevState::lost_on, never decremented: lbhash.h:193,214); its SED / LSQ
+                    // scores count them with the queue (node.c:395-437 read as_stat n_flow_on)
   uint32_t* chgw;   // LDS [4][64]: word w of this lane's 128-bit mask of the reservoir slots
                     // written this launch (DevState::chg), set by one ds_or per insert
   float score, scale;
@@ -163,8 +176,8 @@ template <int G, int POLICY, bool TRACE, bool FAST>
 __device__ __forceinline__ void group_event_loop(const DevState& st, const SimParams& p,
                                                  LaneState<1>& E, SrvLane& V, int s, int gbase,
                                                  int n_alias, const GroupConst& gc, int2* win,
-                                                 int32_t* atab, int4* acache, uint3* const my_res,
-                                                 int2* const my_ring, uint32_t* const my_lost) {
+                                                 int32_t* atab, int4* acache, uint2* const my_res,
+                                                 int2* const my_ring) {
   constexpr int WL = kGroupWL;
   constexpr bool two_choice = (POLICY == 1 || POLICY == 3);
   constexpr bool alias = POLICY == kPolicyAlias;
@@ -193,10 +206,15 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
       cbase = E.arr_idx + 1u;
       const uint32_t k = cbase + (uint32_t)s;
       uint32_t rk0[10], rk1[10];
+      uint32_t k0 = gc.k0, k1 = gc.k1;
+#if LBSIM_DYN_KEYS_IN_BLOCK
+      // opaque here: the compiler would hoist the 20 round keys out of the loop (20 live VGPRs)
+      asm volatile("" : "+v"(k0), "+v"(k1));
+#endif
 #pragma unroll
       for (int r = 0; r < 10; ++r) {
-        rk0[r] = gc.k0 + (uint32_t)r * 0x9E3779B9u;
-        rk1[r] = gc.k1 + (uint32_t)r * 0xBB67AE85u;
+        rk0[r] = k0 + (uint32_t)r * 0x9E3779B9u;
+        rk1[r] = k1 + (uint32_t)r * 0xBB67AE85u;
       }
       const u32x4 d = philox_rk(u32x4{k, E.gid, E.episode, kStreamArrival << 24}, rk0, rk1);
       int32_t gap;
@@ -225,6 +243,11 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
     const bool arrival_due = E.next_arr < dt;  // the same in every lane of the group
     const int32_t th = arrival_due ? E.next_arr : dt;
     const bool due = V.act && V.cnt > 0 && V.head_tc <= th;
+    if constexpr (!FAST) {  // n_flow_on_mode VPP: a popped lost-FIN flow stays in n_flow_on
+      if (p.leak && due &&
+          lf_lost(p, gc.base_ms * 1000u + gc.base_rem + (uint32_t)wslot(V.lh)->y, E.gid, E.episode))
+        V.lost += 1;
+    }
     if (due && V.cnt > WL) {  // rare: the slot the pop frees takes queue entry WL from the ring
       int pw = V.head + WL;
       pw = pw >= Q ? pw - Q : pw;
@@ -232,12 +255,21 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
       __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
     }
     const int nl = (V.lh + 1) & (WL - 1);
+#if LBSIM_DYN_NT_AHEAD
+    const int32_t nt = V.nt;  // next head (valid if cnt > 1), read an iteration ago
+#else
     const int32_t nt = wslot(nl)->x;  // next head (valid if cnt > 1)
+#endif
     V.last = due ? V.head_tc : V.last;
     V.cnt -= due ? 1 : 0;
     V.head = due ? ((V.head + 1 == Q) ? 0 : V.head + 1) : V.head;
     V.lh = due ? nl : V.lh;
     V.head_tc = due ? nt : V.head_tc;
+#if LBSIM_DYN_NT_AHEAD
+    // the entry after the new head, for the next pop: issued now, consumed at the iteration's end
+    // (V.nt below), so its LDS round trip overlaps the choice instead of preceding the pop
+    const int32_t nt_next = wslot((V.lh + 1) & (WL - 1))->x;
+#endif
     const bool more = group_bits<G>(__ballot(due && V.cnt > 0 && nt <= th), gbase) != 0ull;
     if (!arrival_due && !more) break;  // group-uniform
     const bool arr = arrival_due && !more;
@@ -245,10 +277,13 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
     // ---- the arrival: choose a server (node.c:388-441); full servers are not eligible
     const int32_t ta = E.next_arr;
     if constexpr (!alias) {
+      // the data plane's n_flow_on: the queue, plus the lost-FIN flows it never decremented
+      // (n_flow_on_mode VPP only: the general loop; V.lost = 0 otherwise)
+      const int32_t nfo = FAST ? V.cnt : V.cnt + V.lost;
       if constexpr (lsq) {
-        V.score = (float)V.cnt;
+        V.score = (float)nfo;
       } else {  // (cnt + 1) / den correctly rounded (Markstein), division for den 0 / inf / NaN
-        const double c = (double)(V.cnt + 1);
+        const double c = (double)(nfo + 1);
         const double q0 = c * V.rcp;
         double q = fma(fma(-q0, V.den, c), V.rcp, q0);
         if (!FAST && q != q) {
@@ -306,21 +341,19 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
 
     // ---- the pushed flow's Algorithm R draw is this arrival's word r (E.u3)
     const int slot = reservoir_slot_r32(V.rcnt, E.u3);
-    // n_flow_on_mode VPP: a lost-FIN flow completing in this step (only in the general loop:
-    // sim_step_group sends leak handles there, so the FAST loop carries none of this code)
-    if constexpr (!FAST) {
-      if (p.leak && ins)
-        count_lost(p, my_lost, gc.base_ms * 1000u + gc.base_rem + (uint32_t)ta, E.gid, E.episode);
-    }
     if (ins && slot >= 0) {
       const uint32_t fct = lost_fct(p, (uint32_t)(tc_a - ta),
                                     gc.base_ms * 1000u + gc.base_rem + (uint32_t)ta, E.gid, E.episode);
-      // duration (dur_sample): the age tc - ta, or the service time svc = tc - start
-      const uint32_t dur = p.dur_service ? (uint32_t)svc : (uint32_t)(tc_a - ta);
-      my_res[(uint32_t)slot] =
-          make_uint3(fct, dur, gc.base_ms + (gc.base_rem + (uint32_t)tc_a) / 1000u);
+      my_res[(uint32_t)slot] = make_uint2(fct, gc.base_ms + (gc.base_rem + (uint32_t)tc_a) / 1000u);
+      if constexpr (!FAST) {  // the duration plane (sim_step_group sends its handles here):
+        if (st.res_dur != nullptr)  // the age tc - ta, or the service time svc = tc - start
+          st.res_dur[(size_t)(my_res - st.res) + (uint32_t)slot] =
+              p.dur_service ? (uint32_t)svc : (uint32_t)(tc_a - ta);
+      }
       mark(slot);
     }
+    // the pushed flow lands right after the head: it is the next pop's new head
+    const bool nt_push = mine && V.cnt == 1;
     if (mine) {
       const int2 e = make_int2(tc_a, ta);
       if (V.cnt < WL) {
@@ -348,6 +381,11 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
     E.u2 = arr ? nu2 : E.u2;
     E.u3 = arr ? nu3 : E.u3;
     E.arr_idx += arr ? 1u : 0u;
+#if LBSIM_DYN_NT_AHEAD
+    V.nt = nt_push ? tc_a : (due ? nt_next : V.nt);
+#else
+    (void)nt_push;
+#endif
   }
 
 }
@@ -366,9 +404,8 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
   constexpr bool alias = POLICY == kPolicyAlias;
   constexpr bool lsq = (POLICY == 2 || POLICY == 3);
   const uint32_t sb = b * (uint32_t)S + (uint32_t)s;  // valid when V.act
-  uint3* const my_res = st.res + (size_t)sb * K;
+  uint2* const my_res = st.res + (size_t)sb * K;
   int2* const my_ring = st.ring + (size_t)sb * (size_t)Q;
-  uint32_t* const my_lost = st.lost_on + sb;  // used only when p.leak (lost_on allocated)
   const GroupAliasTab tab{atab, gbase};
   const int lane = gbase + s;
   int n_alias = 0;
@@ -400,7 +437,7 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
       V.rcnt = 0u;
       V.big = false;
       mark(0);  // emptied: the next observe recomputes the (zero) features
-      if (p.leak) *my_lost = 0u;
+      V.lost = 0;
     }
     V.qcap = fails ? 0 : (recovers ? Q : V.qcap);
   }
@@ -416,13 +453,13 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
       const u32x4 d = philox4x32_10(
           u32x4{rc >> 1, E.gid, E.episode, (kStreamReservoir << 24) | (uint32_t)s}, p.key0, p.key1);
       const int slot = reservoir_slot(rc, d);
-      count_lost(p, my_lost, (uint32_t)base_us + (uint32_t)eta, E.gid, E.episode);
       if (slot >= 0) {
         const uint32_t fct =
             lost_fct(p, (uint32_t)(etc - eta), (uint32_t)base_us + (uint32_t)eta, E.gid, E.episode);
         const uint32_t dur = dur_sample(p, etc, eta, eta > prev ? eta : prev);
         V.big |= big_record(fct, dur);
-        my_res[(uint32_t)slot] = make_uint3(fct, dur, base_ms + (base_rem + (uint32_t)etc) / 1000u);
+        store_record(st, (size_t)sb * K + (uint32_t)slot, fct, dur,
+                     base_ms + (base_rem + (uint32_t)etc) / 1000u);
         mark(slot);
       }
       prev = etc;
@@ -447,14 +484,15 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
   //      SED2 scores can only be NaN when some den is 0 / inf / NaN: a wave whose servers all have
   //      finite scores runs the loop without the NaN fallbacks (a wave-uniform choice).
   const GroupConst gc = group_const(p, base_ms, base_rem);
+  V.nt = wslot((V.lh + 1) & (WL - 1))->x;  // the entry after the head (group_event_loop)
   const bool finite = lsq || alias || !V.act ||
                       (fabs(V.den) >= 1e-30 && fabs(V.den) <= 1e300);  // false for NaN
-  if (__all(finite) && !p.leak)
+  if (__all(finite) && !p.leak && st.res_dur == nullptr)
     group_event_loop<G, POLICY, TRACE, true>(st, p, E, V, s, gbase, n_alias, gc, win, atab, acache, my_res,
-                                             my_ring, my_lost);
+                                             my_ring);
   else
     group_event_loop<G, POLICY, TRACE, false>(st, p, E, V, s, gbase, n_alias, gc, win, atab, acache, my_res,
-                                              my_ring, my_lost);
+                                              my_ring);
 
   // ---- rebase to the next step's start (this lane's server)
   E.next_arr -= dt;
@@ -550,7 +588,7 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
     V.rcnt = 0u;
     V.qcap = Q;  // every server is up at the episode start
     V.big = false;
-    if (p.leak && V.act) st.lost_on[sb] = 0u;  // n_flow_on_mode VPP: no lost flows yet
+    V.lost = 0;  // n_flow_on_mode VPP: no lost flows yet
 #pragma unroll
     for (int k = 0; k < G; ++k) wall[k] = 1.0f;
   };
@@ -571,8 +609,10 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
     V.rcnt = 0u;
     V.qcap = Q;
     V.big = false;
+    V.lost = 0;
     if (V.act) {
       if (st.down != nullptr && st.down[sb] != 0u) V.qcap = 0;
+      if (p.leak) V.lost = (int32_t)st.lost_on[sb];
       const uint32_t hc = st.hc[sb];
       V.head = (int)(hc & kHcHead);
       V.big = (hc & kHcBig) != 0u;
@@ -615,18 +655,19 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
     reset_out(0);
   } else {
     // kModeStepNR (next-step auto-reset): an env whose last step returned done resets in place of
-    // stepping (its action ignored; ep_step = -1 tells the observe to report the reset).  Two call
-    // sites (113 VGPRs; one loop over both took 130, 3 waves per SIMD); a wave runs the branches
-    // of its groups one after the other, each with only its groups active.
-    if (st.ep_step[b] >= p.max_steps) {
-      reset_in();
-      for (int k = 0; k < p.warmup_steps; ++k)
-        sim_step_group<G, POLICY, TRACE>(st, p, E, V, b, s, gbase, 1.0f, wall, win, atab, acache);
-      reset_out(-1);
-    } else {
-      load_in();
-      sim_step_group<G, POLICY, TRACE>(st, p, E, V, b, s, gbase, w_own, wall, win, atab, acache);
-    }
+    // stepping (its action ignored; ep_step = -1 tells the observe to report the reset).  One call
+    // site, run warmup_steps times for a resetting group and once for the others (a wave with no
+    // resetting group runs the plain step; one with some runs the longest trip, the others masked
+    // off).  Two call sites, one per branch, took 133-137 VGPRs with scratch (3 waves per SIMD,
+    // 190 us against the plain step's 149 at 65536 x 4, profiles/r06b/modes).
+    const bool rs = st.ep_step[b] >= p.max_steps;
+    if (rs) reset_in();
+    else load_in();
+    const int nsteps = rs ? p.warmup_steps : 1;
+    const float w = rs ? 1.0f : w_own;
+    for (int k = 0; k < nsteps; ++k)
+      sim_step_group<G, POLICY, TRACE>(st, p, E, V, b, s, gbase, w, wall, win, atab, acache);
+    if (rs) reset_out(-1);
   }
 
   // ---- this lane's server back to HBM (window into the ring), then the env words (lane 0)
@@ -642,12 +683,13 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
       const uint32_t cw[4] = {chgw[lane], chgw[64 + lane], chgw[128 + lane], chgw[192 + lane]};
       __builtin_amdgcn_s_waitcnt(0);  // the wave's stores acknowledged by L2 (vmcnt 0)
       __asm__ volatile("" ::: "memory");
-      V.big |= big_written(st.res + (size_t)sb * K, cw, V.rcnt);
+      V.big |= big_written(st, sb, cw, V.rcnt);
     }
     st.hc[sb] = (uint32_t)V.head | (V.big ? kHcBig : 0u) | ((uint32_t)V.cnt << 16);
     st.last_tc[sb] = V.last;
     st.res_count[sb] = V.rcnt;
     if (st.down != nullptr) st.down[sb] = V.qcap == 0 ? 1u : 0u;
+    if (p.leak) st.lost_on[sb] = (uint32_t)V.lost;
     *reinterpret_cast<uint4*>(st.chg + (size_t)sb * 4) =
         make_uint4(chgw[lane], chgw[64 + lane], chgw[128 + lane], chgw[192 + lane]);
     if (MODE != kModeReset && assign_out != nullptr) assign_out[sb] = V.assigned;  // 0 if reset

@@ -162,7 +162,8 @@ __device__ __forceinline__ int32_t wave_count(const uint64_t (&live)[NG], int la
 // arrival order (reservoir.py:64-85 with the arrival's draw word, reservoir_slot_r32).
 __device__ __forceinline__ void wave_flush(const SimParams& p, WaveSrv& V, WaveEnv& E,
                                            const WaveBatch& Bt, int nproc, int lane,
-                                           uint3* const res_b, WaveLds& Ld, uint32_t seq,
+                                           uint2* const res_b, uint32_t* const dur_b, WaveLds& Ld,
+                                           uint32_t seq,
                                            uint32_t base_ms, uint32_t base_rem) {
   const int S = p.S;
   const int32_t dt = p.dt_us;
@@ -202,9 +203,9 @@ __device__ __forceinline__ void wave_flush(const SimParams& p, WaveSrv& V, WaveE
     svc = svc < 1 ? 1 : svc;
     const uint32_t fct = lost_fct(p, (uint32_t)(Bt.ltc - Bt.ta),
                                   base_ms * 1000u + base_rem + (uint32_t)Bt.ta, E.gid, E.episode);
-    // duration (dur_sample): the age ltc - ta, or the service time svc = ltc - start
-    const uint32_t dur = p.dur_service ? (uint32_t)svc : (uint32_t)(Bt.ltc - Bt.ta);
-    res_b[key] = make_uint3(fct, dur, base_ms + (base_rem + (uint32_t)Bt.ltc) / 1000u);
+    res_b[key] = make_uint2(fct, base_ms + (base_rem + (uint32_t)Bt.ltc) / 1000u);
+    // the duration plane (dur_sample): the age ltc - ta, or the service time svc = ltc - start
+    if (dur_b != nullptr) dur_b[key] = p.dur_service ? (uint32_t)svc : (uint32_t)(Bt.ltc - Bt.ta);
   }
 }
 
@@ -218,7 +219,8 @@ __device__ __forceinline__ void wave_flush(const SimParams& p, WaveSrv& V, WaveE
 template <int NG, int POLICY, bool TRACE, bool FAST, bool VC>
 __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimParams& p,
                                                 WaveEnv& E, WaveSrv& V, WaveRing<NG>& R,
-                                                int lane, uint3* const res_b, WaveLds& Ld,
+                                                int lane, uint2* const res_b,
+                                                uint32_t* const dur_b, WaveLds& Ld,
                                                 uint32_t& seq, uint32_t base_ms,
                                                 uint32_t base_rem) {
   constexpr bool two_choice = (POLICY == 1 || POLICY == 3);
@@ -401,7 +403,7 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
       wave_sync();
       seq = 1u;
     }
-    wave_flush(p, V, E, Bt, bi, lane, res_b, Ld, seq++, base_ms, base_rem);
+    wave_flush(p, V, E, Bt, bi, lane, res_b, dur_b, Ld, seq++, base_ms, base_rem);
     ta = rdl(Bt.ta, bi);
     if (ta >= dt) break;
     base += 63u;
@@ -420,7 +422,8 @@ __device__ __forceinline__ void wave_event_loop(const DevState& st, const SimPar
 template <int NG, int POLICY, bool TRACE, bool VC>
 __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParams& p, WaveEnv& E,
                                               WaveSrv& V, WaveRing<NG>& R, int lane,
-                                              uint3* const res_b, WaveLds& Ld, uint32_t& seq,
+                                              uint2* const res_b, uint32_t* const dur_b,
+                                              WaveLds& Ld, uint32_t& seq,
                                               float w_own) {
   constexpr bool lsq = (POLICY == 2 || POLICY == 3);
   const int S = p.S, Q = p.Q;
@@ -461,7 +464,8 @@ __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParam
         const uint32_t dur = dur_sample(p, e.x, e.y, e.y > prev ? e.y : prev);
         if (big_record(fct, dur)) Ld.big[lane] = 1u;  // this lane's own server
         res_b[(uint32_t)lane * K + (uint32_t)slot] =
-            make_uint3(fct, dur, base_ms + (base_rem + (uint32_t)e.x) / 1000u);
+            make_uint2(fct, base_ms + (base_rem + (uint32_t)e.x) / 1000u);
+        if (dur_b != nullptr) dur_b[(uint32_t)lane * K + (uint32_t)slot] = dur;
         atomicOr(Ld.chg + ((uint32_t)slot >> 5) * kWaveMaxS + (uint32_t)lane, 1u << (slot & 31));
       }
       prev = e.x;
@@ -475,10 +479,10 @@ __device__ __forceinline__ void sim_step_wave(const DevState& st, const SimParam
   // ---- 2. the arrivals (SED / SED2 scores are finite unless some den is 0 / inf / NaN)
   const bool finite = lsq || !V.act || (fabs(V.den) >= 1e-30 && fabs(V.den) <= 1e300);
   if (__all(finite))
-    wave_event_loop<NG, POLICY, TRACE, true, VC>(st, p, E, V, R, lane, res_b, Ld, seq, base_ms,
+    wave_event_loop<NG, POLICY, TRACE, true, VC>(st, p, E, V, R, lane, res_b, dur_b, Ld, seq, base_ms,
                                              base_rem);
   else
-    wave_event_loop<NG, POLICY, TRACE, false, VC>(st, p, E, V, R, lane, res_b, Ld, seq, base_ms,
+    wave_event_loop<NG, POLICY, TRACE, false, VC>(st, p, E, V, R, lane, res_b, dur_b, Ld, seq, base_ms,
                                               base_rem);
 
   // ---- 3. completions up to dt; the server's count, head and last completion
@@ -526,7 +530,8 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
   if (MODE == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return false;
   const int S = p.S, Q = p.Q;
   const int rpos = lane & 31;
-  uint3* const res_b = st.res + (size_t)b * (size_t)S * K;
+  uint2* const res_b = st.res + (size_t)b * (size_t)S * K;
+  uint32_t* const dur_b = st.res_dur != nullptr ? st.res_dur + (size_t)b * (size_t)S * K : nullptr;
 
   WaveEnv E;
   E.gid = p.env_id_offset + b;
@@ -643,12 +648,12 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
   if constexpr (MODE == kModeStep) {
     load_in();
     wave_sync();
-    sim_step_wave<NG, POLICY, TRACE, VC>(st, p, E, V, R, lane, res_b, Ld, seq, w_own);
+    sim_step_wave<NG, POLICY, TRACE, VC>(st, p, E, V, R, lane, res_b, dur_b, Ld, seq, w_own);
   } else if constexpr (MODE == kModeReset) {
     reset_in();
     wave_sync();
     for (int k = 0; k < p.warmup_steps; ++k)
-      sim_step_wave<NG, POLICY, TRACE, VC>(st, p, E, V, R, lane, res_b, Ld, seq, 1.0f);
+      sim_step_wave<NG, POLICY, TRACE, VC>(st, p, E, V, R, lane, res_b, dur_b, Ld, seq, 1.0f);
     reset_out(0);
   } else {  // kModeStepNR: an env done last step resets in place of stepping (ep_step = -1)
     const bool rs = st.ep_step[b] >= p.max_steps;
@@ -661,7 +666,7 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
     }
     wave_sync();
     for (int k = 0; k < nsim; ++k)
-      sim_step_wave<NG, POLICY, TRACE, VC>(st, p, E, V, R, lane, res_b, Ld, seq, w_own);
+      sim_step_wave<NG, POLICY, TRACE, VC>(st, p, E, V, R, lane, res_b, dur_b, Ld, seq, w_own);
     if (rs) reset_out(-1);
   }
 
@@ -683,7 +688,7 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
                               Ld.chg[3 * kWaveMaxS + lane]};
       __builtin_amdgcn_s_waitcnt(0);  // the wave's stores acknowledged by L2 (vmcnt 0)
       __asm__ volatile("" ::: "memory");
-      big |= big_written(st.res + (size_t)sb * K, cw, V.rcnt);
+      big |= big_written(st, sb, cw, V.rcnt);
     }
     st.hc[sb] = (uint32_t)head | (big ? kHcBig : 0u) | ((uint32_t)V.cnt0 << 16);
     st.last_tc[sb] = V.last;

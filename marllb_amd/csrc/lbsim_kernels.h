@@ -57,8 +57,12 @@ struct DevState {
   int2* ring;
   // reservoirs [B*S*K]; flow completion time / duration samples in integer microseconds (the
   // feature value of a sample is (float)us * 1e-6f seconds, us_to_seconds)
-  uint3* res;           // [B*S*K] slot records {fct us, duration us, timestamp ms}: an insert is
-                        // one 12-B store (one partial line, not three), observe reads dwordx3
+  uint2* res;           // [B*S*K] slot records {fct us, timestamp ms}: an insert is one 8-B store
+                        // (global_store_dwordx2), a server's 128 records are 1 KiB
+  // [B*S*K] duration us of each slot, only when a record's duration can differ from its fct
+  // (duration_mode SERVICE, or lost-FIN guesses); nullptr otherwise: the duration reservoir IS
+  // the fct reservoir (paired records), and observe reads 8 B per slot
+  uint32_t* res_dur;
   // unchanged-reservoir skip of observe: chg[(b*S + s)*4 + w] bit i set if slot
   // 32 w + i of server s was written by the last dynamics launch (its two reservoirs share every
   // replacement decision); fcache[(b*S + s)*10 + f] = the server's 10 reservoir features at the
@@ -146,9 +150,12 @@ __device__ __forceinline__ bool big_record(uint32_t fct, uint32_t dur) {
 // (SimParams::big_in_step: dt >= kPackLimit us, or lost-FIN guesses), by one scan of the slots
 // the launch wrote (below the count) at its end -- nothing in the event loop.  oracle: the same.
 // The record words are read device-coherent: in the wave kernel other lanes stored them.
-__device__ __forceinline__ bool big_written(const uint3* res_s, const uint32_t (&chg)[4],
-                                            uint32_t count) {
+// sb: the (env, server) row; its duration words from the duration plane when the handle has one.
+__device__ __forceinline__ bool big_written(const DevState& st, size_t sb,
+                                            const uint32_t (&chg)[4], uint32_t count) {
   const uint32_t n = count < (uint32_t)K ? count : (uint32_t)K;
+  const uint32_t* fs = reinterpret_cast<const uint32_t*>(st.res + sb * K);
+  const uint32_t* ds = st.res_dur != nullptr ? st.res_dur + sb * K : nullptr;
   bool big = false;
   for (int w = 0; w < 4; ++w) {
     uint32_t m = chg[w];
@@ -156,13 +163,21 @@ __device__ __forceinline__ bool big_written(const uint3* res_s, const uint32_t (
       const uint32_t slot = 32u * (uint32_t)w + (uint32_t)__builtin_ctz(m);
       m &= m - 1u;
       if (slot >= n) continue;
-      const uint32_t* r = reinterpret_cast<const uint32_t*>(res_s + slot);
-      const uint32_t f = __hip_atomic_load(r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t d = __hip_atomic_load(r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t f = __hip_atomic_load(fs + 2 * slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t d = ds != nullptr ? __hip_atomic_load(ds + slot, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT) : f;
       big |= big_record(f, d);
     }
   }
   return big;
+}
+
+// A reservoir insert: the {fct, ts} record (one dwordx2 store) and, when the handle has a duration
+// plane, the duration word.  idx = (env, server) row * K + slot.
+__device__ __forceinline__ void store_record(const DevState& st, size_t idx, uint32_t fct,
+                                             uint32_t dur, uint32_t ts_ms) {
+  st.res[idx] = make_uint2(fct, ts_ms);
+  if (st.res_dur != nullptr) st.res_dur[idx] = dur;
 }
 
 // murmur3's 32-bit finaliser (fmix32): the lost-FIN hash.
@@ -224,13 +239,12 @@ __device__ __forceinline__ bool lf_lost(const SimParams& p, uint32_t abs_ta, uin
   return (lf_mix(abs_ta ^ salt) >> 8) < p.lf_thr;
 }
 
-// n_flow_on_mode VPP (p.leak, a uniform branch): a completing flow that is lost-FIN adds one to
-// its server's lost_on count (a device atomic: every completion point of every kernel counts,
-// whether or not Algorithm R keeps its sample; the count is order-free).
-__device__ __forceinline__ void count_lost(const SimParams& p, uint32_t* ctr, uint32_t abs_ta,
-                                           uint32_t gid, uint32_t episode) {
-  if (p.leak && lf_lost(p, abs_ta, gid, episode)) atomicAdd(ctr, 1u);
-}
+// n_flow_on_mode VPP (p.leak): a lost-FIN flow adds one to its server's lost_on count when it is
+// popped (its completion), whether or not Algorithm R keeps its sample, so that from then on the
+// server's n_flow_on -- the observation's column 0 and the SED / LSQ scores of the arrivals after
+// it -- keeps it (lbhash.h:193,214 never decrement it; node.c:395-437 score on it).  The kernels
+// keep the count in registers during the event loop (the general loop: leak handles never run the
+// FAST one) and store it at the end; oracle: pop_until, score_of.
 
 // Observation column 0: the server's flows in flight, plus its lost-FIN flows under n_flow_on_mode
 // VPP (read device-coherent: the one-launch forms observe right after their own dynamics).
@@ -639,7 +653,7 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
                                            LaneState<MAXS>& L, const Lds& l,
                                            const EvConst<MAXS>& ec, const double (&den)[MAXS],
                                            const double (&rcp)[MAXS], int n_alias,
-                                           uint3* const my_res, int2* const my_ring) {
+                                           uint2* const my_res, int2* const my_ring) {
   constexpr int WL = LaneState<MAXS>::WL;
   constexpr bool REGF = MAXS <= 8;
   constexpr bool two_choice = (POLICY == 1 || POLICY == 3);
@@ -667,6 +681,19 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
       asg[s] = 0;
     }
   }
+  // n_flow_on_mode VPP (p.leak, the general loop only): each server's lost-FIN flows completed so
+  // far (DevState::lost_on), counted at their pop and added to the queue count in the SED / LSQ
+  // scores (node.c:395-437 read as_stat n_flow_on, never decremented for them: lbhash.h:193,214)
+  const size_t row0 = (size_t)(my_res - st.res) / K;  // the env's first (env, server) row
+  int32_t lost[MAXS];
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) lost[s] = 0;
+  if constexpr (!FAST) {
+    if (p.leak) {
+#pragma unroll
+      for (int s = 0; s < MAXS; ++s) lost[s] = s < S ? (int32_t)st.lost_on[row0 + (size_t)s] : 0;
+    }
+  }
   for (;;) {
     const bool arrival_due = L.next_arr < dt;
     const int32_t th = arrival_due ? L.next_arr : dt;  // a completion at the arrival time goes first
@@ -678,6 +705,16 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
       nt[s] = qslot<MAXS>(l, s, (hs[s] + 1) & (WL - 1))->x;  // next head (valid if cnt > 1)
       due[s] = (s < S) & (L.cnt[s] > 0) & (L.head_tc[s] <= th);
       refill |= due[s] & (L.cnt[s] - 1 >= WL);
+    }
+    if constexpr (!FAST) {  // a popped lost-FIN flow stays in n_flow_on (before the refill below
+      if (p.leak) {         // overwrites the head's window slot)
+#pragma unroll
+        for (int s = 0; s < MAXS; ++s)
+          if (due[s] && lf_lost(p, ec.base_ms * 1000u + ec.base_rem +
+                                       (uint32_t)qslot<MAXS>(l, s, hs[s] & (WL - 1))->y,
+                                L.gid, L.episode))
+            lost[s] += 1;
+      }
     }
     if (refill) {  // rare: bring queue entry WL (ring) into the slot the pop frees
 #pragma unroll
@@ -708,9 +745,9 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
 #pragma unroll
       for (int s = 0; s < MAXS; ++s) {
         if constexpr (lsq) {
-          score[s] = (float)L.cnt[s];
+          score[s] = (float)(L.cnt[s] + lost[s]);
         } else {  // (cnt + 1) / den correctly rounded by Markstein's corrected quotient
-          const double c = (double)(L.cnt[s] + 1);
+          const double c = (double)(L.cnt[s] + lost[s] + 1);
           const double q0 = c * rcp[s];
           const double q = fma(fma(-q0, den[s], c), rcp[s], q0);
           if constexpr (!FAST) bad |= q != q;
@@ -721,7 +758,7 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
 #pragma unroll
         for (int s = 0; s < MAXS; ++s) {
           const float q = score[s];
-          if (q != q) score[s] = (float)((double)(L.cnt[s] + 1) / den[s]);
+          if (q != q) score[s] = (float)((double)(L.cnt[s] + lost[s] + 1) / den[s]);
         }
       }
     }
@@ -806,16 +843,15 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
     const u32x4 d = philox_rk(u32x4{L.arr_idx + 1u, L.gid, L.episode, kStreamArrival << 24},
                               ec.rk0, ec.rk1);
     const int slot = reservoir_slot_r32(cres, L.u3);
-    if constexpr (!FAST) {  // n_flow_on_mode VPP (sim_step sends leak handles to this loop)
-      if (p.leak && ins)  // this env's lost_on row: its reservoirs' row (my_res) over K
-        count_lost(p, st.lost_on + (size_t)(my_res - st.res) / K + (size_t)cs,
-                   ec.base_ms * 1000u + ec.base_rem + (uint32_t)ta, L.gid, L.episode);
-    }
     if (ins && slot >= 0) {
       const uint32_t fct = lost_fct(p, (uint32_t)(tc_a - ta),
                                     ec.base_ms * 1000u + ec.base_rem + (uint32_t)ta, L.gid, L.episode);
-      my_res[(uint32_t)cs * (uint32_t)K + (uint32_t)slot] = make_uint3(
-          fct, dur_sample(p, tc_a, ta, start_a), ec.base_ms + (ec.base_rem + (uint32_t)tc_a) / 1000u);
+      const uint32_t ri = (uint32_t)cs * (uint32_t)K + (uint32_t)slot;
+      my_res[ri] = make_uint2(fct, ec.base_ms + (ec.base_rem + (uint32_t)tc_a) / 1000u);
+      if constexpr (!FAST) {  // the duration plane (sim_step sends its handles to this loop)
+        if (st.res_dur != nullptr)
+          st.res_dur[(size_t)(my_res - st.res) + ri] = dur_sample(p, tc_a, ta, start_a);
+      }
       mark_slot<MAXS>(l, cs, slot);
     }
     // queue index < WL: the LDS window (a push that does not happen writes the lane's scratch
@@ -880,6 +916,13 @@ __device__ __forceinline__ void event_loop(const DevState& st, const SimParams& 
     L.head[s] = (int32_t)((uint32_t)(rbase[s] + hs[s]) % (uint32_t)Q);
     L.lh[s] = hs[s] & (WL - 1);
   }
+  if constexpr (!FAST) {
+    if (p.leak) {
+#pragma unroll
+      for (int s = 0; s < MAXS; ++s)
+        if (s < S) st.lost_on[row0 + (size_t)s] = (uint32_t)lost[s];
+    }
+  }
   if constexpr (REGF) {
 #pragma unroll
     for (int s = 0; s < MAXS; ++s) {
@@ -925,7 +968,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
   constexpr bool lsq = (POLICY == 2 || POLICY == 3);
   const uint32_t b0 = b * (uint32_t)S;
   // this env's reservoirs and rings as per-lane (VGPR) pointers: no kernarg reload in the loop
-  uint3* const my_res = st.res + (size_t)b0 * K;
+  uint2* const my_res = st.res + (size_t)b0 * K;
   int2* const my_ring = st.ring + (size_t)b0 * (size_t)Q;
   int n_alias = 0;
   double den[MAXS], rcp[MAXS];
@@ -992,15 +1035,13 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
         const u32x4 d = philox4x32_10(
             u32x4{rc >> 1, L.gid, L.episode, (kStreamReservoir << 24) | (uint32_t)s}, p.key0, p.key1);
         const int slot = reservoir_slot(rc, d);
-        count_lost(p, st.lost_on + b0 + (uint32_t)s, (uint32_t)base_us + (uint32_t)eta, L.gid,
-                   L.episode);
         if (slot >= 0) {
           const uint32_t fct =
               lost_fct(p, (uint32_t)(etc - eta), (uint32_t)base_us + (uint32_t)eta, L.gid, L.episode);
           const uint32_t dur = dur_sample(p, etc, eta, eta > prev ? eta : prev);
           L.bigm |= big_record(fct, dur) ? 1u << s : 0u;
-          my_res[(uint32_t)s * (uint32_t)K + (uint32_t)slot] =
-              make_uint3(fct, dur, base_ms + (base_rem + (uint32_t)etc) / 1000u);
+          store_record(st, (size_t)(b0 + (uint32_t)s) * K + (size_t)slot, fct, dur,
+                       base_ms + (base_rem + (uint32_t)etc) / 1000u);
           mark_slot<MAXS>(l, s, slot);
         }
         prev = etc;
@@ -1028,7 +1069,7 @@ __device__ __forceinline__ void sim_step(const DevState& st, const SimParams& p,
   //      SED/SED2 scores can only be NaN when some den is 0 / inf / NaN: a wave whose envs all
   //      have finite scores runs the loop without the NaN fallbacks (a wave-uniform choice).
   const EvConst<MAXS> ec = ev_const<MAXS>(p, base_ms, base_rem);
-  if ((lsq || alias || __all(finite_scores)) && !p.leak)
+  if ((lsq || alias || __all(finite_scores)) && !p.leak && st.res_dur == nullptr)
     event_loop<MAXS, POLICY, TRACE, true>(st, p, L, l, ec, den, rcp, n_alias, my_res, my_ring);
   else
     event_loop<MAXS, POLICY, TRACE, false>(st, p, L, l, ec, den, rcp, n_alias, my_res, my_ring);
@@ -1090,7 +1131,7 @@ __device__ __forceinline__ void store_servers(const DevState& st, const SimParam
                                 l.m[(s * 4 + 2) * 64 + l.lane], l.m[(s * 4 + 3) * 64 + l.lane]};
         __builtin_amdgcn_s_waitcnt(0);  // the wave's stores acknowledged by L2 (vmcnt 0)
         __asm__ volatile("" ::: "memory");
-        big |= big_written(st.res + (size_t)sb * K, cw, (uint32_t)fld<MAXS>(l, F_RCNT, s));
+        big |= big_written(st, sb, cw, (uint32_t)fld<MAXS>(l, F_RCNT, s));
       }
       st.hc[sb] = (uint32_t)head | (big ? kHcBig : 0u) | ((uint32_t)L.cnt[s] << 16);
       st.last_tc[sb] = L.last[s];
@@ -1502,17 +1543,21 @@ __device__ __forceinline__ void observe_chunk_regs(const DevState& st, const Sim
   const size_t sb = srow + (size_t)(act ? u : 0);
   const int n = FULL ? K : n_in;  // this group's sample count
   const int m8 = FULL ? K : n - (n & 7);
-  // values of reservoir r (the 12-B record is {fct, duration, ts}); timestamps of the half of the
-  // slots whose weights this group computes, 8 (q + 8 r) + j -- the pair's other group reads the
-  // other half, and the newest timestamp is a max over the 16 lanes of the pair
+  // values of reservoir r (the 8-B record is {fct, ts}; the duration reservoir is the duration
+  // plane when the handle has one, else the fct words again); timestamps of the half of the slots
+  // whose weights this group computes, 8 (q + 8 r) + j -- the pair's other group reads the other
+  // half, and the newest timestamp is a max over the 16 lanes of the pair
   const uint32_t* rec = reinterpret_cast<const uint32_t*>(st.res + sb * K + (size_t)j);
+  const bool dplane = r == 1 && st.res_dur != nullptr;
+  const uint32_t* vb = dplane ? st.res_dur + sb * K + (size_t)j : rec;
+  const uint32_t vstep = dplane ? 8u : 16u;
   uint32_t key[16], th[8];
 #pragma unroll
-  for (int e = 0; e < 16; ++e) key[e] = rec[24 * e + r];
-  const uint32_t* rts = rec + 2 + 192 * r;
+  for (int e = 0; e < 16; ++e) key[e] = vb[vstep * (uint32_t)e];
+  const uint32_t* rts = rec + 1 + 128 * r;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    th[q] = rts[24 * q];
+    th[q] = rts[16 * q];
     if constexpr (!FULL) th[q] = 8 * (q + 8 * r) + j < n ? th[q] : 0u;  // empty slots: stale words
   }
   uint32_t tmax = 0;
@@ -1776,11 +1821,11 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
       for (int h = 0; h < 2; ++h) {
         const int slot = lane + 64 * h;
         const bool v = slot < nn[u];
-        if constexpr (US) {  // simulator: one 12-B record per slot
-          const uint3 rec = v ? st.res[sb * K + slot] : make_uint3(0u, 0u, 0u);
+        if constexpr (US) {  // simulator: one 8-B record per slot (+ the duration plane)
+          const uint2 rec = v ? st.res[sb * K + slot] : make_uint2(0u, 0u);
           f[u][h] = rec.x;
-          d[u][h] = rec.y;
-          t[u][h] = rec.z;
+          d[u][h] = (v && st.res_dur != nullptr) ? st.res_dur[sb * K + slot] : rec.x;
+          t[u][h] = rec.y;
         } else {  // features API: one value array serves as both "fct" and "duration"
           f[u][h] = v ? st.feat_vals[sb * K + slot] : 0u;
           d[u][h] = f[u][h];
@@ -2109,13 +2154,13 @@ __device__ double reward_of(const float* obs, int S, int metric, int field) {
 // ================================================================ paired observe (8 rows per wave)
 //
 // With the default duration sample (duration_mode AGE: both samples of a flow are tc - ta,
-// DESIGN.md §3.4) and lost-FIN off, every record the dynamics write holds dur == fct, so a
-// server's duration reservoir equals its fct reservoir slot for slot (same values, timestamps and
-// count) and its 5 duration features equal its 5 fct features bit for bit.  observe_pair_kernel
-// then computes each server's features once: one wave takes up to 8 consecutive (env, server)
-// rows -- the 8 / S whole envs of S <= 8 servers -- and lane (u, j) holds slots 8 e + j of row u
-// (the fct word and the timestamp of each record), so a wave does the work observe_kernel
-// spreads over two.  step_wave_kernel's S = 5-8 observe phase takes the same path for its env.
+// DESIGN.md §3.4) and lost-FIN off, every flow's duration equals its fct, so the handle has no
+// duration plane (DevState::res_dur == nullptr): a server's duration reservoir IS its fct
+// reservoir slot for slot (same values, timestamps and count) and its 5 duration features equal
+// its 5 fct features bit for bit.  observe_pair_kernel then computes each server's features
+// once: one wave takes up to 8 consecutive (env, server) rows -- the 8 / S whole envs of S <= 8
+// servers -- and lane (u, j) holds slots 8 e + j of row u (one 8-B {fct, ts} record each: a
+// server's reservoir is 1 KiB), so a wave does the work observe_kernel spreads over two.  step_wave_kernel's S = 5-8 observe phase takes the same path for its env.
 // Same operations in the same order as observe_chunk_regs' fct group: the same bits.
 
 // (uint64_t)(w * 2^48) for w in [0, 1], from the f32 weight: hi = floor(x / 2^32), lo = the
@@ -2138,13 +2183,14 @@ __device__ __forceinline__ void observe_rows_paired_regs(const DevState& st, con
   const size_t sb = row0 + (size_t)(act ? u : 0);
   const int n = FULL ? K : n_in;  // this row's sample count
   const int m8 = FULL ? K : n - (n & 7);
-  // the fct word and the timestamp of slots 8 e + j (the 12-B record is {fct, duration, ts})
-  const uint32_t* rec = reinterpret_cast<const uint32_t*>(st.res + sb * K + (size_t)j);
+  // the record {fct, ts} of slots 8 e + j: one dwordx2 each, 8 lanes = 64 contiguous bytes
+  const uint2* rec = st.res + sb * K + (size_t)j;
   uint32_t key[16], th[16];
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
-    key[e] = rec[24 * e];
-    th[e] = rec[24 * e + 2];
+    const uint2 r2 = rec[8 * e];
+    key[e] = r2.x;
+    th[e] = r2.y;
     if constexpr (!FULL) th[e] = 8 * e + j < n ? th[e] : 0u;  // empty slots: stale words
   }
   uint32_t tmax = 0;
@@ -2650,7 +2696,7 @@ __device__ __forceinline__ void observe_env_wave(const DevState& st, const SimPa
   const bool fresh = p.next_reset && st.ep_step[b] < 0;
   if constexpr (MAXS <= kObsChunk) {  // one chunk: straight-line code, no loop-carried s0
     observe_chunk<true, true>(st, p, b, 0, S, sc, s_obs, lane, fresh);
-  } else if (LBSIM_STEP_WAVE_PAIRED && MAXS <= 8 && p.dur_service == 0 && p.lf_thr == 0u) {
+  } else if (LBSIM_STEP_WAVE_PAIRED && MAXS <= 8 && st.res_dur == nullptr) {
     // paired records: the env's S <= 8 rows in one pass (observe_rows_paired)
     observe_rows_paired<true>(st, p, b, 1, sc, s_obs, lane, p.next_reset != 0);
   } else {

@@ -59,8 +59,8 @@ void launch_observe_split(const LaunchCtx& L, const ObsOutputs& o, const uint8_t
     LBSIM_LAUNCH((observe_rows_kernel<64, MODE, FAC>), grid, block, 0, stream, L.st, L.prm, o, mask);
 }
 
-// The paired step observe (observe_pair_kernel): records whose duration word equals the fct word
-// by construction (duration_mode AGE, lost-FIN off) and S <= 8 (8 / S whole envs per wave), or S a
+// The paired step observe (observe_pair_kernel): no duration plane (duration == fct by
+// construction: duration_mode AGE, lost-FIN off) and S <= 8 (8 / S whole envs per wave), or S a
 // multiple of 8 (S / 8 waves per env: observe_pair16_kernel, observe_pair_chunks_kernel).  LBSIM_OBSERVE_PAIRED=0
 // turns it off (A/B; the same bits either way).
 bool observe_paired(const LaunchCtx& L) {
@@ -68,8 +68,7 @@ bool observe_paired(const LaunchCtx& L) {
     const char* e = std::getenv("LBSIM_OBSERVE_PAIRED");
     return !(e != nullptr && std::strcmp(e, "0") == 0);
   }();
-  return on && L.prm.dur_service == 0 && L.prm.lf_thr == 0u &&
-         (L.S <= 8 || L.S % 8 == 0);
+  return on && L.st.res_dur == nullptr && (L.S <= 8 || L.S % 8 == 0);
 }
 
 // the problem-05 facade rows (agent_obs / state) come from their own instantiation

@@ -122,10 +122,10 @@ __global__ void __launch_bounds__(64)
     const int i = lane + 64 * h;
     float t = 0.0f, fv = 0.0f, dv = 0.0f;
     if (i < cnt) {
-      const uint3 rec = st.res[sb * K + (size_t)i];
-      t = (float)((double)rec.z * 1e-3);
+      const uint2 rec = st.res[sb * K + (size_t)i];
+      t = (float)((double)rec.y * 1e-3);
       fv = sample_value<true>(rec.x);
-      dv = sample_value<true>(rec.y);
+      dv = st.res_dur != nullptr ? sample_value<true>(st.res_dur[sb * K + (size_t)i]) : fv;
     }
     tv_out[(pair * 2 + 0) * kVppN + i] = make_float2(t, fv);
     tv_out[(pair * 2 + 1) * kVppN + i] = make_float2(t, dv);

@@ -37,7 +37,7 @@ def max_over_ranks(x: float, device=None) -> float:
     """Max of a per-rank scalar (the bench's elapsed time) over the default process group."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return float(x)
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -49,7 +49,7 @@ def gather_over_ranks(x: float, device=None) -> list:
     elapsed times beside their max, so an imbalanced rank shows in the line)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return [float(x)]
     n = dist.get_world_size()
     t = torch.zeros(n, dtype=torch.float64, device=device)

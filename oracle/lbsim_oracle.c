@@ -313,9 +313,12 @@ typedef struct oracle {
   double* ep_return;
   uint32_t* hc; int32_t* last_tc; uint32_t* res_count;
   int32_t* ring; /* [B*S*Q][2] = {t_complete, t_arrival} */
-  /* reservoir slot records [B*S*K][3] = {fct us, duration us, timestamp ms}; the feature value
-   * of a sample is (float)us * 1e-6f */
+  /* reservoir slot records [B*S*K][2] = {fct us, timestamp ms}; the feature value of a sample is
+   * (float)us * 1e-6f.  dur [B*S*K]: the duration us of each slot, only when a duration sample can
+   * differ from its fct (duration_mode SERVICE, lost-FIN guesses): else NULL, and the duration
+   * reservoir IS the fct reservoir */
   uint32_t* res;
+  uint32_t* dur;
   /* unchanged-reservoir skip of observe: slots written by the last dynamics
    * launch (a 128-bit mask per server) and the server's 10 reservoir features at the last
    * observe */
@@ -327,6 +330,7 @@ typedef struct oracle {
    * episode start / the server's last failure, never decremented (lbhash.h:193,214) */
   int leak;
   uint32_t* lost_on;
+  int dur_plane; /* the `dur` section exists (last in the snapshot) */
   /* TRACE arrivals (lbsim_set_trace semantics): us gap before each row, mean-1 work */
   uint32_t* trace_gap; float* trace_work; uint32_t trace_rows;
   /* not state: the Algorithm R draw word of each queued flow that arrived in the current step,
@@ -350,6 +354,7 @@ static void derive(oracle_t* o) {
   o->rec_thr = (uint32_t)llround((double)c->recover_prob * 16777216.0);
   o->big_in_step = (o->dt_us >= (int32_t)((1u << 25) - 1u)) || o->lf_thr != 0u;
   o->leak = c->n_flow_on_mode == LBSIM_NFLOW_VPP && o->lf_thr != 0u;
+  o->dur_plane = c->duration_mode == LBSIM_DURATION_SERVICE || o->lf_thr != 0u;
   o->key[0] = (uint32_t)(c->seed & 0xFFFFFFFFull);
   o->key[1] = (uint32_t)(c->seed >> 32);
 }
@@ -362,9 +367,10 @@ oracle_t* oracle_create(const lbsim_config_t* cfg) {
   o->threads = 1;
   const size_t B = o->B, BS = (size_t)o->B * o->S, BSQ = BS * o->Q, BSK = BS * K;
   const size_t sz[] = {B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4, B * 4,
-                       B * 8, BS * 4, BS * 4, BS * 4, BSQ * 8, BSK * 12, BS * 16, BS * 40,
+                       B * 8, BS * 4, BS * 4, BS * 4, BSQ * 8, BSK * 8, BS * 16, BS * 40,
                        cfg->normalize_obs ? BS * NF * 8 : 0, cfg->normalize_obs ? BS * NF * 8 : 0,
-                       cfg->fail_prob > 0.0f ? BS * 4 : 0, o->leak ? BS * 4 : 0};
+                       cfg->fail_prob > 0.0f ? BS * 4 : 0, o->leak ? BS * 4 : 0,
+                       o->dur_plane ? BSK * 4 : 0};
   size_t total = 0;
   for (size_t i = 0; i < sizeof(sz) / sizeof(sz[0]); ++i) total += sz[i];
   o->bytes = total;
@@ -377,7 +383,7 @@ oracle_t* oracle_create(const lbsim_config_t* cfg) {
                    (void**)&o->norm_count, (void**)&o->ep_return, (void**)&o->hc,
                    (void**)&o->last_tc, (void**)&o->res_count, (void**)&o->ring,
                    (void**)&o->res, (void**)&o->chg, (void**)&o->fcache, (void**)&o->norm_mean,
-                   (void**)&o->norm_std, (void**)&o->down, (void**)&o->lost_on};
+                   (void**)&o->norm_std, (void**)&o->down, (void**)&o->lost_on, (void**)&o->dur};
   for (size_t i = 0; i < sizeof(sz) / sizeof(sz[0]); ++i) {
     *ptrs[i] = sz[i] ? (void*)p : NULL;
     p += sz[i];
@@ -611,9 +617,9 @@ static void reservoir_add(env_ctx* e, int s, uint32_t fct, uint32_t dur, uint32_
     /* HC_BIG at the store for a flow carried in from an earlier step; in-step records by the
      * end-of-launch scan (big_scan) */
     if (!has_r && (fct > dur ? fct : dur) >= PACK_LIMIT) o->hc[sb] |= HC_BIG;
-    o->res[3 * r + 0] = fct;
-    o->res[3 * r + 1] = dur;
-    o->res[3 * r + 2] = ts_ms;
+    o->res[2 * r + 0] = fct;
+    o->res[2 * r + 1] = ts_ms;
+    if (o->dur) o->dur[r] = dur;
     o->chg[sb * 4 + (size_t)(slot >> 5)] |= 1u << (slot & 31);
   }
   if (c != 0xFFFFFFFFu) o->res_count[sb] = c + 1u;
@@ -629,7 +635,8 @@ static void big_scan(oracle_t* o, size_t b) {
     const uint32_t n = c < (uint32_t)K ? c : (uint32_t)K;
     for (uint32_t slot = 0; slot < n; ++slot) {
       if (!((o->chg[sb * 4 + (slot >> 5)] >> (slot & 31)) & 1u)) continue;
-      const uint32_t f = o->res[3 * (sb * K + slot)], d = o->res[3 * (sb * K + slot) + 1];
+      const uint32_t f = o->res[2 * (sb * K + slot)];
+      const uint32_t d = o->dur ? o->dur[sb * K + slot] : f;
       if ((f > d ? f : d) >= PACK_LIMIT) o->hc[sb] |= HC_BIG;
     }
   }
@@ -746,8 +753,12 @@ static void sim_step(env_ctx* e, const float* w) {
     int cnt[LBSIM_MAX_SERVERS];
     float sc[LBSIM_MAX_SERVERS];
     for (int s = 0; s < S; ++s) {
-      cnt[s] = ring_count(o, b * (size_t)S + (size_t)s);
-      sc[s] = score_of(policy, cnt[s], den[s]);
+      const size_t sb = b * (size_t)S + (size_t)s;
+      cnt[s] = ring_count(o, sb);
+      /* node.c:395-437 score on the as_stat n_flow_on, which never drops a lost-FIN flow
+       * (lbhash.h:193,214): under n_flow_on_mode VPP the queue plus the server's lost flows
+       * completed so far (counted at their pop, pop_until); eligibility stays the queue */
+      sc[s] = score_of(policy, cnt[s] + (o->lost_on ? (int32_t)o->lost_on[sb] : 0), den[s]);
     }
     int chosen = -1;
     if (policy == LBSIM_POLICY_ALIAS) {
@@ -869,12 +880,13 @@ static void observe(oracle_t* o, size_t b, float* obs_out, float* reward_out, ui
     float w[K];
     uint64_t wq[K];
     uint32_t ts[K];
-    for (int i = 0; i < n; ++i) ts[i] = o->res[3 * (sb * K + (size_t)i) + 2];
+    for (int i = 0; i < n; ++i) ts[i] = o->res[2 * (sb * K + (size_t)i) + 1];
     slot_weights(ts, n, o->decay_c, w, wq);
     float ff[5], fd[5], vf[K], vd[K];
     for (int i = 0; i < n; ++i) {
-      vf[i] = us_to_seconds(o->res[3 * (sb * K + (size_t)i) + 0]);
-      vd[i] = us_to_seconds(o->res[3 * (sb * K + (size_t)i) + 1]);
+      vf[i] = us_to_seconds(o->res[2 * (sb * K + (size_t)i)]);
+      /* paired records (no duration plane): the duration reservoir is the fct reservoir */
+      vd[i] = o->dur ? us_to_seconds(o->dur[sb * K + (size_t)i]) : vf[i];
     }
     features_one(vf, w, wq, n, ff);
     features_one(vd, w, wq, n, fd);

@@ -4,36 +4,48 @@ import numpy as np
 K, NF = 128, 11
 
 
-def sections(B, S, Q, normalize, failures=False, leak=False):
+def sections(B, S, Q, normalize, failures=False, leak=False, dur_plane=False):
     BS = B * S
     out = [("next_arr", np.int32, B), ("next_work", np.float32, B), ("next_u2", np.uint32, B),
            ("next_u3", np.uint32, B), ("arr_idx", np.uint32, B), ("episode", np.uint32, B),
            ("clock", np.uint32, B), ("ep_step", np.int32, B), ("dropped", np.uint32, B),
            ("norm_count", np.int32, B), ("ep_return", np.float64, B), ("hc", np.uint32, BS),
            ("last_tc", np.int32, BS), ("res_count", np.uint32, BS), ("ring", np.int32, BS * Q * 2),
-           ("res", np.uint32, BS * K * 3), ("chg", np.uint32, BS * 4), ("fcache", np.float32, BS * 10)]
+           ("res", np.uint32, BS * K * 2), ("chg", np.uint32, BS * 4), ("fcache", np.float32, BS * 10)]
     if normalize:
         out += [("norm_mean", np.float64, BS * NF), ("norm_std", np.float64, BS * NF)]
     if failures:
         out += [("down", np.uint32, BS)]
     if leak:  # n_flow_on_mode "vpp" with lost-FIN: lost flows per server
         out += [("lost_on", np.uint32, BS)]
+    if dur_plane:  # duration_mode "service" or lost-FIN: the duration of each slot
+        out += [("res_dur", np.uint32, BS * K)]
     return out
+
+
+def has_dur_plane(cfg) -> bool:
+    return cfg.duration_mode == 1 or cfg.lost_fin_prob > 0
 
 
 def has_leak(cfg) -> bool:
     return cfg.n_flow_on_mode == 1 and cfg.lost_fin_prob > 0
 
 
-def parse(buf: bytes, B, S, Q, normalize, failures=False, leak=False):
+def parse(buf: bytes, B, S, Q, normalize, failures=False, leak=False, dur_plane=None):
+    """dur_plane None: inferred from the snapshot's size (the plane is the last B*S*K words)."""
+    if dur_plane is None:
+        base = sum(np.dtype(dt).itemsize * n for _, dt, n in sections(B, S, Q, normalize, failures, leak))
+        dur_plane = len(buf) == base + 4 * B * S * K
     d, off = {}, 0
-    for name, dt, n in sections(B, S, Q, normalize, failures, leak):
+    for name, dt, n in sections(B, S, Q, normalize, failures, leak, dur_plane):
         nb = np.dtype(dt).itemsize * n
         d[name] = np.frombuffer(buf[off:off + nb], dtype=dt)
         off += nb
     assert off == len(buf), (off, len(buf))
-    rec = d["res"].reshape(-1, 3)  # slot records {fct us, duration us, timestamp ms}
-    d["res_fct"], d["res_dur"], d["res_ts"] = rec[:, 0], rec[:, 1], rec[:, 2]
+    rec = d["res"].reshape(-1, 2)  # slot records {fct us, timestamp ms}
+    d["res_fct"], d["res_ts"] = rec[:, 0], rec[:, 1]
+    if "res_dur" not in d:  # paired records: the duration reservoir is the fct reservoir
+        d["res_dur"] = d["res_fct"]
     return d
 
 

@@ -116,3 +116,47 @@ def test_bench_self_launches_ranks(world, batch):
     assert ranks["world_size"] == world and len(ranks["elapsed_s"]) == world
     assert ranks["elapsed_min_s"] <= ranks["elapsed_max_s"]
     assert abs(ranks["elapsed_max_s"] - out["ms_per_step"] * 3 / 1e3) < 1e-9
+
+
+@pytest.mark.gpu
+def test_bench_torchrun_rccl_world1():
+    """The driver's multi-GPU launch form (`python -m torch.distributed.run --nproc-per-node N
+    ... bench.py --gpus N`) at N = 1 on the one card a test box has: torchrun's environment
+    contract gives the rank, bench.py opens an RCCL ("nccl") process group with device_id, and the
+    timing barrier plus max_over_ranks / gather_over_ranks run as RCCL collectives on a device
+    tensor -- the code path of the 8-GPU scaling run, executed end to end."""
+    import json
+    root = os.path.dirname(HERE)
+    env = {k: v for k, v in os.environ.items() if k != "LBSIM_DIST_BACKEND"}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "1", "--master-addr", "127.0.0.1", "--master-port",
+                        str(free_port()), os.path.join(root, "bench.py"), "--gpus", "1",
+                        "--steps", "3", "--warmup", "1", "--batch", "2048", "--no-cpu-baseline",
+                        "--no-graph", "--prewarm-ms", "0"], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 1 and out["value"] > 0
+    ranks = out["ranks"]
+    assert ranks["backend"] == "nccl" and ranks["world_size"] == 1
+    assert len(ranks["elapsed_s"]) == 1
+    assert abs(ranks["elapsed_max_s"] - out["ms_per_step"] * 3 / 1e3) < 1e-9
+
+
+@pytest.mark.gpu
+def test_bench_graph_leg_runs_in_a_child_process():
+    """The graph leg runs in a child process (bench.graph_leg_child): the headline line carries
+    its result, marked as a child's, and the headline process never captures a graph."""
+    import json
+    root = os.path.dirname(HERE)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "5",
+                        "--warmup", "2", "--batch", "2048", "--no-cpu-baseline", "--prewarm-ms", "0"],
+                       cwd=root, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    g = json.loads(lines[0])["graph"]
+    assert "error" not in g, g
+    assert g["process"].startswith("child") and g["value"] > 0 and g["autoreset"] == "next_step"

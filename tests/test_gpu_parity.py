@@ -269,6 +269,12 @@ CONFIGS = [
     dict(B=40, S=20, kw={"n_flow_on_mode": "vpp", "lost_fin_prob": 0.2, "assign_policy": "sed2"}),
     dict(B=8256, S=4, kw={"n_flow_on_mode": "vpp", "lost_fin_prob": 0.2, "max_steps": 5,
                           "next_step_reset": True}),
+    # ... whose SED / LSQ scores read the leaky count (node.c:395-437): every flow
+    # lost on two-choice LSQ, and SED with unequal weights
+    dict(B=48, S=8, kw={"n_flow_on_mode": "vpp", "lost_fin_prob": 1.0, "assign_policy": "lsq2",
+                        "action_type": "continuous"}),
+    dict(B=66, S=5, kw={"n_flow_on_mode": "vpp", "lost_fin_prob": 0.6,
+                        "discrete_weights": [0.5, 1.0, 3.0]}),
 ]
 
 

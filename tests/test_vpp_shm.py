@@ -187,16 +187,17 @@ def test_gpu_simulator_as_live_vpp(oracle_mod, tmp_path):
         tv, nf, ts = pub.export()
         st = statelayout.parse(ora.state_bytes(), B, S, env.cfg.queue_capacity, False)
         cnt = np.minimum(st["res_count"].reshape(B, S), 128)
-        rec = st["res"].reshape(B, S, 128, 3)
+        words = {0: st["res_fct"].reshape(B, S, 128), 1: st["res_dur"].reshape(B, S, 128)}
+        tsw = st["res_ts"].reshape(B, S, 128)
         clock = st["clock"]
         for b in range(n):
             assert ts[b] == np.float32(clock[b] * 0.25)
             np.testing.assert_array_equal(nf[b], obs_g[b, :, 0].cpu().numpy().astype(np.int32))
             for s in range(S):
                 m = np.arange(128) < cnt[b, s]
-                t = np.where(m, (rec[b, s, :, 2].astype(np.float64) * 1e-3).astype(np.float32), 0)
+                t = np.where(m, (tsw[b, s].astype(np.float64) * 1e-3).astype(np.float32), 0)
                 for r in range(2):
-                    v = np.where(m, rec[b, s, :, r].view(np.int32).astype(np.float32) * np.float32(1e-6), 0)
+                    v = np.where(m, words[r][b, s].view(np.int32).astype(np.float32) * np.float32(1e-6), 0)
                     np.testing.assert_array_equal(tv[b, s, r, :, 0], t)
                     np.testing.assert_array_equal(tv[b, s, r, :, 1], v.astype(np.float32))
         seqs = pub.publish()
@@ -225,13 +226,14 @@ def _tv_from_oracle_state(st, B, S):
     """The VPP view (lbsim_vpp_export's contract) of an oracle state snapshot: [B, S, 2, 128, 2]
     (t, v) f32 and the frame times [B]."""
     cnt = np.minimum(st["res_count"].reshape(B, S), 128)
-    rec = st["res"].reshape(B, S, 128, 3)
+    words = (st["res_fct"].reshape(B, S, 128), st["res_dur"].reshape(B, S, 128))
     m = np.arange(128)[None, None, :] < cnt[:, :, None]
-    t = np.where(m, (rec[..., 2].astype(np.float64) * 1e-3).astype(np.float32), np.float32(0))
+    t = np.where(m, (st["res_ts"].reshape(B, S, 128).astype(np.float64) * 1e-3).astype(np.float32),
+                 np.float32(0))
     tv = np.zeros((B, S, 2, 128, 2), np.float32)
     for r in range(2):
         tv[:, :, r, :, 0] = t
-        tv[:, :, r, :, 1] = np.where(m, rec[..., r].view(np.int32).astype(np.float32) * np.float32(1e-6),
+        tv[:, :, r, :, 1] = np.where(m, words[r].view(np.int32).astype(np.float32) * np.float32(1e-6),
                                      np.float32(0))
     ts = (st["clock"].astype(np.float64) * 0.25).astype(np.float32)
     return tv, ts
