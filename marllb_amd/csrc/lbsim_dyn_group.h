@@ -31,14 +31,6 @@
 namespace lbk {
 
 constexpr int kGroupWL = 8;  // LDS queue window per server: 64 lanes x 8 x 8 B = 4 KiB per wave
-// 1: the entry after the queue head is read one iteration ahead (SrvLane::nt), so an iteration's
-// pop waits on no LDS round trip; 0: read at the pop (A/B)
-#ifndef LBSIM_DYN_NT_AHEAD
-#define LBSIM_DYN_NT_AHEAD 1
-#endif
-#ifndef LBSIM_DYN_KEYS_IN_BLOCK
-#define LBSIM_DYN_KEYS_IN_BLOCK 1
-#endif
 
 // Reductions over the aligned G-lane group (G <= 16: one DPP row).  Lanes read only within their
 // group, so groups that left the event loop (inactive lanes) are never read.  mov_dpp with
@@ -124,8 +116,6 @@ __device__ __forceinline__ uint64_t group_bits(uint64_t m, int gbase) {
 // The server this lane owns (fields of DESIGN.md §4, in registers).
 struct SrvLane {
   int32_t cnt, head_tc, head, lh, tail, last, assigned;
-  int32_t nt;       // t_complete of the entry after the head (valid if cnt > 1): the next pop's
-                    // new head_tc from a register, refreshed from LDS one iteration ahead
   int32_t qcap;     // Q, or 0 while the server is down (fail_prob > 0): not eligible, as full
   bool big;         // the server's sticky kHcBig flag
   uint32_t rcnt;
@@ -171,8 +161,11 @@ __device__ __forceinline__ GroupConst group_const(const SimParams& p, uint32_t b
 }
 
 // The event loop of sim_step_group (section 2).  FAST (wave-uniform): every SED score finite, so no
-// NaN fallback division and no NaN ballot.
-template <int G, int POLICY, bool TRACE, bool FAST>
+// NaN fallback division and no NaN ballot.  KEYS: the Philox round keys are formed inside the
+// draw-ahead block (kModeStepNR: the compiler otherwise hoists them into 20 loop-long VGPRs,
+// which took that kernel past the 4-wave budget); the plain step lets them be hoisted (measured
+// 4 us faster at 65536 x 4 than forming them in the block, profiles/r06c/).
+template <int G, int POLICY, bool TRACE, bool FAST, bool KEYS = false>
 __device__ __forceinline__ void group_event_loop(const DevState& st, const SimParams& p,
                                                  LaneState<1>& E, SrvLane& V, int s, int gbase,
                                                  int n_alias, const GroupConst& gc, int2* win,
@@ -207,10 +200,7 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
       const uint32_t k = cbase + (uint32_t)s;
       uint32_t rk0[10], rk1[10];
       uint32_t k0 = gc.k0, k1 = gc.k1;
-#if LBSIM_DYN_KEYS_IN_BLOCK
-      // opaque here: the compiler would hoist the 20 round keys out of the loop (20 live VGPRs)
-      asm volatile("" : "+v"(k0), "+v"(k1));
-#endif
+      if constexpr (KEYS) asm volatile("" : "+v"(k0), "+v"(k1));  // opaque: not hoisted
 #pragma unroll
       for (int r = 0; r < 10; ++r) {
         rk0[r] = k0 + (uint32_t)r * 0x9E3779B9u;
@@ -254,22 +244,15 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
       *wslot(V.lh) = my_ring[(uint32_t)pw];
       __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
     }
+    // (reading the entry after the new head one iteration ahead, into a register, measured 4 us
+    // slower at 65536 x 4: profiles/r06c/)
     const int nl = (V.lh + 1) & (WL - 1);
-#if LBSIM_DYN_NT_AHEAD
-    const int32_t nt = V.nt;  // next head (valid if cnt > 1), read an iteration ago
-#else
     const int32_t nt = wslot(nl)->x;  // next head (valid if cnt > 1)
-#endif
     V.last = due ? V.head_tc : V.last;
     V.cnt -= due ? 1 : 0;
     V.head = due ? ((V.head + 1 == Q) ? 0 : V.head + 1) : V.head;
     V.lh = due ? nl : V.lh;
     V.head_tc = due ? nt : V.head_tc;
-#if LBSIM_DYN_NT_AHEAD
-    // the entry after the new head, for the next pop: issued now, consumed at the iteration's end
-    // (V.nt below), so its LDS round trip overlaps the choice instead of preceding the pop
-    const int32_t nt_next = wslot((V.lh + 1) & (WL - 1))->x;
-#endif
     const bool more = group_bits<G>(__ballot(due && V.cnt > 0 && nt <= th), gbase) != 0ull;
     if (!arrival_due && !more) break;  // group-uniform
     const bool arr = arrival_due && !more;
@@ -352,8 +335,6 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
       }
       mark(slot);
     }
-    // the pushed flow lands right after the head: it is the next pop's new head
-    const bool nt_push = mine && V.cnt == 1;
     if (mine) {
       const int2 e = make_int2(tc_a, ta);
       if (V.cnt < WL) {
@@ -381,16 +362,10 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
     E.u2 = arr ? nu2 : E.u2;
     E.u3 = arr ? nu3 : E.u3;
     E.arr_idx += arr ? 1u : 0u;
-#if LBSIM_DYN_NT_AHEAD
-    V.nt = nt_push ? tc_a : (due ? nt_next : V.nt);
-#else
-    (void)nt_push;
-#endif
   }
-
 }
 
-template <int G, int POLICY, bool TRACE>
+template <int G, int POLICY, bool TRACE, bool KEYS = false>
 __device__ __forceinline__ void sim_step_group(const DevState& st, const SimParams& p,
                                                LaneState<1>& E, SrvLane& V, uint32_t b, int s,
                                                int gbase, float w_own, const float (&wall)[G],
@@ -484,15 +459,14 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
   //      SED2 scores can only be NaN when some den is 0 / inf / NaN: a wave whose servers all have
   //      finite scores runs the loop without the NaN fallbacks (a wave-uniform choice).
   const GroupConst gc = group_const(p, base_ms, base_rem);
-  V.nt = wslot((V.lh + 1) & (WL - 1))->x;  // the entry after the head (group_event_loop)
   const bool finite = lsq || alias || !V.act ||
                       (fabs(V.den) >= 1e-30 && fabs(V.den) <= 1e300);  // false for NaN
   if (__all(finite) && !p.leak && st.res_dur == nullptr)
-    group_event_loop<G, POLICY, TRACE, true>(st, p, E, V, s, gbase, n_alias, gc, win, atab, acache, my_res,
-                                             my_ring);
+    group_event_loop<G, POLICY, TRACE, true, KEYS>(st, p, E, V, s, gbase, n_alias, gc, win, atab,
+                                                   acache, my_res, my_ring);
   else
-    group_event_loop<G, POLICY, TRACE, false>(st, p, E, V, s, gbase, n_alias, gc, win, atab, acache, my_res,
-                                              my_ring);
+    group_event_loop<G, POLICY, TRACE, false, KEYS>(st, p, E, V, s, gbase, n_alias, gc, win, atab,
+                                                    acache, my_res, my_ring);
 
   // ---- rebase to the next step's start (this lane's server)
   E.next_arr -= dt;
@@ -589,6 +563,9 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
     V.qcap = Q;  // every server is up at the episode start
     V.big = false;
     V.lost = 0;  // n_flow_on_mode VPP: no lost flows yet
+    // emptied reservoirs: slot 0 marked written, so the next observe recomputes every server of
+    // the env (its cached features are the last episode's)
+    if (V.act) chgw[lane] = 1u;
 #pragma unroll
     for (int k = 0; k < G; ++k) wall[k] = 1.0f;
   };
@@ -666,7 +643,7 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
     const int nsteps = rs ? p.warmup_steps : 1;
     const float w = rs ? 1.0f : w_own;
     for (int k = 0; k < nsteps; ++k)
-      sim_step_group<G, POLICY, TRACE>(st, p, E, V, b, s, gbase, w, wall, win, atab, acache);
+      sim_step_group<G, POLICY, TRACE, true>(st, p, E, V, b, s, gbase, w, wall, win, atab, acache);
     if (rs) reset_out(-1);
   }
 

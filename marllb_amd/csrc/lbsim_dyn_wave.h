@@ -586,6 +586,9 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
     V.tail = 0;
     V.last = kLastNone;
     V.rcnt = 0u;
+    // emptied reservoirs: slot 0 marked written, so the next observe recomputes every server of
+    // the env (its cached features are the last episode's)
+    if (lane < S) Ld.chg[lane] = 1u;
   };
   auto load_in = [&]() {  // the env, its ring lanes and server fields from HBM, the step's weight
     E.episode = st.episode[b];

@@ -546,8 +546,10 @@ __device__ __forceinline__ void clear_servers(const SimParams& p, LaneState<MAXS
     L.last[s] = kLastNone;
     fld<MAXS>(l, F_RCNT, s) = 0;
     fld<MAXS>(l, F_ASSIGNED, s) = 0;
+    // emptied reservoirs: slot 0 marked written, so the next observe recomputes every server
+    // (its cached features are the last episode's)
 #pragma unroll
-    for (int w = 0; w < 4; ++w) l.m[(s * 4 + w) * 64 + l.lane] = 0u;
+    for (int w = 0; w < 4; ++w) l.m[(s * 4 + w) * 64 + l.lane] = (w == 0 && s < p.S) ? 1u : 0u;
   }
 }
 
@@ -1769,9 +1771,9 @@ __device__ __forceinline__ bool observe_chunk_full(const DevState& st, const Sim
 // statistics come from the sorted keys (reservoir.py:144, 165-196).
 // INC (step mode with state): a chunk none of whose reservoirs this step's dynamics wrote
 // (DevState::chg all zero) takes its features from DevState::fcache instead of recomputing them;
-// every computed chunk refreshes the cache (US: reset and step modes).
-// fresh: the env was reset by this step (next-step auto-reset): every chunk is recomputed (the
-// cached features are the previous episode's).
+// every computed chunk refreshes the cache (US: reset and step modes).  A reset (also the one
+// inside a next-step auto-reset step) marks slot 0 of every server written, so a reset env never
+// takes the previous episode's cached features, with no reset flag to load here.
 // REGS = false: the general path only -- observe_rows_paired's fallback for rows the register
 // path cannot take (one copy of the code instead of two more register-path instantiations: fewer
 // SGPR / VGPR spills in observe_pair_kernel, 131 -> 125 us at 65536 x 4, 241 -> 229 us at
@@ -1779,7 +1781,7 @@ __device__ __forceinline__ bool observe_chunk_full(const DevState& st, const Sim
 template <bool US, bool INC, bool REGS = true>
 __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParams& p, size_t b,
                                               int s_base, int S, ObsScratch& sc, float* obs_out,
-                                              int lane, bool fresh = false) {
+                                              int lane) {
   const size_t srow = b * (size_t)p.S + (size_t)s_base;  // first (env, server) of the chunk
   const int R = 2 * S;
   const int g = lane >> 3, j = lane & 7;
@@ -1793,7 +1795,7 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
   }
   if constexpr (INC) {
     const uint32_t w = lane < 4 * S ? st.chg[(srow + (size_t)(lane >> 2)) * 4 + (lane & 3)] : 0u;
-    if (!fresh && !__any(w != 0u)) {  // no reservoir of the chunk changed: the cached features
+    if (!__any(w != 0u)) {  // no reservoir of the chunk changed: the cached features
       for (int e = lane; e < S * NF; e += 64) {
         const int s = e / NF, c = e - s * NF;
         obs_out[s_base * NF + e] = c == 0 ? n_flow_on(st, srow + (size_t)s)
@@ -1812,19 +1814,27 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
     uint32_t f[4][2], d[4][2], t[4][2];
     int nn[4];
 #pragma unroll
+    for (int u = 0; u < 4; ++u) {  // the counts first: one round trip, then every slot load
+      const int s = s0 + u;
+      const uint32_t rcl = st.res_count[srow + (size_t)(s < S ? s : 0)];  // branch-free loads
+      const uint32_t rc = s < S ? rcl : 0u;
+      nn[u] = rc < (uint32_t)K ? (int)rc : K;
+    }
+#pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int s = s0 + u;
       const size_t sb = srow + (size_t)(s < S ? s : 0);
-      const uint32_t rc = s < S ? st.res_count[sb] : 0u;
-      nn[u] = rc < (uint32_t)K ? (int)rc : K;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int slot = lane + 64 * h;
         const bool v = slot < nn[u];
         if constexpr (US) {  // simulator: one 8-B record per slot (+ the duration plane)
+          const bool dplane = st.res_dur != nullptr;
           const uint2 rec = v ? st.res[sb * K + slot] : make_uint2(0u, 0u);
+          // (the plane's load must not wait for the record: both issued, then the select)
+          const uint32_t dw = (v && dplane) ? st.res_dur[sb * K + slot] : 0u;
           f[u][h] = rec.x;
-          d[u][h] = (v && st.res_dur != nullptr) ? st.res_dur[sb * K + slot] : rec.x;
+          d[u][h] = dplane ? dw : rec.x;
           t[u][h] = rec.y;
         } else {  // features API: one value array serves as both "fct" and "duration"
           f[u][h] = v ? st.feat_vals[sb * K + slot] : 0u;
@@ -2174,10 +2184,12 @@ __device__ __forceinline__ uint64_t fixed48(float w) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// hcw: the hc word of the lane's row (loaded with the decision words): column 0 from it, no load.
 template <bool FULL>
 __device__ __forceinline__ void observe_rows_paired_regs(const DevState& st, const SimParams& p,
                                                          size_t row0, int nrows, int n_in,
-                                                         ObsScratch& sc, float* obs_out, int lane) {
+                                                         ObsScratch& sc, float* obs_out, int lane,
+                                                         uint32_t hcw) {
   const int u = lane >> 3, j = lane & 7;
   const bool act = u < nrows;
   const size_t sb = row0 + (size_t)(act ? u : 0);
@@ -2356,7 +2368,10 @@ __device__ __forceinline__ void observe_rows_paired_regs(const DevState& st, con
       st.fcache[sb * 10 + (size_t)j] = v;
       st.fcache[sb * 10 + (size_t)(5 + j)] = v;
     } else if (j == 5) {
-      obs_out[u * NF] = n_flow_on(st, sb);
+      uint32_t nfo = hcw >> 16;  // n_flow_on (n_flow_on_mode VPP: + the lost-FIN flows)
+      if (st.lost_on != nullptr)
+        nfo += __hip_atomic_load(st.lost_on + sb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      obs_out[u * NF] = (float)nfo;
     }
   }
   wave_sync();
@@ -2372,7 +2387,7 @@ __device__ __forceinline__ void observe_rows_paired_regs(const DevState& st, con
 template <bool INC>
 __device__ __forceinline__ void observe_rows_paired(const DevState& st, const SimParams& p,
                                                     size_t b0, int nenv, ObsScratch& sc,
-                                                    float* obs_out, int lane, bool nr) {
+                                                    float* obs_out, int lane) {
   const int S = p.S, nrows = nenv * S;
   const size_t row0 = b0 * (size_t)S;
   const int u = lane >> 3;
@@ -2382,9 +2397,8 @@ __device__ __forceinline__ void observe_rows_paired(const DevState& st, const Si
   const uint32_t hcw = st.hc[usb];
   if constexpr (INC) {
     const uint32_t w = lane < 4 * nrows ? st.chg[(row0 + (size_t)(lane >> 2)) * 4 + (lane & 3)] : 0u;
-    // one round trip for the decision words and the reset flags: every load is issued first
-    const bool fresh = nr && __any(lane < nenv && st.ep_step[b0 + (size_t)lane] < 0);
-    if (!fresh && !__any(w != 0u)) {  // no reservoir of the rows changed: the cached features
+    // one round trip for the decision words (a reset env's rows are marked written: no reset flag)
+    if (!__any(w != 0u)) {  // no reservoir of the rows changed: the cached features
       for (int e = lane; e < nrows * NF; e += 64) {
         const int s = e / NF, c = e - s * NF;
         obs_out[e] = c == 0 ? n_flow_on(st, row0 + (size_t)s)
@@ -2396,27 +2410,27 @@ __device__ __forceinline__ void observe_rows_paired(const DevState& st, const Si
   }
   const int n = rc < (uint32_t)K ? (int)rc : K;
   if (!__any(act && (n < 8 || (hcw & kHcBig) != 0u))) {
-    if (!__any(act && n < K)) observe_rows_paired_regs<true>(st, p, row0, nrows, K, sc, obs_out, lane);
-    else observe_rows_paired_regs<false>(st, p, row0, nrows, n, sc, obs_out, lane);
+    if (!__any(act && n < K))
+      observe_rows_paired_regs<true>(st, p, row0, nrows, K, sc, obs_out, lane, hcw);
+    else
+      observe_rows_paired_regs<false>(st, p, row0, nrows, n, sc, obs_out, lane, hcw);
     return;
   }
   for (int e = 0; e < nenv; ++e) {
-    const bool fe = nr && st.ep_step[b0 + (size_t)e] < 0;
     for (int s0 = 0; s0 < S; s0 += kObsChunk)
       observe_chunk<true, INC, LBSIM_OBS_PAIR_FALLBACK_REGS != 0>(
           st, p, b0 + (size_t)e, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk, sc,
-          obs_out + e * S * NF, lane, fe);
+          obs_out + e * S * NF, lane);
   }
 }
 
 // Rows [s0, s0 + 8) of env b of a wide env (S a multiple of 8, S >= 16): the paired register
 // path of observe_rows_paired over one wave's 8 rows, written to obs_env + s0 * NF; the rows the
-// register path cannot take go through the two 4-server observe_chunk calls.  fresh: env b was
-// reset by this step (no cached features).
+// register path cannot take go through the two 4-server observe_chunk calls.
 template <bool INC>
 __device__ __forceinline__ void observe_rows_paired_wide(const DevState& st, const SimParams& p,
                                                          size_t b, int s0, ObsScratch& sc,
-                                                         float* obs_env, int lane, bool fresh) {
+                                                         float* obs_env, int lane) {
   const size_t row0 = b * (size_t)p.S + (size_t)s0;
   const size_t usb = row0 + (size_t)(lane >> 3);
   float* obs_out = obs_env + s0 * NF;
@@ -2424,7 +2438,7 @@ __device__ __forceinline__ void observe_rows_paired_wide(const DevState& st, con
   const uint32_t hcw = st.hc[usb];
   if constexpr (INC) {
     const uint32_t w = lane < 32 ? st.chg[(row0 + (size_t)(lane >> 2)) * 4 + (lane & 3)] : 0u;
-    if (!fresh && !__any(w != 0u)) {  // none of the 8 reservoirs changed: the cached features
+    if (!__any(w != 0u)) {  // none of the 8 reservoirs changed: the cached features
       for (int e = lane; e < 8 * NF; e += 64) {
         const int s = e / NF, c = e - s * NF;
         obs_out[e] = c == 0 ? n_flow_on(st, row0 + (size_t)s)
@@ -2436,13 +2450,13 @@ __device__ __forceinline__ void observe_rows_paired_wide(const DevState& st, con
   }
   const int n = rc < (uint32_t)K ? (int)rc : K;
   if (!__any(n < 8 || (hcw & kHcBig) != 0u)) {
-    if (!__any(n < K)) observe_rows_paired_regs<true>(st, p, row0, 8, K, sc, obs_out, lane);
-    else observe_rows_paired_regs<false>(st, p, row0, 8, n, sc, obs_out, lane);
+    if (!__any(n < K)) observe_rows_paired_regs<true>(st, p, row0, 8, K, sc, obs_out, lane, hcw);
+    else observe_rows_paired_regs<false>(st, p, row0, 8, n, sc, obs_out, lane, hcw);
     return;
   }
   for (int c = s0; c < s0 + 8; c += kObsChunk)
     observe_chunk<true, INC, LBSIM_OBS_PAIR_FALLBACK_REGS != 0>(st, p, b, c, kObsChunk, sc,
-                                                                 obs_env, lane, fresh);
+                                                                 obs_env, lane);
 }
 
 // ================================================================ observe (one wave = one env)
@@ -2471,11 +2485,14 @@ constexpr int kObsWavesPerEnv = MAXS <= kObsChunk ? 1 : MAXS / kObsChunk;
 
 // The reward, episode bookkeeping and output rows of env b once its (S, 11) rows are in s_obs
 // (rewards.py:290-381, env.py:261-281, env.py:450-470): threads tid < 64 (one wave) compute the
-// reward, all nthr threads write the rows.
+// reward, all nthr threads write the rows.  es_pf / er_pf: the env's ep_step / ep_return words
+// when the caller loaded them ahead (LDS), else nullptr (loaded here).
 template <int MAXS, int MODE, bool FAC>
 __device__ __forceinline__ void observe_outputs(const DevState& st, const SimParams& p,
                                                 const ObsOutputs& out, size_t b,
-                                                float* s_obs, float* s_act, int tid, int nthr) {
+                                                float* s_obs, float* s_act, int tid, int nthr,
+                                                const int32_t* es_pf = nullptr,
+                                                const double* er_pf = nullptr) {
   const int S = p.S;
   // active servers (any column > 0): lane s of wave 0 scans its row, one ballot; their
   // reward-field values compacted into s_act in server order
@@ -2492,7 +2509,8 @@ __device__ __forceinline__ void observe_outputs(const DevState& st, const SimPar
       const int na = __popcll(act_mask);
       double r = 0.0;
       // reset by this step (next-step auto-reset, ep_step = -1): reward 0, episode step 0, not done
-      const bool fresh = p.next_reset && st.ep_step[b] < 0;
+      const int32_t es0 = es_pf != nullptr ? *es_pf : st.ep_step[b];
+      const bool fresh = p.next_reset && es0 < 0;
       if (fok && !fresh) {
         // (compile-time for observe_kernel<4>; fused G = 8 with S <= 4 at run time)
         if ((MAXS <= kObsChunk || S <= kObsChunk) && p.reward_metric == 0)
@@ -2501,8 +2519,8 @@ __device__ __forceinline__ void observe_outputs(const DevState& st, const SimPar
           r = reward_values(na, [&](int i) { return (double)s_act[i]; }, p.reward_metric);
       }
       out.reward[b] = (float)r;
-      const int32_t es = st.ep_step[b] + 1;  // -1 + 1 = 0 for a fresh env
-      const double er = st.ep_return[b] + r;  // 0 + 0
+      const int32_t es = es0 + 1;  // -1 + 1 = 0 for a fresh env
+      const double er = (er_pf != nullptr ? *er_pf : st.ep_return[b]) + r;  // 0 + 0
       st.ep_step[b] = es;
       st.ep_return[b] = er;
       out.done[b] = (uint8_t)(es >= p.max_steps ? 1 : 0);
@@ -2581,9 +2599,8 @@ __global__ void __launch_bounds__(64 * kObsWavesPerEnv<MAXS>, 5)
   const int S = p.S;
   {
     const int s0 = wv * kObsChunk;  // the launch has ceil(S / 4) waves
-    const bool fresh = mode == kModeStep && p.next_reset && st.ep_step[b] < 0;
     observe_chunk<true, mode == kModeStep>(st, p, b, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk,
-                                           sc, s_obs, lane, fresh);
+                                           sc, s_obs, lane);
   }
   __syncthreads();
   observe_outputs<MAXS, MODE, FAC>(st, p, out, b, s_obs, s_act, tid, nthr);
@@ -2603,13 +2620,30 @@ __global__ void __launch_bounds__(64, LBSIM_OBS_PAIR_WAVES)
   __shared__ ObsScratch sc;
   __shared__ float s_obs[8 * NF];
   __shared__ float s_act[8];
+  __shared__ int32_t s_es[8];
+  __shared__ double s_er[8];
   const int S = p.S, epw = 8 / S, lane = (int)threadIdx.x;
   const size_t b0 = (size_t)blockIdx.x * (size_t)epw;
   const int nenv = (size_t)p.B - b0 < (size_t)epw ? (int)((size_t)p.B - b0) : epw;
-  observe_rows_paired<MODE == kModeStep>(st, p, b0, nenv, sc, s_obs, lane,
-                                         MODE == kModeStep && p.next_reset != 0);
+  // the envs' episode words, requested first and straight into LDS (global_load_lds: no VGPR
+  // holds them, no wait before the decision words): they arrive with the decision words instead
+  // of costing each env's bookkeeping a round trip of its own after the features
+  if constexpr (MODE == kModeStep) {
+    typedef __attribute__((address_space(1))) void gvoid;
+    typedef __attribute__((address_space(3))) void lvoid;
+    if (lane < nenv)
+      __builtin_amdgcn_global_load_lds((gvoid*)(st.ep_step + b0 + (size_t)lane), (lvoid*)s_es, 4,
+                                       0, 0);
+    if (lane < 2 * nenv)  // a double as two dwords
+      __builtin_amdgcn_global_load_lds(
+          (gvoid*)(reinterpret_cast<const uint32_t*>(st.ep_return + b0) + lane), (lvoid*)s_er, 4,
+          0, 0);
+  }
+  observe_rows_paired<MODE == kModeStep>(st, p, b0, nenv, sc, s_obs, lane);
   for (int e = 0; e < nenv; ++e) {
-    observe_outputs<8, MODE, FAC>(st, p, out, b0 + (size_t)e, s_obs + e * S * NF, s_act, lane, 64);
+    observe_outputs<8, MODE, FAC>(st, p, out, b0 + (size_t)e, s_obs + e * S * NF, s_act, lane, 64,
+                                  MODE == kModeStep ? s_es + e : nullptr,
+                                  MODE == kModeStep ? s_er + e : nullptr);
     wave_sync();  // s_act reused by the next env
   }
 }
@@ -2629,8 +2663,7 @@ __global__ void __launch_bounds__(128, LBSIM_OBS_PAIR16_WAVES)
   __shared__ float s_act[16];
   const size_t b = blockIdx.x;
   const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const bool fresh = MODE == kModeStep && p.next_reset && st.ep_step[b] < 0;
-  observe_rows_paired_wide<MODE == kModeStep>(st, p, b, 8 * wv, sc[wv], s_obs, lane, fresh);
+  observe_rows_paired_wide<MODE == kModeStep>(st, p, b, 8 * wv, sc[wv], s_obs, lane);
   __syncthreads();
   observe_outputs<16, MODE, FAC>(st, p, out, b, s_obs, s_act, tid, 128);
 }
@@ -2643,10 +2676,8 @@ __global__ void __launch_bounds__(64, LBSIM_OBS_PAIR_WAVES)
   const size_t b = blockIdx.x / (unsigned)ngroups;
   const int c = (int)(blockIdx.x - b * (unsigned)ngroups);
   __shared__ ObsScratch sc;
-  const bool fresh = MODE == kModeStep && p.next_reset && st.ep_step[b] < 0;
   observe_rows_paired_wide<MODE == kModeStep>(st, p, b, 8 * c, sc,
-                                              out.obs + b * (size_t)p.S * NF, (int)threadIdx.x,
-                                              fresh);
+                                              out.obs + b * (size_t)p.S * NF, (int)threadIdx.x);
 }
 
 // Wide envs (S > 16: configs[4] read literally, 4 agents x 16 servers), in two launches instead of
@@ -2665,9 +2696,8 @@ __global__ void __launch_bounds__(64, 5)
   if (MODE == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
   __shared__ ObsScratch sc;
   const int S = p.S, s0 = c * kObsChunk, lane = (int)threadIdx.x;
-  const bool fresh = MODE == kModeStep && p.next_reset && st.ep_step[b] < 0;
   observe_chunk<true, MODE == kModeStep>(st, p, b, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk,
-                                         sc, out.obs + b * (size_t)S * NF, lane, fresh);
+                                         sc, out.obs + b * (size_t)S * NF, lane);
 }
 
 template <int MAXS, int MODE, bool FAC>
@@ -2693,12 +2723,11 @@ __device__ __forceinline__ void observe_env_wave(const DevState& st, const SimPa
                                                  const ObsOutputs& out, size_t b, ObsScratch& sc,
                                                  float* s_obs, float* s_act, int lane) {
   const int S = p.S;
-  const bool fresh = p.next_reset && st.ep_step[b] < 0;
   if constexpr (MAXS <= kObsChunk) {  // one chunk: straight-line code, no loop-carried s0
-    observe_chunk<true, true>(st, p, b, 0, S, sc, s_obs, lane, fresh);
+    observe_chunk<true, true>(st, p, b, 0, S, sc, s_obs, lane);
   } else if (LBSIM_STEP_WAVE_PAIRED && MAXS <= 8 && st.res_dur == nullptr) {
     // paired records: the env's S <= 8 rows in one pass (observe_rows_paired)
-    observe_rows_paired<true>(st, p, b, 1, sc, s_obs, lane, p.next_reset != 0);
+    observe_rows_paired<true>(st, p, b, 1, sc, s_obs, lane);
   } else {
     // rolled, with b and lane opaque per chunk: nothing derived from them is hoisted and held
     // across both chunks (step_wave_kernel<4, ..., 8>: 124 VGPRs instead of 184 B of spills/lane)
@@ -2708,7 +2737,7 @@ __device__ __forceinline__ void observe_env_wave(const DevState& st, const SimPa
       int ln = lane;
       asm volatile("" : "+s"(bb), "+v"(ln));
       observe_chunk<true, true>(st, p, bb, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk, sc, s_obs,
-                                ln, fresh);
+                                ln);
     }
   }
   observe_outputs<MAXS, kModeStep, true>(st, p, out, b, s_obs, s_act, lane, 64);

@@ -927,7 +927,9 @@ static void reset_env(oracle_t* o, size_t b) {
     o->hc[sb] = 0u;
     o->last_tc[sb] = LAST_NONE;
     o->res_count[sb] = 0u;
-    for (int w = 0; w < 4; ++w) o->chg[sb * 4 + (size_t)w] = 0u;
+    /* emptied reservoirs: slot 0 marked written (the GPU's next observe recomputes every server
+     * of the env instead of reusing the last episode's cached features) */
+    for (int w = 0; w < 4; ++w) o->chg[sb * 4 + (size_t)w] = w == 0 ? 1u : 0u;
     if (o->down) o->down[sb] = 0u; /* every server is up at the episode start */
     if (o->lost_on) o->lost_on[sb] = 0u;
   }
