@@ -32,7 +32,8 @@
 extern "C" {
 #endif
 
-#define LBSIM_ABI_VERSION 8  /* 8: snapshot layout -- 8-B {fct, ts} records + duration plane */
+#define LBSIM_ABI_VERSION 9  /* 9: lost-FIN guesses deferred to their wrap-up time (split fct /  */
+                             /* duration reservoirs, pending rings), reservoir_mode VPP          */
 #define LBSIM_MAX_SERVERS 64   /* S <= 64: BASELINE configs[4] read literally is 4 agents x 16 */
                                /* servers = 64 (S > 16: server-per-lane dynamics only)       */
 #define LBSIM_RESERVOIR_K 128  /* reservoir.py:31 capacity=128, reservoir.h:24               */
@@ -94,6 +95,16 @@ enum lbsim_duration_mode { LBSIM_DURATION_AGE = 0, LBSIM_DURATION_SERVICE = 1 };
  * lost-FIN flows completed since the episode start (or its last failure).  Only differs from
  * QUEUE with lost_fin_prob > 0. */
 enum lbsim_n_flow_on_mode { LBSIM_NFLOW_QUEUE = 0, LBSIM_NFLOW_VPP = 1 };
+
+/* Reservoir replacement rule.  ALGR (default): problem-01's Algorithm R (reservoir.py:64-85) --
+ * slot `count` while count < 128, else slot j = randint(0, count + 1) if j < 128; observe takes
+ * the features over the first min(count, 128) slots.  VPP: the live data plane's rule
+ * (src/vpp/lb/lbhash.h:108,179 `res_id = rand() % RESERVOIR_N_BIN`, register_reservoir_as): every
+ * sample overwrites slot rand() % 128 unconditionally, and the bins start zeroed at reset (VPP's
+ * zeroed shm), so the upstream agent's process_reservoir over ALL 128 bins (shm_proxy.py:518-543,
+ * lbsim_vpp_export / feature_mode "upstream") sees a sparse, recency-biased reservoir until every
+ * bin was hit.  The counts still count samples. */
+enum lbsim_reservoir_mode { LBSIM_RESERVOIR_ALGR = 0, LBSIM_RESERVOIR_VPP = 1 };
 
 /* Dynamics-kernel mapping; every choice produces the same bits.  AUTO = SERVER_PER_LANE (faster
  * than one lane per env at every measured shape). */
@@ -158,8 +169,13 @@ typedef struct lbsim_config {
   /* Lost-FIN flows (VPP's timed-out flow sample, src/vpp/lb/lbhash.h:175-217, stats.h:27): a
    * flow's FIN/RST is missed with probability lost_fin_prob; its flow-table entry expires
    * flow_timeout_s after its last packet and the next flow hashed into its bucket (an exponential
-   * wait of mean flow_buckets / arrival_rate) wraps it up with fct = now - t_init - 40 s.  The
-   * sample (signed us) is recorded at the flow's completion.  0 = off. */
+   * wait of mean flow_buckets / arrival_rate) wraps it up with fct = now - t_init - 40 s.  That
+   * signed-us sample enters the server's fct reservoir at the wrap-up time (completion +
+   * flow_timeout + wait), stamped with it, in time order with the server's other samples: each
+   * server holds its pending guesses in a ring of lost_fin_pending entries sorted by due time (a
+   * guess arriving at a full ring is dropped and counted).  The flow's duration sample is
+   * recorded at its completion, so under lost-FIN the fct and duration reservoirs are separate
+   * (own counts, own timestamps).  0 = off. */
   float lost_fin_prob;       /* [0, 1], default 0                                            */
   float flow_timeout_s;      /* the lb plugin's flow timeout, default 40 (lb.c:1437)        */
   int32_t flow_buckets;      /* sticky buckets per core, default 1024 (lb.h:46)             */
@@ -179,6 +195,8 @@ typedef struct lbsim_config {
   int32_t next_step_reset;
   int32_t duration_mode;     /* lbsim_duration_mode, default AGE            */
   int32_t n_flow_on_mode;    /* lbsim_n_flow_on_mode, default QUEUE         */
+  int32_t lost_fin_pending;  /* pending lost-FIN guesses held per server, 1..4096, default 256 */
+  int32_t reservoir_mode;    /* lbsim_reservoir_mode, default ALGR           */
 } lbsim_config_t;
 
 typedef struct lbsim lbsim_t; /* opaque handle */

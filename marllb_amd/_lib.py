@@ -31,6 +31,7 @@ METRICS = ["jain", "variance", "std", "cv", "max", "min", "product", "range", "g
 POLICIES = ["sed", "sed2", "lsq", "lsq2", "alias"]
 DURATION_MODES = ("age", "service")  # lbsim_duration_mode
 N_FLOW_ON_MODES = ("queue", "vpp")  # lbsim_n_flow_on_mode
+RESERVOIR_MODES = ("algr", "vpp")  # lbsim_reservoir_mode
 
 
 class LbsimConfig(ctypes.Structure):
@@ -68,6 +69,8 @@ class LbsimConfig(ctypes.Structure):
         ("next_step_reset", ctypes.c_int32),
         ("duration_mode", ctypes.c_int32),
         ("n_flow_on_mode", ctypes.c_int32),
+        ("lost_fin_pending", ctypes.c_int32),
+        ("reservoir_mode", ctypes.c_int32),
     ]
 
 

@@ -58,9 +58,11 @@ def _compile(unit, verbose: bool) -> str:
 
 
 def build_library(force: bool = False, verbose: bool = False, jobs: int = 0,
-                  variant: str | None = None, defines: tuple = ()) -> str:
+                  variant: str | None = None, defines: tuple = (), only: tuple = ()) -> str:
     """Build liblbsim.so, or with `variant` an A/B build with extra `defines` into
-    marllb_amd/exp/liblbsim_<variant>.so (loaded through LBSIM_LIBRARY, see _lib.py)."""
+    marllb_amd/exp/liblbsim_<variant>.so (loaded through LBSIM_LIBRARY, see _lib.py).  `only`
+    (object names, e.g. "dyn_step.o"): a variant compiles just those units and links the main
+    build's objects for the rest."""
     out, objdir = OUT, OBJDIR
     if variant:
         out = os.path.join(HERE, "exp", f"liblbsim_{variant}.so")
@@ -70,9 +72,11 @@ def build_library(force: bool = False, verbose: bool = False, jobs: int = 0,
     os.makedirs(objdir, exist_ok=True)
     os.makedirs(os.path.dirname(out), exist_ok=True)
     jobs = jobs or min(len(UNITS), os.cpu_count() or 1, 16)
-    units = [(src, [*defs, *defines], os.path.join(objdir, obj)) for src, defs, obj in UNITS]
+    units = [(src, [*defs, *defines], os.path.join(objdir, obj)) for src, defs, obj in UNITS
+             if not (variant and only) or obj in only]
     with ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda u: _compile(u, verbose), units))
+        built = dict(zip([u[2] for u in units], ex.map(lambda u: _compile(u, verbose), units)))
+    objs = [built.get(os.path.join(objdir, obj), os.path.join(OBJDIR, obj)) for _, _, obj in UNITS]
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp", *objs]
     if verbose:
         print(" ".join(cmd), flush=True)
@@ -85,4 +89,6 @@ if __name__ == "__main__":
     args = sys.argv[1:]
     variant = args[args.index("--variant") + 1] if "--variant" in args else None
     defines = tuple(a for a in args if a.startswith("-D"))
-    print(build_library(force="--force" in args, verbose=True, variant=variant, defines=defines))
+    only = tuple(args[args.index("--only") + 1].split(",")) if "--only" in args else ()
+    print(build_library(force="--force" in args, verbose=True, variant=variant, defines=defines,
+                        only=only))

@@ -161,18 +161,24 @@ int validate(const lbsim_config_t* c, char* msg, size_t n) {
   if (!(c->lost_fin_prob >= 0.0f) || !(c->lost_fin_prob <= 1.0f))
     return bad("lost_fin_prob must be in [0, 1]");
   if (c->lost_fin_prob > 0.0f) {
-    if (!(c->flow_timeout_s >= 0.0f) || !(c->flow_timeout_s <= 3600.0f))
-      return bad("flow_timeout_s must be in [0, 3600]");
-    if (c->flow_buckets < 1 || (double)c->flow_buckets / (double)c->arrival_rate > 100.0)
-      return bad("flow_buckets must be >= 1 with flow_buckets / arrival_rate <= 100 s");
-    // the guess fct + (flow_timeout - 40 s) + wait is a signed int32 us sample: with the wait
-    // <= 16.7 x its mean (24-bit uniforms) and an fct of at most ~1,070 s (64 queued flows of
-    // <= 16.7 s service each at >= 1 flow/s), <= 1000 s for the other two terms keeps it below
-    // 2^31 us (lost_fct also saturates, for trace work beyond that bound)
-    if ((double)c->flow_timeout_s - 40.0 +
-            16.7 * (double)c->flow_buckets / (double)c->arrival_rate > 1000.0)
-      return bad("lost-FIN: flow_timeout_s - 40 + 16.7 * flow_buckets / arrival_rate must be "
-                 "<= 1000 s (the guessed fct is a signed 32-bit us sample)");
+    if (!(c->flow_timeout_s >= 0.0f)) return bad("flow_timeout_s must be >= 0");
+    if (c->flow_buckets < 1) return bad("flow_buckets must be >= 1");
+    // the guess fct + (flow_timeout - 40 s) + wait and its wrap-up delay flow_timeout + wait are
+    // signed int32 us: with the wait <= 16.7 x its mean flow_buckets / arrival_rate (24-bit
+    // uniforms) and an fct of at most ~1,070 s (64 queued flows of <= 16.7 s service each at
+    // >= 1 flow/s), flow_timeout + 16.7 x the mean wait <= 1040 s keeps both below 2^31 us
+    // (lost_fct also saturates, for trace work beyond that bound)
+    const double wmean = (double)c->flow_buckets / (double)c->arrival_rate;
+    if ((double)c->flow_timeout_s + 16.7 * wmean > 1040.0) {
+      if ((double)c->flow_timeout_s >= 1040.0)
+        return bad("lost-FIN: flow_timeout_s must be < 1040 s (got %.1f)", c->flow_timeout_s);
+      return bad("lost-FIN: flow_timeout_s + 16.7 * flow_buckets / arrival_rate must be <= 1040 s "
+                 "(signed 32-bit us guesses): with flow_timeout_s = %.1f, flow_buckets / "
+                 "arrival_rate must be <= %.3f s (got %.3f)",
+                 c->flow_timeout_s, (1040.0 - (double)c->flow_timeout_s) / 16.7, wmean);
+    }
+    if (c->lost_fin_pending < 1 || c->lost_fin_pending > 4096)
+      return bad("lost_fin_pending must be in [1, 4096]");
   }
   if (c->lost_fin_prob > 0.0f && std::llround((double)c->lost_fin_prob * 16777216.0) == 0)
     return bad("lost_fin_prob must be 0 or >= 2^-25 (a 24-bit threshold)");
@@ -184,6 +190,8 @@ int validate(const lbsim_config_t* c, char* msg, size_t n) {
     return bad("unknown duration_mode %d", c->duration_mode);
   if (c->n_flow_on_mode != LBSIM_NFLOW_QUEUE && c->n_flow_on_mode != LBSIM_NFLOW_VPP)
     return bad("unknown n_flow_on_mode %d", c->n_flow_on_mode);
+  if (c->reservoir_mode != LBSIM_RESERVOIR_ALGR && c->reservoir_mode != LBSIM_RESERVOIR_VPP)
+    return bad("unknown reservoir_mode %d", c->reservoir_mode);
   if (!(c->recover_prob >= 0.0f) || !(c->recover_prob <= 1.0f))
     return bad("recover_prob must be in [0, 1]");
   if (c->dyn_mapping == LBSIM_DYN_ENV_PER_LANE && c->num_servers > 16)
@@ -229,6 +237,9 @@ void derive_params(const lbsim_config_t& c, SimParams& p) {
   p.next_reset = c.next_step_reset ? 1 : 0;
   p.dur_service = c.duration_mode == LBSIM_DURATION_SERVICE ? 1 : 0;
   p.leak = (c.n_flow_on_mode == LBSIM_NFLOW_VPP && p.lf_thr != 0u) ? 1 : 0;
+  p.split = p.lf_thr != 0u ? 1 : 0;
+  p.pend_P = p.split ? c.lost_fin_pending : 0;
+  p.res_vpp = c.reservoir_mode == LBSIM_RESERVOIR_VPP ? 1 : 0;
 }
 
 // Whether a handle keeps a duration plane (DevState::res_dur): duration_mode SERVICE (the service
@@ -259,8 +270,15 @@ std::vector<Section> sections(lbsim_t* h) {
   }
   if (h->cfg.fail_prob > 0.0f) v.push_back({(void**)&s.down, BS * 4});
   if (h->prm.leak) v.push_back({(void**)&s.lost_on, BS * 4});
-  // the duration plane: only when a flow's duration sample can differ from its fct
-  if (dur_plane(h->prm)) v.push_back({(void**)&s.res_dur, BSK * 4});
+  // the duration plane: only when a flow's duration sample can differ from its fct; split
+  // handles (lost-FIN): {us, ts} records, the duration count, the pending guesses, lf_over
+  if (dur_plane(h->prm)) v.push_back({(void**)&s.res_dur, BSK * (h->prm.split ? 8 : 4)});
+  if (h->prm.split) {
+    v.push_back({(void**)&s.res_count_dur, BS * 4});
+    v.push_back({(void**)&s.pend_hc, BS * 4});
+    v.push_back({(void**)&s.pend, BS * (size_t)h->prm.pend_P * 8});
+    v.push_back({(void**)&s.lf_over, B * 4});
+  }
   return v;
 }
 
@@ -453,6 +471,9 @@ bool use_step_wave(const lbsim_t* h) {
 bool use_fused_step(const lbsim_t* h) {
   // AUTO = SPLIT: the fused kernel measured slower at every shape tried
   if (step_kernel_of(h) != LBSIM_STEP_FUSED || h->prm.next_reset) return false;
+  // full handles (dynamics_group_full_kernel: leak, a duration plane, lost-FIN deferral,
+  // reservoir_mode VPP) step in the two launches
+  if (h->prm.leak || dur_plane(h->prm) || h->prm.res_vpp) return false;
   const int g = dyn_group_lanes(ctx(h));
   return g >= 2 && g <= 16;
 }
@@ -523,6 +544,8 @@ int lbsim_config_default(lbsim_config_t* c) {
   c->fail_prob = 0.0f;
   c->recover_prob = 0.1f;
   c->duration_mode = LBSIM_DURATION_AGE;  // lbhash.h:129-136: the flow's age
+  c->lost_fin_pending = 256;
+  c->reservoir_mode = LBSIM_RESERVOIR_ALGR;
   return LBSIM_OK;
 }
 

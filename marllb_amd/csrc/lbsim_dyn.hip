@@ -41,6 +41,17 @@ void launch_dyn_group(const LaunchCtx& L, const void* action, int dtype, int32_t
   SimParams prm = L.prm;
   prm.dyn_epw = epw;
   const dim3 block(64), grid((unsigned)((L.B + epw - 1) / epw));
+  // a full handle (n_flow_on_mode VPP, a duration plane, lost-FIN deferral, reservoir_mode VPP):
+  // the kernel with every feature's code (group_event_loop FULL), its own register budget
+  if (L.prm.leak || L.st.res_dur != nullptr || L.prm.res_vpp) {
+    if (L.prm.trace)
+      LBSIM_LAUNCH((dynamics_group_full_kernel<G, MODE, POLICY, true>), grid, block, 0, stream,
+                   L.st, prm, action, dtype, assign, mask);
+    else
+      LBSIM_LAUNCH((dynamics_group_full_kernel<G, MODE, POLICY, false>), grid, block, 0, stream,
+                   L.st, prm, action, dtype, assign, mask);
+    return;
+  }
   // the step of a next-step auto-reset handle inlines the event loop twice (the reset's warm-up
   // and the step): unconstrained it took 133-137 VGPRs, 3 waves per SIMD, and ran 190 us against
   // the plain step's 149 at 65536 x 4 (profiles/r06b/modes): held to the 4-wave budget

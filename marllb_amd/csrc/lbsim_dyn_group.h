@@ -127,6 +127,12 @@ struct SrvLane {
   float score, scale;
   double den, rcp;
   bool act;  // s < S
+  // split handles (lost-FIN, SimParams::split): the duration reservoir's count, the pending
+  // guesses' ring head / count, the head entry's due word (absolute us mod 2^32), and the guesses
+  // this lane dropped at a full ring in this launch
+  uint32_t rcnt_d;
+  int32_t phead, pcnt;
+  uint32_t pdue, over;
 };
 
 // ALIAS table of the group in LDS: word f of active position k at [f][gbase + k].  Every lane of
@@ -136,6 +142,102 @@ struct GroupAliasTab {
   int gbase;
   __device__ int32_t& operator()(int f, int k) const { return t[f * 64 + gbase + k]; }
 };
+
+// ---- split handles (lost-FIN; oracle split_add / pend_push / pend_flush): the
+//      fct and duration reservoirs of a server make their own decisions, and a timed-out flow's
+//      guess waits in the server's pending ring (HBM, sorted by due time) until its wrap-up.
+//      Rare paths of the general event loop: a lane loops on its own.
+// One sample into the fct (is_dur false) or duration reservoir of server row sb: own count, own
+// slot (res_slot; the duration reservoir draws as a run without losses would, the fct
+// reservoir's stream word carries 1 << 16), {us, ts} record; a
+// carried-in or deferred sample (!has_r) sets the big flag at its store.
+__device__ __forceinline__ void split_add(const DevState& st, const SimParams& p, SrvLane& V,
+                                          uint32_t sb, uint32_t gid, uint32_t episode, int s,
+                                          bool is_dur, uint32_t v, uint32_t ts_ms, bool has_r,
+                                          uint32_t r) {
+  const uint32_t c = is_dur ? V.rcnt_d : V.rcnt;
+  const int slot = res_slot(p, c, has_r, r, gid, episode,
+                            (kStreamReservoir << 24) | (is_dur ? 0u : 1u << 16) | (uint32_t)s);
+  if (slot >= 0) {
+    if (!has_r && v >= kPackLimit) V.big = true;
+    uint2* rec = is_dur ? reinterpret_cast<uint2*>(st.res_dur) : st.res;
+    rec[(size_t)sb * K + (uint32_t)slot] = make_uint2(v, ts_ms);
+    atomicOr(V.chgw + ((uint32_t)slot >> 5) * 64u, 1u << (slot & 31));
+  }
+  if (is_dur) V.rcnt_d = count_inc(c);
+  else V.rcnt = count_inc(c);
+}
+// The guesses due by step time t (relative us) into the fct reservoir, in due order, each stamped
+// with its due time (lbhash.h:182-217: the bucket's next flow records now - t_init - 40 s).
+__device__ __forceinline__ void split_flush(const DevState& st, const SimParams& p, SrvLane& V,
+                                            uint32_t sb, uint32_t gid, uint32_t episode, int s,
+                                            int32_t t, uint64_t base_us) {
+  const int P = p.pend_P;
+  const uint2* ring = st.pend + (size_t)sb * (uint32_t)P;
+  while (V.pcnt > 0) {
+    const int32_t rel = (int32_t)(V.pdue - (uint32_t)base_us);
+    if (rel > t) break;
+    const uint32_t val = ring[V.phead].y;
+    const uint32_t ts = (uint32_t)((uint64_t)((int64_t)base_us + (int64_t)rel) / 1000u);
+    split_add(st, p, V, sb, gid, episode, s, false, val, ts, false, 0u);
+    V.phead = V.phead + 1 == P ? 0 : V.phead + 1;
+    V.pcnt -= 1;
+    if (V.pcnt > 0) V.pdue = ring[V.phead].x;
+  }
+}
+// A guess due at `due` into the sorted ring (insertion from the tail; an equal due goes after
+// the entries already there); a full ring drops it (V.over, summed into lf_over).
+__device__ __forceinline__ void split_push(const DevState& st, const SimParams& p, SrvLane& V,
+                                           uint32_t sb, uint32_t due, uint32_t val) {
+  const int P = p.pend_P;
+  if (V.pcnt == P) {
+    V.over += 1u;
+    return;
+  }
+  uint2* ring = st.pend + (size_t)sb * (uint32_t)P;
+  int i = V.pcnt;
+  while (i > 0) {
+    int pos = V.phead + i - 1;
+    pos = pos >= P ? pos - P : pos;
+    const uint2 e = ring[pos];
+    if ((int32_t)(e.x - due) <= 0) break;
+    ring[pos + 1 == P ? 0 : pos + 1] = e;
+    --i;
+  }
+  int pos = V.phead + i;
+  pos = pos >= P ? pos - P : pos;
+  ring[pos] = make_uint2(due, val);
+  V.pcnt += 1;
+  if (i == 0) V.pdue = due;
+}
+// A flow completing at tc (arrived at ta; relative us) on a split handle (oracle pop_until): the
+// guesses due by tc, its duration sample now (lbhash.h:129-136), then its fct -- now (RSTACK,
+// :116-124) or, lost, as a guess due at tc + flow_timeout + the bucket wait (:182-192, :204-213).
+__device__ __forceinline__ void split_complete(const DevState& st, const SimParams& p, SrvLane& V,
+                                               uint32_t sb, uint32_t gid, uint32_t episode, int s,
+                                               int32_t tc, int32_t ta, uint32_t dur, uint32_t ts_ms,
+                                               bool has_r, uint32_t r, uint64_t base_us) {
+  split_flush(st, p, V, sb, gid, episode, s, tc, base_us);
+  split_add(st, p, V, sb, gid, episode, s, true, dur, ts_ms, has_r, r);
+  int32_t wait = 0;
+  if (lf_wait(p, (uint32_t)base_us + (uint32_t)ta, gid, episode, wait))
+    split_push(st, p, V, sb,
+               (uint32_t)base_us + (uint32_t)tc + (uint32_t)(p.lf_off_us + 40000000) +
+                   (uint32_t)wait,
+               lf_guess((uint32_t)(tc - ta), p.lf_off_us, wait));
+  else
+    split_add(st, p, V, sb, gid, episode, s, false, (uint32_t)(tc - ta), ts_ms, has_r, r);
+}
+// reservoir_mode VPP: the server's bins zeroed (reset, failure; VPP's zeroed shm).
+__device__ __forceinline__ void vpp_zero_bins(const DevState& st, const SimParams& p, uint32_t sb) {
+  uint4* r4 = reinterpret_cast<uint4*>(st.res + (size_t)sb * K);
+  for (int i = 0; i < K / 2; ++i) r4[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (st.res_dur != nullptr) {
+    const int n4 = p.split ? K / 2 : K / 4;
+    uint4* d4 = reinterpret_cast<uint4*>(st.res_dur + (size_t)sb * K * (p.split ? 2u : 1u));
+    for (int i = 0; i < n4; ++i) d4[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
+}
 
 // Loop constants of one step: the Philox keys and the scalars the loop reads, pinned in VGPRs so
 // the loop never reloads them from the kernarg segment.  Only the two base keys are kept: round
@@ -165,7 +267,11 @@ __device__ __forceinline__ GroupConst group_const(const SimParams& p, uint32_t b
 // draw-ahead block (kModeStepNR: the compiler otherwise hoists them into 20 loop-long VGPRs,
 // which took that kernel past the 4-wave budget); the plain step lets them be hoisted (measured
 // 4 us faster at 65536 x 4 than forming them in the block, profiles/r06c/).
-template <int G, int POLICY, bool TRACE, bool FAST, bool KEYS = false>
+// FULL: the handle's features beyond the plain simulator -- n_flow_on_mode VPP's lost-flow counts,
+// a duration plane (duration_mode SERVICE), lost-FIN deferral (split reservoirs), reservoir_mode
+// VPP -- compiled only into dynamics_group_full_kernel, so none of their registers weigh on the
+// plain kernel (126 VGPRs, 4 waves per SIMD; with them inlined it took 164).
+template <int G, int POLICY, bool TRACE, bool FAST, bool KEYS = false, bool FULL = false>
 __device__ __forceinline__ void group_event_loop(const DevState& st, const SimParams& p,
                                                  LaneState<1>& E, SrvLane& V, int s, int gbase,
                                                  int n_alias, const GroupConst& gc, int2* win,
@@ -233,7 +339,7 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
     const bool arrival_due = E.next_arr < dt;  // the same in every lane of the group
     const int32_t th = arrival_due ? E.next_arr : dt;
     const bool due = V.act && V.cnt > 0 && V.head_tc <= th;
-    if constexpr (!FAST) {  // n_flow_on_mode VPP: a popped lost-FIN flow stays in n_flow_on
+    if constexpr (FULL) {  // n_flow_on_mode VPP: a popped lost-FIN flow stays in n_flow_on
       if (p.leak && due &&
           lf_lost(p, gc.base_ms * 1000u + gc.base_rem + (uint32_t)wslot(V.lh)->y, E.gid, E.episode))
         V.lost += 1;
@@ -252,6 +358,8 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
     V.cnt -= due ? 1 : 0;
     V.head = due ? ((V.head + 1 == Q) ? 0 : V.head + 1) : V.head;
     V.lh = due ? nl : V.lh;
+    // (computing the choice key here, before the next head's LDS read is waited for, measured
+    // 3 us slower at 65536 x 4, profiles/r06e/)
     V.head_tc = due ? nt : V.head_tc;
     const bool more = group_bits<G>(__ballot(due && V.cnt > 0 && nt <= th), gbase) != 0ull;
     if (!arrival_due && !more) break;  // group-uniform
@@ -262,7 +370,7 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
     if constexpr (!alias) {
       // the data plane's n_flow_on: the queue, plus the lost-FIN flows it never decremented
       // (n_flow_on_mode VPP only: the general loop; V.lost = 0 otherwise)
-      const int32_t nfo = FAST ? V.cnt : V.cnt + V.lost;
+      const int32_t nfo = FULL ? V.cnt + V.lost : V.cnt;
       if constexpr (lsq) {
         V.score = (float)nfo;
       } else {  // (cnt + 1) / den correctly rounded (Markstein), division for den 0 / inf / NaN
@@ -323,18 +431,30 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
     const bool ins = mine && tc_a <= dt;  // completes in this step: its sample now
 
     // ---- the pushed flow's Algorithm R draw is this arrival's word r (E.u3)
-    const int slot = reservoir_slot_r32(V.rcnt, E.u3);
-    if (ins && slot >= 0) {
-      const uint32_t fct = lost_fct(p, (uint32_t)(tc_a - ta),
-                                    gc.base_ms * 1000u + gc.base_rem + (uint32_t)ta, E.gid, E.episode);
+    const int slot = (FULL && p.res_vpp) ? (int)(E.u3 >> 25) : reservoir_slot_r32(V.rcnt, E.u3);
+    bool split = false;  // split handles (lost-FIN): their own inserts (split_complete)
+    if constexpr (FULL) {
+      split = p.split != 0;
+      if (split && ins) {
+        const uint64_t base_us = (uint64_t)gc.base_ms * 1000u + gc.base_rem;
+        split_complete(st, p, V, (uint32_t)((size_t)(my_res - st.res) / K), E.gid, E.episode, s,
+                       tc_a, ta, p.dur_service ? (uint32_t)svc : (uint32_t)(tc_a - ta),
+                       gc.base_ms + (gc.base_rem + (uint32_t)tc_a) / 1000u, true, E.u3, base_us);
+      }
+    }
+    if (!split && ins && slot >= 0) {
+      // lost-FIN flows only on split handles: fct = tc - ta here
+      const uint32_t fct = (uint32_t)(tc_a - ta);
       my_res[(uint32_t)slot] = make_uint2(fct, gc.base_ms + (gc.base_rem + (uint32_t)tc_a) / 1000u);
-      if constexpr (!FAST) {  // the duration plane (sim_step_group sends its handles here):
+      if constexpr (FULL) {  // the duration plane:
         if (st.res_dur != nullptr)  // the age tc - ta, or the service time svc = tc - start
           st.res_dur[(size_t)(my_res - st.res) + (uint32_t)slot] =
               p.dur_service ? (uint32_t)svc : (uint32_t)(tc_a - ta);
       }
       mark(slot);
     }
+    // (a branch-free push, non-pushing lanes storing to scratch slots, measured 3 us slower at
+    // 65536 x 4, profiles/r06e/)
     if (mine) {
       const int2 e = make_int2(tc_a, ta);
       if (V.cnt < WL) {
@@ -349,7 +469,7 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
       V.assigned += 1;
       V.head_tc = V.cnt == 0 ? tc_a : V.head_tc;
       V.cnt += 1;
-      V.rcnt = ins ? count_inc(V.rcnt) : V.rcnt;
+      V.rcnt = (ins && !split) ? count_inc(V.rcnt) : V.rcnt;
     }
 
     // ---- next arrival (identical in every lane of the group): arrival arr_idx + 1 from the
@@ -365,7 +485,7 @@ __device__ __forceinline__ void group_event_loop(const DevState& st, const SimPa
   }
 }
 
-template <int G, int POLICY, bool TRACE, bool KEYS = false>
+template <int G, int POLICY, bool TRACE, bool KEYS = false, bool FULL = false>
 __device__ __forceinline__ void sim_step_group(const DevState& st, const SimParams& p,
                                                LaneState<1>& E, SrvLane& V, uint32_t b, int s,
                                                int gbase, float w_own, const float (&wall)[G],
@@ -413,6 +533,12 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
       V.big = false;
       mark(0);  // emptied: the next observe recomputes the (zero) features
       V.lost = 0;
+      if constexpr (FULL) {
+        V.rcnt_d = 0u;  // split: the duration reservoir and the pending guesses go too
+        V.pcnt = 0;
+        V.phead = 0;
+        if (p.res_vpp) vpp_zero_bins(st, p, sb);
+      }
     }
     V.qcap = fails ? 0 : (recovers ? Q : V.qcap);
   }
@@ -425,20 +551,31 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
     int32_t eta = wslot(V.lh)->y;
     int i = 0;
     for (;;) {
-      const u32x4 d = philox4x32_10(
-          u32x4{rc >> 1, E.gid, E.episode, (kStreamReservoir << 24) | (uint32_t)s}, p.key0, p.key1);
-      const int slot = reservoir_slot(rc, d);
-      if (slot >= 0) {
-        const uint32_t fct =
-            lost_fct(p, (uint32_t)(etc - eta), (uint32_t)base_us + (uint32_t)eta, E.gid, E.episode);
-        const uint32_t dur = dur_sample(p, etc, eta, eta > prev ? eta : prev);
-        V.big |= big_record(fct, dur);
-        store_record(st, (size_t)sb * K + (uint32_t)slot, fct, dur,
-                     base_ms + (base_rem + (uint32_t)etc) / 1000u);
-        mark(slot);
+      if (FULL && p.split) {  // lost-FIN: split reservoirs and deferred guesses (split_complete)
+        split_complete(st, p, V, sb, E.gid, E.episode, s, etc, eta,
+                       dur_sample(p, etc, eta, eta > prev ? eta : prev),
+                       base_ms + (base_rem + (uint32_t)etc) / 1000u, false, 0u, base_us);
+        rc = V.rcnt;
+      } else {
+        const u32x4 d = philox4x32_10(
+            u32x4{rc >> 1, E.gid, E.episode, (kStreamReservoir << 24) | (uint32_t)s}, p.key0,
+            p.key1);
+        // reservoir_mode VPP: slot rand() % 128 for every sample (res_slot)
+        const int slot =
+            (FULL && p.res_vpp) ? (int)(((rc & 1u) ? d.w : d.y) >> 25) : reservoir_slot(rc, d);
+        if (slot >= 0) {
+          // (lost-FIN flows only on split handles; the duration sample differs from the fct only
+          // under duration_mode SERVICE: a full handle)
+          const uint32_t fct = (uint32_t)(etc - eta);
+          const uint32_t dur = FULL ? dur_sample(p, etc, eta, eta > prev ? eta : prev) : fct;
+          V.big |= big_record(fct, dur);
+          store_record(st, (size_t)sb * K + (uint32_t)slot, fct, dur,
+                       base_ms + (base_rem + (uint32_t)etc) / 1000u);
+          mark(slot);
+        }
+        rc = count_inc(rc);
       }
       prev = etc;
-      rc = count_inc(rc);
       if (++i >= V.cnt) break;
       int2 e;
       if (i < WL) {
@@ -461,12 +598,18 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
   const GroupConst gc = group_const(p, base_ms, base_rem);
   const bool finite = lsq || alias || !V.act ||
                       (fabs(V.den) >= 1e-30 && fabs(V.den) <= 1e300);  // false for NaN
-  if (__all(finite) && !p.leak && st.res_dur == nullptr)
+  if constexpr (FULL) {  // (a full handle always runs the general loop)
+    group_event_loop<G, POLICY, TRACE, false, KEYS, true>(st, p, E, V, s, gbase, n_alias, gc, win,
+                                                          atab, acache, my_res, my_ring);
+    // split handles: the guesses due by the step's end (oracle sim_step)
+    if (p.split && V.act) split_flush(st, p, V, sb, E.gid, E.episode, s, dt, base_us);
+  } else if (__all(finite)) {
     group_event_loop<G, POLICY, TRACE, true, KEYS>(st, p, E, V, s, gbase, n_alias, gc, win, atab,
                                                    acache, my_res, my_ring);
-  else
+  } else {
     group_event_loop<G, POLICY, TRACE, false, KEYS>(st, p, E, V, s, gbase, n_alias, gc, win, atab,
                                                     acache, my_res, my_ring);
+  }
 
   // ---- rebase to the next step's start (this lane's server)
   E.next_arr -= dt;
@@ -505,7 +648,7 @@ struct DynGroupLds {
 // One step (or reset) of the 64 / G envs of wave `wave` (env b = wave * 64 / G + lane / G), lane s
 // of a group owning server s: state in, the event loop, state back to HBM.  Lanes of envs past B
 // (or outside the reset mask) return at once, whole groups together.
-template <int G, int MODE, int POLICY, bool TRACE>
+template <int G, int MODE, int POLICY, bool TRACE, bool FULL = false>
 __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimParams& p,
                                                const void* action, int action_dtype,
                                                int32_t* assign_out, const uint8_t* reset_mask,
@@ -533,6 +676,8 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
   E.gid = p.env_id_offset + b;
   SrvLane V;
   V.act = s < S;
+  V.over = 0u;
+  uint32_t lfo_base = 0u;  // split: the env's lf_over at launch start (0 after a reset)
   V.scale = p.svc_scale[0];
 #pragma unroll
   for (int k = 1; k < G; ++k) V.scale = (k == s) ? p.svc_scale[k] : V.scale;
@@ -563,6 +708,14 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
     V.qcap = Q;  // every server is up at the episode start
     V.big = false;
     V.lost = 0;  // n_flow_on_mode VPP: no lost flows yet
+    V.rcnt_d = 0u;  // split: empty duration reservoir, no pending guesses
+    V.phead = 0;
+    V.pcnt = 0;
+    V.pdue = 0u;
+    lfo_base = 0u;
+    if constexpr (FULL) {
+      if (p.res_vpp && V.act) vpp_zero_bins(st, p, sb);  // VPP's zeroed bins
+    }
     // emptied reservoirs: slot 0 marked written, so the next observe recomputes every server of
     // the env (its cached features are the last episode's)
     if (V.act) chgw[lane] = 1u;
@@ -587,9 +740,21 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
     V.qcap = Q;
     V.big = false;
     V.lost = 0;
+    V.rcnt_d = 0u;
+    V.phead = 0;
+    V.pcnt = 0;
+    V.pdue = 0u;
+    if (FULL && p.split) lfo_base = st.lf_over[b];
     if (V.act) {
       if (st.down != nullptr && st.down[sb] != 0u) V.qcap = 0;
-      if (p.leak) V.lost = (int32_t)st.lost_on[sb];
+      if (FULL && p.leak) V.lost = (int32_t)st.lost_on[sb];
+      if (FULL && p.split) {
+        V.rcnt_d = st.res_count_dur[sb];
+        const uint32_t ph = st.pend_hc[sb];
+        V.phead = (int32_t)(ph & 0xFFFFu);
+        V.pcnt = (int32_t)(ph >> 16);
+        if (V.pcnt > 0) V.pdue = st.pend[(size_t)sb * (uint32_t)p.pend_P + (uint32_t)V.phead].x;
+      }
       const uint32_t hc = st.hc[sb];
       V.head = (int)(hc & kHcHead);
       V.big = (hc & kHcBig) != 0u;
@@ -624,11 +789,13 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
   };
   if constexpr (MODE == kModeStep) {
     load_in();
-    sim_step_group<G, POLICY, TRACE>(st, p, E, V, b, s, gbase, w_own, wall, win, atab, acache);
+    sim_step_group<G, POLICY, TRACE, false, FULL>(st, p, E, V, b, s, gbase, w_own, wall, win, atab,
+                                                  acache);
   } else if constexpr (MODE == kModeReset) {
     reset_in();
     for (int k = 0; k < p.warmup_steps; ++k)
-      sim_step_group<G, POLICY, TRACE>(st, p, E, V, b, s, gbase, 1.0f, wall, win, atab, acache);
+      sim_step_group<G, POLICY, TRACE, false, FULL>(st, p, E, V, b, s, gbase, 1.0f, wall, win,
+                                                    atab, acache);
     reset_out(0);
   } else {
     // kModeStepNR (next-step auto-reset): an env whose last step returned done resets in place of
@@ -643,7 +810,8 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
     const int nsteps = rs ? p.warmup_steps : 1;
     const float w = rs ? 1.0f : w_own;
     for (int k = 0; k < nsteps; ++k)
-      sim_step_group<G, POLICY, TRACE, true>(st, p, E, V, b, s, gbase, w, wall, win, atab, acache);
+      sim_step_group<G, POLICY, TRACE, true, FULL>(st, p, E, V, b, s, gbase, w, wall, win, atab,
+                                                   acache);
     if (rs) reset_out(-1);
   }
 
@@ -660,18 +828,25 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
       const uint32_t cw[4] = {chgw[lane], chgw[64 + lane], chgw[128 + lane], chgw[192 + lane]};
       __builtin_amdgcn_s_waitcnt(0);  // the wave's stores acknowledged by L2 (vmcnt 0)
       __asm__ volatile("" ::: "memory");
-      V.big |= big_written(st, sb, cw, V.rcnt);
+      V.big |= big_written(st, sb, cw, V.rcnt, V.rcnt_d);
+    }
+    if (FULL && p.split) {
+      st.res_count_dur[sb] = V.rcnt_d;
+      st.pend_hc[sb] = (uint32_t)V.phead | ((uint32_t)V.pcnt << 16);
     }
     st.hc[sb] = (uint32_t)V.head | (V.big ? kHcBig : 0u) | ((uint32_t)V.cnt << 16);
     st.last_tc[sb] = V.last;
     st.res_count[sb] = V.rcnt;
     if (st.down != nullptr) st.down[sb] = V.qcap == 0 ? 1u : 0u;
-    if (p.leak) st.lost_on[sb] = (uint32_t)V.lost;
+    if (FULL && p.leak) st.lost_on[sb] = (uint32_t)V.lost;
     *reinterpret_cast<uint4*>(st.chg + (size_t)sb * 4) =
         make_uint4(chgw[lane], chgw[64 + lane], chgw[128 + lane], chgw[192 + lane]);
     if (MODE != kModeReset && assign_out != nullptr) assign_out[sb] = V.assigned;  // 0 if reset
   }
+  // split: the guesses this env's servers dropped at full rings (every lane of the group adds)
+  const uint32_t over = (FULL && p.split) ? group_add<G>(V.over) : 0u;
   if (s == 0) {
+    if (FULL && p.split) st.lf_over[b] = lfo_base + over;
     st.episode[b] = E.episode;
     st.clock[b] = E.clock;
     st.dropped[b] = E.dropped;
@@ -694,6 +869,18 @@ __global__ void __launch_bounds__(64, WAVES)
   __shared__ DynGroupLds<POLICY> L;
   dyn_group_wave<G, MODE, POLICY, TRACE>(st, p, action, action_dtype, assign_out, reset_mask,
                                          blockIdx.x, (int)threadIdx.x, L);
+}
+
+// The same for a full handle (group_event_loop's FULL: n_flow_on_mode VPP, a duration plane,
+// lost-FIN deferral, reservoir_mode VPP): the general event loop with every feature, on its own
+// register budget.
+template <int G, int MODE, int POLICY, bool TRACE>
+__global__ void __launch_bounds__(64)
+    dynamics_group_full_kernel(DevState st, SimParams p, const void* action, int action_dtype,
+                               int32_t* assign_out, const uint8_t* reset_mask) {
+  __shared__ DynGroupLds<POLICY> L;
+  dyn_group_wave<G, MODE, POLICY, TRACE, true>(st, p, action, action_dtype, assign_out,
+                                               reset_mask, blockIdx.x, (int)threadIdx.x, L);
 }
 
 }  // namespace lbk

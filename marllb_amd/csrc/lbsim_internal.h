@@ -47,7 +47,9 @@ struct LaunchCtx {
 // lanes: 4096 x 4 0.0908 -> 0.0894 ms, 8192 x 4 0.0962 -> 0.0947
 // (profiles/r02_round2b/ab_group_lanes_small.txt); slower from 16384 envs on.
 inline int dyn_group_lanes(const LaunchCtx& L) {
-  if (L.dyn_mapping == LBSIM_DYN_ENV_PER_LANE && L.S <= 16) return 0;
+  // (split lost-FIN handles and reservoir_mode VPP run the server-per-lane kernel only)
+  if (L.dyn_mapping == LBSIM_DYN_ENV_PER_LANE && L.S <= 16 && !L.prm.split && !L.prm.res_vpp)
+    return 0;
   static const int forced = [] {
     const char* e = std::getenv("LBSIM_DYN_GROUP_LANES");
     return e ? std::atoi(e) : 0;
@@ -82,8 +84,9 @@ inline bool dyn_wave_fits(const LaunchCtx& L) {
   static const bool forced_lanes = std::getenv("LBSIM_DYN_GROUP_LANES") != nullptr;
   if (dyn_wave_mode() == 0 || forced_lanes || L.dyn_mapping == LBSIM_DYN_ENV_PER_LANE) return false;
   if (L.S > 8 || L.prm.Q > 32 || L.prm.policy == LBSIM_POLICY_ALIAS) return false;
-  // server failures, n_flow_on_mode VPP's lost-flow counts: the group / env-lane kernels
-  return L.prm.fail_thr == 0u && L.prm.leak == 0;
+  // server failures, n_flow_on_mode VPP's lost-flow counts: the group / env-lane kernels; lost-FIN
+  // deferral (split reservoirs, pending guesses) and reservoir_mode VPP: the group kernel
+  return L.prm.fail_thr == 0u && L.prm.leak == 0 && L.prm.split == 0 && L.prm.res_vpp == 0;
 }
 
 inline bool dyn_wave_ok(const LaunchCtx& L) {

@@ -76,6 +76,15 @@ struct DevState {
   // flows of server s completed since the episode start / its last failure, never decremented
   // (lbhash.h:193,214); observation column 0 adds it (n_flow_on)
   uint32_t* lost_on;
+  // lost-FIN deferral (SimParams::split, else nullptr): the duration reservoir's
+  // own count [B*S] (res_dur is then [B*S*K] {duration us, timestamp ms} records, read as uint2),
+  // each server's pending timed-out fct guesses [B*S*P] {due us mod 2^32 (absolute: clock * dt +
+  // t), guess us} sorted by due time with pend_hc = head | count << 16 [B*S], and lf_over [B]:
+  // guesses dropped at a full ring this episode
+  uint32_t* res_count_dur;
+  uint32_t* pend_hc;
+  uint2* pend;
+  uint32_t* lf_over;
   // stateless features API only: caller's separate value / timestamp arrays [n*K]
   const uint32_t* feat_vals;
   const uint32_t* feat_ts;
@@ -129,6 +138,12 @@ struct SimParams {
   int32_t dur_service;
   // n_flow_on_mode VPP and lost-FIN on: count the lost flows per server (DevState::lost_on)
   int32_t leak;
+  // lost-FIN on: split fct / duration reservoirs and deferred guesses (DevState::pend), P entries
+  // per server; the wrap-up delay of a guess is lf_off_us + 40 s + its wait
+  int32_t split, pend_P;
+  // reservoir_mode VPP: every sample overwrites slot rand() % 128 (lbhash.h:108,179), bins zeroed
+  // at reset / failure
+  int32_t res_vpp;
 };
 
 constexpr uint32_t kStreamFailure = 5u;  // Philox stream of the failure / recovery draws
@@ -152,20 +167,29 @@ __device__ __forceinline__ bool big_record(uint32_t fct, uint32_t dur) {
 // The record words are read device-coherent: in the wave kernel other lanes stored them.
 // sb: the (env, server) row; its duration words from the duration plane when the handle has one.
 __device__ __forceinline__ bool big_written(const DevState& st, size_t sb,
-                                            const uint32_t (&chg)[4], uint32_t count) {
+                                            const uint32_t (&chg)[4], uint32_t count,
+                                            uint32_t count_dur = 0u) {
   const uint32_t n = count < (uint32_t)K ? count : (uint32_t)K;
   const uint32_t* fs = reinterpret_cast<const uint32_t*>(st.res + sb * K);
-  const uint32_t* ds = st.res_dur != nullptr ? st.res_dur + sb * K : nullptr;
+  // a split handle's duration reservoir: {us, ts} records with their own count
+  const bool split = st.res_count_dur != nullptr;  // count_dur: the lane's register copy
+  const uint32_t cd = split ? count_dur : count;
+  const uint32_t nd = cd < (uint32_t)K ? cd : (uint32_t)K;
+  const uint32_t* ds = st.res_dur != nullptr ? st.res_dur + sb * K * (split ? 2u : 1u) : nullptr;
+  const uint32_t dstep = split ? 2u : 1u;
   bool big = false;
   for (int w = 0; w < 4; ++w) {
     uint32_t m = chg[w];
     while (m) {
       const uint32_t slot = 32u * (uint32_t)w + (uint32_t)__builtin_ctz(m);
       m &= m - 1u;
-      if (slot >= n) continue;
-      const uint32_t f = __hip_atomic_load(fs + 2 * slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t d = ds != nullptr ? __hip_atomic_load(ds + slot, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT) : f;
+      if (slot >= n && slot >= nd) continue;
+      const uint32_t f = slot < n ? __hip_atomic_load(fs + 2 * slot, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      const uint32_t d = slot >= nd ? 0u
+                         : (ds != nullptr ? __hip_atomic_load(ds + dstep * slot, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT)
+                                          : f);
       big |= big_record(f, d);
     }
   }
@@ -229,6 +253,18 @@ __device__ __forceinline__ uint32_t lost_fct(const SimParams& p, uint32_t fct, u
 __device__ __forceinline__ uint32_t dur_sample(const SimParams& p, int32_t tc, int32_t ta,
                                                int32_t start) {
   return (uint32_t)(tc - (p.dur_service ? start : ta));
+}
+
+// Lost or not, and the bucket wait in us (oracle lf_test), of the flow that arrived at abs_ta.
+__device__ __forceinline__ bool lf_wait(const SimParams& p, uint32_t abs_ta, uint32_t gid,
+                                        uint32_t episode, int32_t& wait) {
+  const uint32_t salt =
+      lf_mix(lf_mix(p.key0 ^ (episode * 0x9E3779B9u)) ^ gid ^ (p.key1 * 0x85EBCA6Bu));
+  const uint32_t h = lf_mix(abs_ta ^ salt);
+  if ((h >> 8) >= p.lf_thr) return false;
+  const uint32_t h2 = lf_mix(h ^ 0x6A09E667u);
+  wait = (int32_t)(-lb_logf(u01_open0(h2)) * p.lf_wait_us);
+  return true;
 }
 
 // Whether the flow that arrived at abs_ta is a lost-FIN flow (the test of lost_fct).
@@ -562,6 +598,20 @@ __device__ __forceinline__ int reservoir_slot(uint32_t cres, const u32x4& d) {
   const uint32_t lo = (cres & 1u) ? d.z : d.x;
   const uint64_t j = mulhi64_by_u33(hi, lo, (uint64_t)cres + 1u);
   return cres < (uint32_t)K ? (int)cres : (j < (uint64_t)K ? (int)j : -1);
+}
+
+// The slot one sample takes in a reservoir holding c samples (-1: not kept; oracle res_slot): ALGR
+// (reservoir.py:64-85) or VPP (every sample to slot rand() % 128, lbhash.h:108,179: the top 7
+// bits of the draw).  A flow that arrived in this step (has_r) draws with its arrival's word r;
+// otherwise the reservoir stream's block (c >> 1), half (c & 1), counter word w3.
+__device__ __forceinline__ int reservoir_slot_r32(uint32_t cres, uint32_t r);
+__device__ __forceinline__ int res_slot(const SimParams& p, uint32_t c, bool has_r, uint32_t r,
+                                        uint32_t gid, uint32_t episode, uint32_t w3) {
+  if (!p.res_vpp && c < (uint32_t)K) return (int)c;
+  if (has_r) return p.res_vpp ? (int)(r >> 25) : reservoir_slot_r32(c, r);
+  const u32x4 d = philox4x32_10(u32x4{c >> 1, gid, episode, w3}, p.key0, p.key1);
+  if (p.res_vpp) return (int)(((c & 1u) ? d.w : d.y) >> 25);
+  return reservoir_slot(c, d);
 }
 
 // Algorithm R slot of a flow that arrives and completes in the same step: the draw is its arrival's
@@ -1778,47 +1828,34 @@ __device__ __forceinline__ bool observe_chunk_full(const DevState& st, const Sim
 // path cannot take (one copy of the code instead of two more register-path instantiations: fewer
 // SGPR / VGPR spills in observe_pair_kernel, 131 -> 125 us at 65536 x 4, 241 -> 229 us at
 // 65536 x 8, profiles/r05f/; LBSIM_OBS_PAIR_FALLBACK_REGS=1 restores the full observe_chunk).
-template <bool US, bool INC, bool REGS = true>
-__device__ __forceinline__ void observe_chunk(const DevState& st, const SimParams& p, size_t b,
-                                              int s_base, int S, ObsScratch& sc, float* obs_out,
-                                              int lane) {
+// The general path of observe_chunk (LDS image of the reservoirs) for servers [s_base, s_base +
+// S) of env b.  Split handles (lost-FIN, DevState::res_count_dur) give the duration reservoir its
+// own count and timestamps, hence its own decay weights: reservoir r then uses weight row r (S <= 2
+// per call), else the server's row r >> 1.
+template <bool US>
+__device__ __forceinline__ void observe_chunk_general(const DevState& st, const SimParams& p,
+                                                      size_t b, int s_base, int S, ObsScratch& sc,
+                                                      float* obs_out, int lane) {
   const size_t srow = b * (size_t)p.S + (size_t)s_base;  // first (env, server) of the chunk
   const int R = 2 * S;
   const int g = lane >> 3, j = lane & 7;
-  // the register path's decision words, issued with the written-slot masks (no round trip of
-  // their own after the unchanged-chunk test)
-  uint32_t rc = 0u, hcw = 0u;
-  if constexpr (US) {
-    const size_t usb = srow + (size_t)((lane >> 4) < S ? (lane >> 4) : 0);
-    rc = st.res_count[usb];
-    hcw = st.hc[usb];
-  }
-  if constexpr (INC) {
-    const uint32_t w = lane < 4 * S ? st.chg[(srow + (size_t)(lane >> 2)) * 4 + (lane & 3)] : 0u;
-    if (!__any(w != 0u)) {  // no reservoir of the chunk changed: the cached features
-      for (int e = lane; e < S * NF; e += 64) {
-        const int s = e / NF, c = e - s * NF;
-        obs_out[s_base * NF + e] = c == 0 ? n_flow_on(st, srow + (size_t)s)
-                                          : st.fcache[(srow + (size_t)s) * 10 + (size_t)(c - 1)];
-      }
-      wave_sync();
-      return;
-    }
-  }
-  if constexpr (US && REGS) {
-    if (observe_chunk_full<INC>(st, p, b, s_base, S, sc, obs_out, lane, rc, hcw)) return;
-  }
+  const bool split = US && st.res_count_dur != nullptr;
+  const int wsh = split ? 0 : 1;  // reservoir r's weight row: r >> wsh
   // ---- phase 1: reservoirs into LDS, decay weights relative to each server's newest sample.
   //      Loads of 4 servers are issued before any is consumed (memory-level parallelism).
   for (int s0 = 0; s0 < S; s0 += 4) {
-    uint32_t f[4][2], d[4][2], t[4][2];
+    uint32_t f[4][2], d[4][2], t[4][2], td[4][2];
     int nn[4];
+    int nd[4];  // the duration reservoir's count (split handles; else nn)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {  // the counts first: one round trip, then every slot load
       const int s = s0 + u;
       const uint32_t rcl = st.res_count[srow + (size_t)(s < S ? s : 0)];  // branch-free loads
+      const uint32_t rcd = split ? st.res_count_dur[srow + (size_t)(s < S ? s : 0)] : rcl;
       const uint32_t rc = s < S ? rcl : 0u;
+      const uint32_t rd = s < S ? rcd : 0u;
       nn[u] = rc < (uint32_t)K ? (int)rc : K;
+      nd[u] = rd < (uint32_t)K ? (int)rd : K;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -1831,15 +1868,25 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
         if constexpr (US) {  // simulator: one 8-B record per slot (+ the duration plane)
           const bool dplane = st.res_dur != nullptr;
           const uint2 rec = v ? st.res[sb * K + slot] : make_uint2(0u, 0u);
-          // (the plane's load must not wait for the record: both issued, then the select)
-          const uint32_t dw = (v && dplane) ? st.res_dur[sb * K + slot] : 0u;
+          if (split) {  // the duration reservoir's own {us, ts} records
+            const bool vd = slot < nd[u];
+            const uint2 dr = vd ? reinterpret_cast<const uint2*>(st.res_dur)[sb * K + slot]
+                                : make_uint2(0u, 0u);
+            d[u][h] = dr.x;
+            td[u][h] = dr.y;
+          } else {
+            // (the plane's load must not wait for the record: both issued, then the select)
+            const uint32_t dw = (v && dplane) ? st.res_dur[sb * K + slot] : 0u;
+            d[u][h] = dplane ? dw : rec.x;
+            td[u][h] = rec.y;
+          }
           f[u][h] = rec.x;
-          d[u][h] = dplane ? dw : rec.x;
           t[u][h] = rec.y;
         } else {  // features API: one value array serves as both "fct" and "duration"
           f[u][h] = v ? st.feat_vals[sb * K + slot] : 0u;
           d[u][h] = f[u][h];
           t[u][h] = v ? st.feat_ts[sb * K + slot] : 0u;
+          td[u][h] = t[u][h];
         }
       }
     }
@@ -1848,16 +1895,23 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
       const int s = s0 + u;
       if (s < S) {
         const uint32_t newest = wave_max_u32(t[u][0] > t[u][1] ? t[u][0] : t[u][1], lane);
+        // split: the duration reservoir's weights from its own timestamps (weight row 2 s + 1)
+        const uint32_t newd =
+            split ? wave_max_u32(td[u][0] > td[u][1] ? td[u][0] : td[u][1], lane) : 0u;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int slot = lane + 64 * h;
           sc.vals[2 * s][slot] = f[u][h];
           sc.vals[2 * s + 1][slot] = d[u][h];
-          sc.wts[s][slot] = slot < nn[u] ? lb_exp2f((float)(newest - t[u][h]) * p.decay_c) : 0.0f;
+          sc.wts[split ? 2 * s : s][slot] =
+              slot < nn[u] ? lb_exp2f((float)(newest - t[u][h]) * p.decay_c) : 0.0f;
+          if (split)
+            sc.wts[2 * s + 1][slot] =
+                slot < nd[u] ? lb_exp2f((float)(newd - td[u][h]) * p.decay_c) : 0.0f;
         }
         if (lane == 0) {
           sc.n[2 * s] = nn[u];
-          sc.n[2 * s + 1] = nn[u];
+          sc.n[2 * s + 1] = nd[u];
         }
       }
     }
@@ -1876,7 +1930,7 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
     const int r = job0 + g;
     const int n = r < R ? sc.n[r] : 0;
     const uint32_t* a = sc.vals[r < R ? r : 0];
-    const float* w = sc.wts[r < R ? r >> 1 : 0];
+    const float* w = sc.wts[r < R ? r >> wsh : 0];
     double sw;
     const double svw = pairwise8x2<double>(n, j, sw, [&](int i, double& wi) {
       wi = (double)w[i];
@@ -1884,7 +1938,8 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
     });
     if (j == 0 && r < R) {
       sc.svw[r] = svw;
-      if ((r & 1) == 0) sc.swt[r >> 1] = sw;  // the two reservoirs of a server share w
+      // the two reservoirs of a server share w (split handles: each its own)
+      if (split || (r & 1) == 0) sc.swt[r >> wsh] = sw;
     }
   }
   wave_sync();
@@ -1899,7 +1954,7 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
     });
     if (j == 0 && r < R) {
       sc.sd[r] = n > 0 ? sqrtf(ss / (float)n) : 0.0f;
-      sc.md[r] = n > 0 ? (float)(sc.svw[r] / sc.swt[r >> 1]) : 0.0f;
+      sc.md[r] = n > 0 ? (float)(sc.svw[r] / sc.swt[r >> wsh]) : 0.0f;
     }
   }
   wave_sync();
@@ -1910,7 +1965,7 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
     const bool act = r < R;
     const int rr = act ? r : 0;
     const int n = act ? sc.n[r] : 0;
-    const float* wrow = sc.wts[rr >> 1];
+    const float* wrow = sc.wts[rr >> wsh];
     uint32_t* vrow = sc.vals[rr];
     // any initial placement sorts to the same keys; ties only permute equal keys, which changes
     // neither p90 nor the weighted p90 (exact integer cumsums), so load strided (bank-free)
@@ -2037,6 +2092,46 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
   wave_sync();
 }
 
+
+template <bool US, bool INC, bool REGS = true>
+__device__ __forceinline__ void observe_chunk(const DevState& st, const SimParams& p, size_t b,
+                                              int s_base, int S, ObsScratch& sc, float* obs_out,
+                                              int lane) {
+  const size_t srow = b * (size_t)p.S + (size_t)s_base;  // first (env, server) of the chunk
+  // the register path's decision words, issued with the written-slot masks (no round trip of
+  // their own after the unchanged-chunk test)
+  uint32_t rc = 0u, hcw = 0u;
+  if constexpr (US) {
+    const size_t usb = srow + (size_t)((lane >> 4) < S ? (lane >> 4) : 0);
+    rc = st.res_count[usb];
+    hcw = st.hc[usb];
+  }
+  if constexpr (INC) {
+    const uint32_t w = lane < 4 * S ? st.chg[(srow + (size_t)(lane >> 2)) * 4 + (lane & 3)] : 0u;
+    if (!__any(w != 0u)) {  // no reservoir of the chunk changed: the cached features
+      for (int e = lane; e < S * NF; e += 64) {
+        const int s = e / NF, c = e - s * NF;
+        obs_out[s_base * NF + e] = c == 0 ? n_flow_on(st, srow + (size_t)s)
+                                          : st.fcache[(srow + (size_t)s) * 10 + (size_t)(c - 1)];
+      }
+      wave_sync();
+      return;
+    }
+  }
+  if constexpr (US && REGS) {  // (not for split handles: their reservoirs differ in count and ts)
+    if (st.res_count_dur == nullptr &&
+        observe_chunk_full<INC>(st, p, b, s_base, S, sc, obs_out, lane, rc, hcw))
+      return;
+  }
+  if constexpr (US) {
+    if (st.res_count_dur != nullptr) {  // split handles: two servers (four weight rows) per pass
+      for (int h = 0; h < S; h += 2)
+        observe_chunk_general<US>(st, p, b, s_base + h, S - h < 2 ? S - h : 2, sc, obs_out, lane);
+      return;
+    }
+  }
+  observe_chunk_general<US>(st, p, b, s_base, S, sc, obs_out, lane);
+}
 
 // ================================================================ reward (rewards.py)
 
@@ -2485,14 +2580,11 @@ constexpr int kObsWavesPerEnv = MAXS <= kObsChunk ? 1 : MAXS / kObsChunk;
 
 // The reward, episode bookkeeping and output rows of env b once its (S, 11) rows are in s_obs
 // (rewards.py:290-381, env.py:261-281, env.py:450-470): threads tid < 64 (one wave) compute the
-// reward, all nthr threads write the rows.  es_pf / er_pf: the env's ep_step / ep_return words
-// when the caller loaded them ahead (LDS), else nullptr (loaded here).
+// reward, all nthr threads write the rows.
 template <int MAXS, int MODE, bool FAC>
 __device__ __forceinline__ void observe_outputs(const DevState& st, const SimParams& p,
                                                 const ObsOutputs& out, size_t b,
-                                                float* s_obs, float* s_act, int tid, int nthr,
-                                                const int32_t* es_pf = nullptr,
-                                                const double* er_pf = nullptr) {
+                                                float* s_obs, float* s_act, int tid, int nthr) {
   const int S = p.S;
   // active servers (any column > 0): lane s of wave 0 scans its row, one ballot; their
   // reward-field values compacted into s_act in server order
@@ -2509,7 +2601,7 @@ __device__ __forceinline__ void observe_outputs(const DevState& st, const SimPar
       const int na = __popcll(act_mask);
       double r = 0.0;
       // reset by this step (next-step auto-reset, ep_step = -1): reward 0, episode step 0, not done
-      const int32_t es0 = es_pf != nullptr ? *es_pf : st.ep_step[b];
+      const int32_t es0 = st.ep_step[b];
       const bool fresh = p.next_reset && es0 < 0;
       if (fok && !fresh) {
         // (compile-time for observe_kernel<4>; fused G = 8 with S <= 4 at run time)
@@ -2520,7 +2612,7 @@ __device__ __forceinline__ void observe_outputs(const DevState& st, const SimPar
       }
       out.reward[b] = (float)r;
       const int32_t es = es0 + 1;  // -1 + 1 = 0 for a fresh env
-      const double er = (er_pf != nullptr ? *er_pf : st.ep_return[b]) + r;  // 0 + 0
+      const double er = st.ep_return[b] + r;  // 0 + 0
       st.ep_step[b] = es;
       st.ep_return[b] = er;
       out.done[b] = (uint8_t)(es >= p.max_steps ? 1 : 0);
@@ -2620,30 +2712,14 @@ __global__ void __launch_bounds__(64, LBSIM_OBS_PAIR_WAVES)
   __shared__ ObsScratch sc;
   __shared__ float s_obs[8 * NF];
   __shared__ float s_act[8];
-  __shared__ int32_t s_es[8];
-  __shared__ double s_er[8];
   const int S = p.S, epw = 8 / S, lane = (int)threadIdx.x;
   const size_t b0 = (size_t)blockIdx.x * (size_t)epw;
   const int nenv = (size_t)p.B - b0 < (size_t)epw ? (int)((size_t)p.B - b0) : epw;
-  // the envs' episode words, requested first and straight into LDS (global_load_lds: no VGPR
-  // holds them, no wait before the decision words): they arrive with the decision words instead
-  // of costing each env's bookkeeping a round trip of its own after the features
-  if constexpr (MODE == kModeStep) {
-    typedef __attribute__((address_space(1))) void gvoid;
-    typedef __attribute__((address_space(3))) void lvoid;
-    if (lane < nenv)
-      __builtin_amdgcn_global_load_lds((gvoid*)(st.ep_step + b0 + (size_t)lane), (lvoid*)s_es, 4,
-                                       0, 0);
-    if (lane < 2 * nenv)  // a double as two dwords
-      __builtin_amdgcn_global_load_lds(
-          (gvoid*)(reinterpret_cast<const uint32_t*>(st.ep_return + b0) + lane), (lvoid*)s_er, 4,
-          0, 0);
-  }
+  // (loading the envs' episode words into LDS up front with global_load_lds measured 12 us slower
+  // at 65536 x 4: 92.8 -> 104.5 us, profiles/r06e/)
   observe_rows_paired<MODE == kModeStep>(st, p, b0, nenv, sc, s_obs, lane);
   for (int e = 0; e < nenv; ++e) {
-    observe_outputs<8, MODE, FAC>(st, p, out, b0 + (size_t)e, s_obs + e * S * NF, s_act, lane, 64,
-                                  MODE == kModeStep ? s_es + e : nullptr,
-                                  MODE == kModeStep ? s_er + e : nullptr);
+    observe_outputs<8, MODE, FAC>(st, p, out, b0 + (size_t)e, s_obs + e * S * NF, s_act, lane, 64);
     wave_sync();  // s_act reused by the next env
   }
 }

@@ -9,8 +9,9 @@
 // follows, decays the weights instead).
 //
 //   vpp_export_kernel    simulator state -> that wire view: per (env, server) the 2 x 128 (t, v)
-//                        pairs (slots >= min(count, 128) as the zeros of VPP's fresh shm), the
-//                        server's n_flow_on and the frame timestamp of each env.
+//                        pairs (reservoir_mode ALGR: slots >= min(count, 128) as the zeros of
+//                        VPP's fresh shm; VPP: every bin as stored), the server's n_flow_on and
+//                        the frame timestamp of each env.
 //   vpp_features_kernel  process_reservoir on n raw reservoirs, one wave each: numpy's pairwise
 //                        sums (pairwise8), its std and its 'linear' percentile, so everything but
 //                        the f64 pow of the decay factor is bit-identical to numpy.
@@ -115,20 +116,33 @@ __global__ void __launch_bounds__(64)
   const int64_t e = pair / S;
   const int s = (int)(pair - e * S);
   const size_t b = (size_t)(e0 + e), sb = b * (size_t)S + (size_t)s;
+  // reservoir_mode VPP: every bin as stored (zeroed at reset: VPP's shm); ALGR: the first
+  // min(count, 128).  Split handles (lost-FIN): the duration reservoir's own count and timestamps.
+  const bool split = st.res_count_dur != nullptr;
   const uint32_t c = st.res_count[sb];
-  const int cnt = c < (uint32_t)K ? (int)c : K;
+  const uint32_t cd = split ? st.res_count_dur[sb] : c;
+  const int cnt = p.res_vpp ? K : (c < (uint32_t)K ? (int)c : K);
+  const int cntd = p.res_vpp ? K : (cd < (uint32_t)K ? (int)cd : K);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int i = lane + 64 * h;
-    float t = 0.0f, fv = 0.0f, dv = 0.0f;
+    float t = 0.0f, fv = 0.0f, td = 0.0f, dv = 0.0f;
     if (i < cnt) {
       const uint2 rec = st.res[sb * K + (size_t)i];
       t = (float)((double)rec.y * 1e-3);
       fv = sample_value<true>(rec.x);
-      dv = st.res_dur != nullptr ? sample_value<true>(st.res_dur[sb * K + (size_t)i]) : fv;
+      if (!split) {
+        td = t;
+        dv = st.res_dur != nullptr ? sample_value<true>(st.res_dur[sb * K + (size_t)i]) : fv;
+      }
+    }
+    if (split && i < cntd) {
+      const uint2 dr = reinterpret_cast<const uint2*>(st.res_dur)[sb * K + (size_t)i];
+      td = (float)((double)dr.y * 1e-3);
+      dv = sample_value<true>(dr.x);
     }
     tv_out[(pair * 2 + 0) * kVppN + i] = make_float2(t, fv);
-    tv_out[(pair * 2 + 1) * kVppN + i] = make_float2(t, dv);
+    tv_out[(pair * 2 + 1) * kVppN + i] = make_float2(td, dv);
   }
   if (lane == 0) {
     if (nflow_out != nullptr) nflow_out[pair] = (int32_t)n_flow_on(st, sb);

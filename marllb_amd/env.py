@@ -106,7 +106,8 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
                 lost_fin_prob: float = 0.0, flow_timeout: float = 40.0, flow_buckets: int = 1024,
                 fail_prob: float = 0.0, recover_prob: float = 0.1,
                 next_step_reset: bool = False,
-                duration_mode: str = "age", n_flow_on_mode: str = "queue") -> _lib.LbsimConfig:
+                duration_mode: str = "age", n_flow_on_mode: str = "queue",
+                lost_fin_pending: int = 256, reservoir_mode: str = "algr") -> _lib.LbsimConfig:
     """Build and validate an lbsim_config_t from reference-style kwargs.
 
     server_rates defaults to identical servers at utilisation `load`: mu = rate / (load * S).
@@ -118,8 +119,13 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
     simulates then observes each workgroup's envs); results are identical.
     lost_fin_prob / flow_timeout / flow_buckets: flows whose FIN/RST the VPP data plane misses
     record its timed-out guess fct = now - t_init - 40 s (src/vpp/lb/lbhash.h:175-217) instead of
-    their fct: flow_timeout (s) is the lb plugin's entry timeout, flow_buckets / arrival_rate the
-    mean wait for the next flow in the bucket.  0 = off.
+    their fct, at the wrap-up time (completion + flow_timeout + the wait for the next flow in the
+    bucket, of mean flow_buckets / arrival_rate) and stamped with it.  0 = off.
+    lost_fin_pending: the guesses each server holds until their wrap-up (a guess arriving at a
+    full ring is dropped and counted, Handle.lost_fin_overflow).
+    reservoir_mode: "algr" = problem-01's Algorithm R (reservoir.py:64-85); "vpp" = the data
+    plane's rule, every sample overwrites slot rand() % 128 of a zeroed reservoir
+    (lbhash.h:108,179), for feature_mode="upstream" / the VPP export.
     fail_prob / recover_prob: per server and step, an up server fails (its queue and reservoirs are
     lost) and a down one recovers (THEORY.md §6.4 server_failure ~ Bernoulli(p_fail)).  0 = off.
     next_step_reset: lbsim_step resets, in place of stepping, the envs whose last step returned
@@ -191,6 +197,10 @@ def make_config(num_envs: int, num_servers: int = 4, action_type: str = "discret
     if n_flow_on_mode not in _lib.N_FLOW_ON_MODES:
         raise ValueError(f"Unknown n_flow_on_mode: {n_flow_on_mode}. Supported: {_lib.N_FLOW_ON_MODES}")
     cfg.n_flow_on_mode = _lib.N_FLOW_ON_MODES.index(n_flow_on_mode)
+    cfg.lost_fin_pending = int(lost_fin_pending)
+    if reservoir_mode not in _lib.RESERVOIR_MODES:
+        raise ValueError(f"Unknown reservoir_mode: {reservoir_mode}. Supported: {_lib.RESERVOIR_MODES}")
+    cfg.reservoir_mode = _lib.RESERVOIR_MODES.index(reservoir_mode)
     _lib.validate(cfg)
     return cfg
 

@@ -330,7 +330,20 @@ typedef struct oracle {
    * episode start / the server's last failure, never decremented (lbhash.h:193,214) */
   int leak;
   uint32_t* lost_on;
-  int dur_plane; /* the `dur` section exists (last in the snapshot) */
+  int dur_plane; /* the `dur` section exists */
+  /* lost-FIN deferral (split: lf_thr != 0): the fct and duration reservoirs are
+   * separate -- dur is then [B*S*K][2] {duration us, timestamp ms} with its own count
+   * res_count_dur -- and each server holds its pending timed-out fct guesses in a ring of P
+   * entries {due us mod 2^32 (absolute: clock * dt + t), guess us} sorted by due time, pend_hc =
+   * head | count << 16; lf_over counts the guesses dropped at a full ring (per env, this episode) */
+  int split, P;
+  uint32_t* res_count_dur;
+  uint32_t* pend_hc;
+  uint32_t* pend;
+  uint32_t* lf_over;
+  /* reservoir_mode VPP: every sample overwrites slot rand() % 128 (lbhash.h:108,179), bins zeroed
+   * at reset / failure */
+  int res_vpp;
   /* TRACE arrivals (lbsim_set_trace semantics): us gap before each row, mean-1 work */
   uint32_t* trace_gap; float* trace_work; uint32_t trace_rows;
   /* not state: the Algorithm R draw word of each queued flow that arrived in the current step,
@@ -355,6 +368,9 @@ static void derive(oracle_t* o) {
   o->big_in_step = (o->dt_us >= (int32_t)((1u << 25) - 1u)) || o->lf_thr != 0u;
   o->leak = c->n_flow_on_mode == LBSIM_NFLOW_VPP && o->lf_thr != 0u;
   o->dur_plane = c->duration_mode == LBSIM_DURATION_SERVICE || o->lf_thr != 0u;
+  o->split = o->lf_thr != 0u;
+  o->P = o->split ? c->lost_fin_pending : 0;
+  o->res_vpp = c->reservoir_mode == LBSIM_RESERVOIR_VPP;
   o->key[0] = (uint32_t)(c->seed & 0xFFFFFFFFull);
   o->key[1] = (uint32_t)(c->seed >> 32);
 }
@@ -370,7 +386,9 @@ oracle_t* oracle_create(const lbsim_config_t* cfg) {
                        B * 8, BS * 4, BS * 4, BS * 4, BSQ * 8, BSK * 8, BS * 16, BS * 40,
                        cfg->normalize_obs ? BS * NF * 8 : 0, cfg->normalize_obs ? BS * NF * 8 : 0,
                        cfg->fail_prob > 0.0f ? BS * 4 : 0, o->leak ? BS * 4 : 0,
-                       o->dur_plane ? BSK * 4 : 0};
+                       o->dur_plane ? BSK * (o->split ? 8 : 4) : 0, o->split ? BS * 4 : 0,
+                       o->split ? BS * 4 : 0, o->split ? BS * (size_t)o->P * 8 : 0,
+                       o->split ? B * 4 : 0};
   size_t total = 0;
   for (size_t i = 0; i < sizeof(sz) / sizeof(sz[0]); ++i) total += sz[i];
   o->bytes = total;
@@ -383,7 +401,9 @@ oracle_t* oracle_create(const lbsim_config_t* cfg) {
                    (void**)&o->norm_count, (void**)&o->ep_return, (void**)&o->hc,
                    (void**)&o->last_tc, (void**)&o->res_count, (void**)&o->ring,
                    (void**)&o->res, (void**)&o->chg, (void**)&o->fcache, (void**)&o->norm_mean,
-                   (void**)&o->norm_std, (void**)&o->down, (void**)&o->lost_on, (void**)&o->dur};
+                   (void**)&o->norm_std, (void**)&o->down, (void**)&o->lost_on, (void**)&o->dur,
+                   (void**)&o->res_count_dur, (void**)&o->pend_hc, (void**)&o->pend,
+                   (void**)&o->lf_over};
   for (size_t i = 0; i < sizeof(sz) / sizeof(sz[0]); ++i) {
     *ptrs[i] = sz[i] ? (void*)p : NULL;
     p += sz[i];
@@ -564,19 +584,32 @@ static uint32_t lf_mix(uint32_t h) {
  * Lost or not, and the wait, are a hash of (seed, global env id, episode, the flow's absolute
  * arrival us mod 2^32): a pure function of the flow, whichever step records it.  Signed us, in
  * uint32 arithmetic. */
-uint32_t oracle_lost_fin_fct(uint32_t fct, uint32_t abs_ta, uint32_t gid, uint32_t episode,
-                             uint32_t key0, uint32_t key1, uint32_t thr, int32_t off_us,
-                             float wait_us) {
-  if (thr == 0u) return fct;
+/* Lost or not (the 24-bit test), and the bucket wait in us, of the flow that arrived at abs_ta. */
+static int lf_test(uint32_t abs_ta, uint32_t gid, uint32_t episode, uint32_t key0, uint32_t key1,
+                   uint32_t thr, float wait_us, int32_t* wait_out) {
+  if (thr == 0u) return 0;
   const uint32_t salt = lf_mix(lf_mix(key0 ^ (episode * 0x9E3779B9u)) ^ gid ^ (key1 * 0x85EBCA6Bu));
   const uint32_t h = lf_mix(abs_ta ^ salt);
-  if ((h >> 8) >= thr) return fct;
+  if ((h >> 8) >= thr) return 0;
   const uint32_t h2 = lf_mix(h ^ 0x6A09E667u);
-  const int32_t wait = (int32_t)(-oracle_logf(u01(h2)) * wait_us);
-  /* signed int32 us, saturated (the config bound keeps Poisson work in range) */
+  *wait_out = (int32_t)(-oracle_logf(u01(h2)) * wait_us);
+  return 1;
+}
+
+/* The guess fct + off_us + wait as a signed int32 us sample, saturated (the config bound keeps
+ * Poisson work in range). */
+static uint32_t lf_guess(uint32_t fct, int32_t off_us, int32_t wait) {
   int64_t g = (int64_t)(int32_t)fct + (int64_t)off_us + (int64_t)wait;
   g = g > (int64_t)INT32_MAX ? (int64_t)INT32_MAX : (g < (int64_t)INT32_MIN ? (int64_t)INT32_MIN : g);
   return (uint32_t)(int32_t)g;
+}
+
+uint32_t oracle_lost_fin_fct(uint32_t fct, uint32_t abs_ta, uint32_t gid, uint32_t episode,
+                             uint32_t key0, uint32_t key1, uint32_t thr, int32_t off_us,
+                             float wait_us) {
+  int32_t wait = 0;
+  if (!lf_test(abs_ta, gid, episode, key0, key1, thr, wait_us, &wait)) return fct;
+  return lf_guess(fct, off_us, wait);
 }
 
 /* Algorithm R slot for a flow that arrived in the step it completes in: the draw
@@ -588,30 +621,37 @@ long oracle_algr_slot_r32(uint32_t count, uint32_t r) {
   return j < (uint64_t)K ? (long)j : -1;
 }
 
-/* Algorithm R insert of one completion into both reservoirs of server s (shared decision).  A
- * flow that arrived in this step (has_r) uses its arrival's draw word r; a flow carried in from an
- * earlier step uses the reservoir stream's block (count >> 1), half (count & 1). */
+/* The slot one sample takes in a reservoir holding c samples (-1: not kept).  ALGR (reservoir.py:
+ * 64-85): c < K -> c, else j = randint(0, c + 1) if j < K; VPP (lbhash.h:108,179): rand() % 128,
+ * always.  The draw: a flow that arrived in this step (has_r) uses its arrival's word r (the top 7
+ * bits for VPP); otherwise the reservoir stream's block (c >> 1), half (c & 1), at counter word w
+ * (2 << 24) | sub | s -- sub = 1 << 16 for the fct reservoir of a split handle. */
+static long res_slot(env_ctx* e, int s, uint32_t c, int has_r, uint32_t r, uint32_t sub) {
+  oracle_t* o = e->o;
+  if (!o->res_vpp && c < (uint32_t)K) return (long)c;
+  if (has_r) return o->res_vpp ? (long)(r >> 25) : oracle_algr_slot_r32(c, r);
+  const uint32_t ctr[4] = {c >> 1, e->gid, o->episode[e->b], (2u << 24) | sub | (uint32_t)s};
+  uint32_t d[4];
+  oracle_philox(ctr, o->key, d);
+  const uint32_t hi = (c & 1u) ? d[3] : d[1];
+  const uint32_t lo = (c & 1u) ? d[2] : d[0];
+  if (o->res_vpp) return (long)(hi >> 25);
+  /* j = floor(r64 * (c + 1) / 2^64): randint(0, count + 1) (reservoir.py:76) */
+  const unsigned __int128 prod = (unsigned __int128)(((uint64_t)hi << 32) | lo) * ((uint64_t)c + 1u);
+  const uint64_t j = (uint64_t)(prod >> 64);
+  return j < (uint64_t)K ? (long)j : -1;
+}
+
+/* Algorithm R insert of one completion into both reservoirs of server s (shared decision, paired
+ * handles).  A flow that arrived in this step (has_r) uses its arrival's draw word r; a flow
+ * carried in from an earlier step uses the reservoir stream's block (count >> 1), half
+ * (count & 1). */
 static void reservoir_add(env_ctx* e, int s, uint32_t fct, uint32_t dur, uint32_t ts_ms, int has_r,
                           uint32_t r) {
   oracle_t* o = e->o;
   const size_t sb = e->b * (size_t)o->S + (size_t)s;
   const uint32_t c = o->res_count[sb];
-  long slot;
-  if (c < (uint32_t)K) {
-    slot = (long)c;
-  } else if (has_r) {
-    slot = oracle_algr_slot_r32(c, r);
-  } else {
-    const uint32_t ctr[4] = {c >> 1, e->gid, o->episode[e->b], (2u << 24) | (uint32_t)s};
-    uint32_t d[4];
-    oracle_philox(ctr, o->key, d);
-    const uint32_t hi = (c & 1u) ? d[3] : d[1];
-    const uint32_t lo = (c & 1u) ? d[2] : d[0];
-    /* j = floor(r64 * (c + 1) / 2^64): randint(0, count + 1) (reservoir.py:76) */
-    const unsigned __int128 prod = (unsigned __int128)(((uint64_t)hi << 32) | lo) * ((uint64_t)c + 1u);
-    const uint64_t j = (uint64_t)(prod >> 64);
-    slot = j < (uint64_t)K ? (long)j : -1;
-  }
+  const long slot = res_slot(e, s, c, has_r, r, 0u);
   if (slot >= 0) {
     const size_t r = sb * K + (size_t)slot;
     /* HC_BIG at the store for a flow carried in from an earlier step; in-step records by the
@@ -625,6 +665,75 @@ static void reservoir_add(env_ctx* e, int s, uint32_t fct, uint32_t dur, uint32_
   if (c != 0xFFFFFFFFu) o->res_count[sb] = c + 1u;
 }
 
+/* Split handles (lost-FIN): one sample into the fct reservoir (res, res_count) or the duration
+ * reservoir (dur {us, ts}, res_count_dur) of server s, each with its own decision. */
+static void split_add(env_ctx* e, int s, int is_dur, uint32_t v, uint32_t ts_ms, int has_r,
+                      uint32_t r) {
+  oracle_t* o = e->o;
+  const size_t sb = e->b * (size_t)o->S + (size_t)s;
+  uint32_t* cnt = is_dur ? o->res_count_dur : o->res_count;
+  const uint32_t c = cnt[sb];
+  /* the duration reservoir draws as the paired reservoirs of a run without losses (its samples
+   * are the same: every completion's), the fct reservoir's carried / deferred draws at 1 << 16 */
+  const long slot = res_slot(e, s, c, has_r, r, is_dur ? 0u : 1u << 16);
+  if (slot >= 0) {
+    const size_t i = sb * K + (size_t)slot;
+    if (!has_r && v >= PACK_LIMIT) o->hc[sb] |= HC_BIG;
+    uint32_t* rec = is_dur ? o->dur : o->res;
+    rec[2 * i + 0] = v;
+    rec[2 * i + 1] = ts_ms;
+    o->chg[sb * 4 + (size_t)(slot >> 5)] |= 1u << (slot & 31);
+  }
+  if (c != 0xFFFFFFFFu) cnt[sb] = c + 1u;
+}
+
+/* A timed-out flow's guess, due (absolute us mod 2^32) at its wrap-up, into server s's pending
+ * ring, sorted by due time (wrap-aware; an equal due goes after the entries already there), by an
+ * insertion from the tail.  A full ring drops it (lf_over). */
+static void pend_push(env_ctx* e, int s, uint32_t due, uint32_t val) {
+  oracle_t* o = e->o;
+  const size_t sb = e->b * (size_t)o->S + (size_t)s;
+  const int P = o->P;
+  const int head = (int)(o->pend_hc[sb] & 0xFFFFu), cnt = (int)(o->pend_hc[sb] >> 16);
+  if (cnt == P) { o->lf_over[e->b] += 1u; return; }
+  uint32_t* ring = o->pend + sb * (size_t)P * 2;
+  int i = cnt;
+  while (i > 0) {
+    int pos = head + i - 1;
+    if (pos >= P) pos -= P;
+    if ((int32_t)(ring[2 * pos] - due) <= 0) break;
+    int to = pos + 1 == P ? 0 : pos + 1;
+    ring[2 * to] = ring[2 * pos];
+    ring[2 * to + 1] = ring[2 * pos + 1];
+    --i;
+  }
+  int pos = head + i;
+  if (pos >= P) pos -= P;
+  ring[2 * pos] = due;
+  ring[2 * pos + 1] = val;
+  o->pend_hc[sb] = (uint32_t)head | ((uint32_t)(cnt + 1) << 16);
+}
+
+/* Server s's pending guesses due by step time t (relative us) into its fct reservoir, in due
+ * order, each stamped with its due time (the wrap-up of lbhash.h:182-217: the next flow of the
+ * bucket records now - t_init - 40 s at its own arrival). */
+static void pend_flush(env_ctx* e, int s, int32_t t, uint64_t base_us) {
+  oracle_t* o = e->o;
+  const size_t sb = e->b * (size_t)o->S + (size_t)s;
+  const int P = o->P;
+  int head = (int)(o->pend_hc[sb] & 0xFFFFu), cnt = (int)(o->pend_hc[sb] >> 16);
+  const uint32_t* ring = o->pend + sb * (size_t)P * 2;
+  while (cnt > 0) {
+    const int32_t rel = (int32_t)(ring[2 * head] - (uint32_t)base_us);
+    if (rel > t) break;
+    const uint32_t ts_ms = (uint32_t)((uint64_t)((int64_t)base_us + (int64_t)rel) / 1000u);
+    split_add(e, s, 0, ring[2 * head + 1], ts_ms, 0, 0u);
+    head = head + 1 == P ? 0 : head + 1;
+    cnt -= 1;
+  }
+  o->pend_hc[sb] = (uint32_t)head | ((uint32_t)cnt << 16);
+}
+
 /* End of a dynamics launch (a step, or a reset with its warm-up): when an in-step record can be
  * big, HC_BIG |= any slot the launch wrote (below the count) holding one -- the GPU's big_written. */
 static void big_scan(oracle_t* o, size_t b) {
@@ -633,12 +742,31 @@ static void big_scan(oracle_t* o, size_t b) {
     const size_t sb = b * (size_t)o->S + (size_t)s;
     const uint32_t c = o->res_count[sb];
     const uint32_t n = c < (uint32_t)K ? c : (uint32_t)K;
-    for (uint32_t slot = 0; slot < n; ++slot) {
+    /* split handles: the duration reservoir's own count and {us, ts} records */
+    const uint32_t cd = o->split ? o->res_count_dur[sb] : c;
+    const uint32_t nd = cd < (uint32_t)K ? cd : (uint32_t)K;
+    for (uint32_t slot = 0; slot < K; ++slot) {
       if (!((o->chg[sb * 4 + (slot >> 5)] >> (slot & 31)) & 1u)) continue;
-      const uint32_t f = o->res[2 * (sb * K + slot)];
-      const uint32_t d = o->dur ? o->dur[sb * K + slot] : f;
+      const uint32_t f = slot < n ? o->res[2 * (sb * K + slot)] : 0u;
+      const uint32_t d = slot >= nd ? 0u
+                         : (o->split ? o->dur[2 * (sb * K + slot)]
+                                     : (o->dur ? o->dur[sb * K + slot] : f));
       if ((f > d ? f : d) >= PACK_LIMIT) o->hc[sb] |= HC_BIG;
     }
+  }
+}
+
+/* Emptied reservoirs (reset, failure): split handles drop the duration count and the pending
+ * guesses; reservoir_mode VPP zeroes every bin (VPP's zeroed shm, shm_proxy.py:518-543 reads all
+ * 128). */
+static void clear_reservoirs(oracle_t* o, size_t sb) {
+  if (o->split) {
+    o->res_count_dur[sb] = 0u;
+    o->pend_hc[sb] = 0u;
+  }
+  if (o->res_vpp) {
+    memset(o->res + sb * K * 2, 0, (size_t)K * 8);
+    if (o->dur) memset(o->dur + sb * K * (o->split ? 2 : 1), 0, (size_t)K * (o->split ? 8 : 4));
   }
 }
 
@@ -670,7 +798,26 @@ static void pop_until(env_ctx* e, int s, int32_t t, uint64_t base_us, double den
     o->last_tc[sb] = tc;
     const uint32_t ts_ms = (uint32_t)((base_us + (uint64_t)(int64_t)tc) / 1000u);
     /* ta >= 0: arrived in this step (times are relative to the step start) */
-    reservoir_add(e, s, fct, dur, ts_ms, ta >= 0, o->flow_r[sb * o->Q + (size_t)head]);
+    const uint32_t r = o->flow_r[sb * o->Q + (size_t)head];
+    if (o->split) {
+      /* lost-FIN (lbhash.h:175-217): the guesses due by tc first, then this flow's duration
+       * sample (its age at its last packet, lbhash.h:129-136: recorded now), then its fct -- now
+       * (RSTACK seen, :116-124) or, lost, as a guess due at the wrap-up: the entry expires
+       * flow_timeout after this last packet and the next flow hashed into the bucket, after the
+       * wait, records now - t_init - 40 s (:182-192, :204-213) */
+      pend_flush(e, s, tc, base_us);
+      split_add(e, s, 1, dur, ts_ms, ta >= 0, r);
+      int32_t wait = 0;
+      if (lf_test((uint32_t)base_us + (uint32_t)ta, e->gid, o->episode[e->b], o->key[0], o->key[1],
+                  o->lf_thr, o->lf_wait_us, &wait))
+        pend_push(e, s, (uint32_t)base_us + (uint32_t)tc + (uint32_t)(o->lf_off_us + 40000000) +
+                            (uint32_t)wait,
+                  lf_guess((uint32_t)(tc - ta), o->lf_off_us, wait));
+      else
+        split_add(e, s, 0, (uint32_t)(tc - ta), ts_ms, ta >= 0, r);
+    } else {
+      reservoir_add(e, s, fct, dur, ts_ms, ta >= 0, r);
+    }
     head = head + 1 == o->Q ? 0 : head + 1;
     cnt -= 1;
   }
@@ -742,6 +889,7 @@ static void sim_step(env_ctx* e, const float* w) {
         o->res_count[sb] = 0u;
         if (o->lost_on) o->lost_on[sb] = 0u;
         o->chg[sb * 4] |= 1u; /* emptied: the next observe recomputes the (zero) features */
+        clear_reservoirs(o, sb);
       }
       if (o->down[sb]) qcap[s] = 0;
     }
@@ -816,6 +964,9 @@ static void sim_step(env_ctx* e, const float* w) {
     draw_arrival(e, ta);
   }
   for (int s = 0; s < S; ++s) pop_until(e, s, o->dt_us, base_us, den[s]);
+  /* split handles: the guesses due by the step's end */
+  if (o->split)
+    for (int s = 0; s < S; ++s) pend_flush(e, s, o->dt_us, base_us);
   /* rebase to the next step */
   const int32_t dt = o->dt_us;
   o->next_arr[b] -= dt;
@@ -886,10 +1037,24 @@ static void observe(oracle_t* o, size_t b, float* obs_out, float* reward_out, ui
     for (int i = 0; i < n; ++i) {
       vf[i] = us_to_seconds(o->res[2 * (sb * K + (size_t)i)]);
       /* paired records (no duration plane): the duration reservoir is the fct reservoir */
-      vd[i] = o->dur ? us_to_seconds(o->dur[sb * K + (size_t)i]) : vf[i];
+      vd[i] = o->dur && !o->split ? us_to_seconds(o->dur[sb * K + (size_t)i]) : vf[i];
     }
     features_one(vf, w, wq, n, ff);
-    features_one(vd, w, wq, n, fd);
+    if (o->split) {
+      /* the duration reservoir of a split handle: its own count and timestamps */
+      const uint32_t cd = o->res_count_dur[sb];
+      const int nd = cd < (uint32_t)K ? (int)cd : K;
+      float wd[K];
+      uint64_t wqd[K];
+      for (int i = 0; i < nd; ++i) {
+        vd[i] = us_to_seconds(o->dur[2 * (sb * K + (size_t)i)]);
+        ts[i] = o->dur[2 * (sb * K + (size_t)i) + 1];
+      }
+      slot_weights(ts, nd, o->decay_c, wd, wqd);
+      features_one(vd, wd, wqd, nd, fd);
+    } else {
+      features_one(vd, w, wq, n, fd);
+    }
     for (int f = 0; f < 5; ++f) { o->fcache[sb * 10 + (size_t)f] = ff[f]; o->fcache[sb * 10 + 5 + (size_t)f] = fd[f]; }
     /* n_flow_on: flows in flight, plus the lost-FIN flows VPP never decrements (n_flow_on_mode
      * VPP, lbhash.h:193,214) */
@@ -932,7 +1097,9 @@ static void reset_env(oracle_t* o, size_t b) {
     for (int w = 0; w < 4; ++w) o->chg[sb * 4 + (size_t)w] = w == 0 ? 1u : 0u;
     if (o->down) o->down[sb] = 0u; /* every server is up at the episode start */
     if (o->lost_on) o->lost_on[sb] = 0u;
+    clear_reservoirs(o, sb);
   }
+  if (o->split) o->lf_over[b] = 0u;
   float w1[LBSIM_MAX_SERVERS];
   for (int s = 0; s < LBSIM_MAX_SERVERS; ++s) w1[s] = 1.0f;
   for (int k = 0; k < o->cfg.warmup_steps; ++k) sim_step(&e, w1);

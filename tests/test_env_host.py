@@ -88,10 +88,14 @@ def test_optional_dynamics_config():
                     # a nonzero probability below the 24-bit threshold's resolution
                     ({"fail_prob": 1e-9}, "fail_prob"),
                     ({"lost_fin_prob": 1e-9}, "lost_fin_prob"),
-                    # the guessed fct must fit a signed 32-bit us sample
-                    ({"lost_fin_prob": 0.1, "flow_timeout": 3600.0}, "signed 32-bit"),
+                    # the guessed fct and its wrap-up delay must fit signed 32-bit us (ADVICE
+                    # r04); the message states the limit for the given timeout
+                    ({"lost_fin_prob": 0.1, "flow_timeout": 3600.0}, "flow_timeout_s must be < 1040"),
                     ({"lost_fin_prob": 0.1, "flow_timeout": 600.0, "flow_buckets": 40000},
-                     "signed 32-bit"),
+                     r"signed 32-bit.*must be <= 26\.347 s \(got 100\.000\)"),
+                    ({"lost_fin_prob": 0.1, "lost_fin_pending": 0}, "lost_fin_pending"),
+                    ({"lost_fin_prob": 0.1, "lost_fin_pending": 5000}, "lost_fin_pending"),
+                    ({"reservoir_mode": "random"}, "reservoir_mode"),
                     ({"duration_mode": "wall"}, "duration_mode")]:
         with pytest.raises(ValueError, match=msg):
             E.make_config(8, 4, **kw)

@@ -216,13 +216,19 @@ CONFIGS = [
     dict(B=36, S=4, kw={"load": 1.25, "discrete_weights": [0.5, 1.0, 8.0]}),
     dict(B=30, S=4, kw={"queue_capacity": 16, "load": 1.4, "action_type": "continuous"}),
     dict(B=60, S=4, kw={"action_type": "continuous", "_nan_actions": 0.2}),
-    # lost-FIN flows (src/vpp/lb/lbhash.h:175-217): VPP's timed-out fct guess -- positive outliers
-    # with the default 40 s flow timeout (fct + the bucket wait), negative samples with a 10 s one
-    # (fct - 30 s + wait: observe's signed two-pass sort), every flow lost on a 3-server LSQ env
+    # lost-FIN flows (src/vpp/lb/lbhash.h:175-217): VPP's timed-out fct guess, recorded when the
+    # bucket's next flow wraps the flow up (completion + flow_timeout + wait) -- with the default
+    # 40 s timeout every guess is still pending at the end; 0.6 s and 0.3 s timeouts (2-3 steps
+    # of 0.25 s) flush them into the fct reservoir as negative samples (fct - 39.4 s + wait:
+    # observe's signed two-pass sort), every flow lost on a 3-server LSQ env; a 4-entry pending
+    # ring that overflows
     dict(B=90, S=4, kw={"lost_fin_prob": 0.3}),
-    dict(B=64, S=8, kw={"lost_fin_prob": 0.25, "flow_timeout": 10.0, "assign_policy": "sed2"}),
-    dict(B=50, S=3, kw={"lost_fin_prob": 1.0, "flow_timeout": 25.0, "assign_policy": "lsq",
+    dict(B=64, S=8, kw={"lost_fin_prob": 0.25, "flow_timeout": 0.6, "flow_buckets": 64,
+                        "assign_policy": "sed2"}),
+    dict(B=50, S=3, kw={"lost_fin_prob": 1.0, "flow_timeout": 0.3, "assign_policy": "lsq",
                         "action_type": "continuous", "flow_buckets": 64}),
+    dict(B=40, S=4, kw={"lost_fin_prob": 0.8, "flow_timeout": 1.5, "flow_buckets": 32,
+                        "lost_fin_pending": 4}),
     # server failure / recovery (THEORY.md §6.4): queues and reservoirs lost, down servers never
     # chosen (every policy), their all-zero rows inactive in the reward (env.py:410-413)
     dict(B=100, S=4, kw={"fail_prob": 0.15, "recover_prob": 0.3}),
@@ -249,7 +255,8 @@ CONFIGS = [
     dict(B=64, S=3, kw={"duration_mode": "service", "queue_capacity": 6, "load": 1.3}),
     dict(B=40, S=20, kw={"duration_mode": "service", "assign_policy": "sed2",
                          "arrival_rate": 800.0}),
-    dict(B=48, S=8, kw={"duration_mode": "service", "lost_fin_prob": 0.2, "flow_timeout": 10.0}),
+    dict(B=48, S=8, kw={"duration_mode": "service", "lost_fin_prob": 0.2, "flow_timeout": 0.4,
+                        "flow_buckets": 64}),
     dict(B=8256, S=4, kw={"duration_mode": "service", "load": 1.1}),
     # paired observe of wide envs (S = 16: two waves per env, observe_pair16_kernel; S = 32:
     # one wave per 8-row group + the rows kernel): next-step auto-reset with normalisation,
@@ -275,6 +282,17 @@ CONFIGS = [
                         "action_type": "continuous"}),
     dict(B=66, S=5, kw={"n_flow_on_mode": "vpp", "lost_fin_prob": 0.6,
                         "discrete_weights": [0.5, 1.0, 3.0]}),
+    # reservoir_mode "vpp" (lbhash.h:108,179: every sample to slot rand() % 128 of a zeroed
+    # reservoir): the headline group shape with next-step resets, lost-FIN deferral with failures,
+    # ALIAS on 16 servers, sparse arrivals (bins that stay zero), service durations
+    dict(B=64, S=4, kw={"reservoir_mode": "vpp"}),
+    dict(B=8256, S=4, kw={"reservoir_mode": "vpp", "max_steps": 5, "next_step_reset": True}),
+    dict(B=40, S=6, kw={"reservoir_mode": "vpp", "lost_fin_prob": 0.3, "flow_timeout": 0.5,
+                        "flow_buckets": 32, "fail_prob": 0.1, "recover_prob": 0.3}),
+    dict(B=48, S=16, kw={"reservoir_mode": "vpp", "assign_policy": "alias",
+                         "action_type": "continuous"}),
+    dict(B=64, S=4, kw={"reservoir_mode": "vpp", "arrival_rate": 6.0,
+                        "server_rates": [3.0, 4.0, 5.0, 6.0], "duration_mode": "service"}),
 ]
 
 
@@ -299,14 +317,17 @@ def _actions(rng, B, S, cfgkw):
     return rng.integers(-n, n, (B, S)).astype(np.int64)
 
 
-def _compare_state(h_gpu, ora, B, S, Q, norm, fail=False, leak=False):
-    g = statelayout.parse(h_gpu.state_bytes(), B, S, Q, norm, fail, leak)
-    o = statelayout.parse(ora.state_bytes(), B, S, Q, norm, fail, leak)
+def _compare_state(h_gpu, ora, B, S, Q, norm, fail=False, leak=False, split_P=0):
+    g = statelayout.parse(h_gpu.state_bytes(), B, S, Q, norm, fail, leak, split_P=split_P)
+    o = statelayout.parse(ora.state_bytes(), B, S, Q, norm, fail, leak, split_P=split_P)
     for name in g:
-        if name == "ring":
+        if name in ("ring", "pend"):
             continue
         np.testing.assert_array_equal(g[name], o[name], err_msg=name)
     np.testing.assert_array_equal(statelayout.live_ring(g, B, S, Q), statelayout.live_ring(o, B, S, Q))
+    if split_P:  # the pending lost-FIN guesses in their rings
+        np.testing.assert_array_equal(statelayout.live_pend(g, B, S, split_P),
+                                      statelayout.live_pend(o, B, S, split_P))
 
 
 def _run_vs_oracle(oracle_mod, B, S, kw, akw, case, mapping="auto", steps=12, post_steps=4,
@@ -320,6 +341,7 @@ def _run_vs_oracle(oracle_mod, B, S, kw, akw, case, mapping="auto", steps=12, po
     ora = oracle_mod.OracleEnv(make_config(B, S, **kw), threads=threads, trace=kw.get("trace"))
     Q, norm, fail = env.cfg.queue_capacity, bool(env.cfg.normalize_obs), env.cfg.fail_prob > 0
     leak = statelayout.has_leak(env.cfg)
+    sp = statelayout.split_p(env.cfg)
     obs_g = env.reset().cpu().numpy()
     obs_o = ora.reset()
     np.testing.assert_array_equal(obs_g, obs_o)
@@ -332,7 +354,7 @@ def _run_vs_oracle(oracle_mod, B, S, kw, akw, case, mapping="auto", steps=12, po
         np.testing.assert_array_equal(og.cpu().numpy(), oo, err_msg=f"obs step {k}")
         np.testing.assert_array_equal(rg.cpu().numpy(), ro, err_msg=f"reward step {k}")
         np.testing.assert_array_equal(dg.cpu().numpy().astype(np.uint8), do)
-    _compare_state(env.handle, ora, B, S, Q, norm, fail, leak)
+    _compare_state(env.handle, ora, B, S, Q, norm, fail, leak, sp)
     # masked reset of every third env, then more steps
     mask = (np.arange(B) % 3 == 0).astype(np.uint8)
     og = env.reset(mask=torch.from_numpy(mask)).cpu().numpy()
@@ -344,7 +366,7 @@ def _run_vs_oracle(oracle_mod, B, S, kw, akw, case, mapping="auto", steps=12, po
         oo, ro, do, _ = ora.step(a)
         np.testing.assert_array_equal(og.cpu().numpy(), oo)
         np.testing.assert_array_equal(rg.cpu().numpy(), ro)
-    _compare_state(env.handle, ora, B, S, Q, norm, fail, leak)
+    _compare_state(env.handle, ora, B, S, Q, norm, fail, leak, sp)
     ora.close()
     return env
 

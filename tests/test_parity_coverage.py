@@ -42,7 +42,8 @@ def run_case(oracle_mod, case, steps=12):
     for _ in range(steps):
         ora.step(_actions(rng, B, S, c["kw"]))  # the GPU test's action stream
         st = statelayout.parse(ora.state_bytes(), B, S, cfg.queue_capacity, bool(cfg.normalize_obs),
-                               cfg.fail_prob > 0, statelayout.has_leak(cfg))
+                               cfg.fail_prob > 0, statelayout.has_leak(cfg),
+                               split_P=statelayout.split_p(cfg))
         max_q = max(max_q, int((st["hc"] >> 16).max()))
         per_server = np.unpackbits(st["chg"].view(np.uint8)).reshape(B, S, 128).sum(2)
         written.append(per_server.sum(1))  # slots written per env (all its servers)

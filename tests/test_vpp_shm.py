@@ -222,21 +222,71 @@ def test_gpu_simulator_as_live_vpp(oracle_mod, tmp_path):
         env.close()
 
 
-def _tv_from_oracle_state(st, B, S):
+def _tv_from_oracle_state(st, B, S, vpp=False):
     """The VPP view (lbsim_vpp_export's contract) of an oracle state snapshot: [B, S, 2, 128, 2]
-    (t, v) f32 and the frame times [B]."""
-    cnt = np.minimum(st["res_count"].reshape(B, S), 128)
+    (t, v) f32 and the frame times [B].  vpp (reservoir_mode "vpp"): every bin as stored, else the
+    first min(count, 128); a split (lost-FIN) snapshot's duration reservoir has its own count and
+    timestamps."""
+    cnts = (st["res_count"], st.get("res_count_dur", st["res_count"]))
     words = (st["res_fct"].reshape(B, S, 128), st["res_dur"].reshape(B, S, 128))
-    m = np.arange(128)[None, None, :] < cnt[:, :, None]
-    t = np.where(m, (st["res_ts"].reshape(B, S, 128).astype(np.float64) * 1e-3).astype(np.float32),
-                 np.float32(0))
+    tss = (st["res_ts"].reshape(B, S, 128), st.get("res_dur_ts", st["res_ts"]).reshape(B, S, 128))
     tv = np.zeros((B, S, 2, 128, 2), np.float32)
     for r in range(2):
-        tv[:, :, r, :, 0] = t
+        cnt = np.minimum(cnts[r].reshape(B, S), 128)
+        m = np.arange(128)[None, None, :] < (128 if vpp else cnt[:, :, None])
+        tv[:, :, r, :, 0] = np.where(m, (tss[r].astype(np.float64) * 1e-3).astype(np.float32),
+                                     np.float32(0))
         tv[:, :, r, :, 1] = np.where(m, words[r].view(np.int32).astype(np.float32) * np.float32(1e-6),
                                      np.float32(0))
     ts = (st["clock"].astype(np.float64) * 0.25).astype(np.float32)
     return tv, ts
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", [dict(reservoir_mode="vpp"),
+                                dict(lost_fin_prob=0.4, flow_timeout=0.5, flow_buckets=32),
+                                dict(reservoir_mode="vpp", lost_fin_prob=0.4, flow_timeout=0.5,
+                                     flow_buckets=32, duration_mode="service")])
+def test_gpu_vpp_export_reservoir_modes(oracle_mod, kw):
+    """lbsim_vpp_export under reservoir_mode "vpp" (every sample to bin rand() % 128 of a zeroed
+    reservoir, lbhash.h:108,179: the agent's process_reservoir reads all 128 bins, shm_proxy.py:
+    518-543) and under lost-FIN deferral (the duration reservoir's own count and timestamps):
+    the GPU's wire view equals the oracle state's, bin for bin, after a reset and steps; under
+    "vpp" never-written bins stay (0, 0) at first and fill as samples land."""
+    import torch
+
+    from marllb_amd.env import VecLoadBalanceEnv, make_config
+    from tests import statelayout
+    B, S = 24, 4
+    kw = dict(seed=4242, **kw)
+    env = VecLoadBalanceEnv(B, S, device="cuda:0", autoreset=False, **kw)
+    cfg = make_config(B, S, **kw)
+    ora = oracle_mod.OracleEnv(cfg, threads=2)
+    vpp = kw.get("reservoir_mode") == "vpp"
+    env.reset()
+    ora.reset()
+    rng = np.random.default_rng(1)
+    zero_bins = []
+    for k in range(6):
+        a = rng.integers(0, 3, (B, S)).astype(np.int64)
+        env.step(torch.from_numpy(a))
+        ora.step(a)
+        st = statelayout.parse(ora.state_bytes(), B, S, cfg.queue_capacity, False,
+                               split_P=statelayout.split_p(cfg))
+        want, ts_w = _tv_from_oracle_state(st, B, S, vpp)
+        pub = vs.VppPublisher(env, path_fmt=os.path.join("/dev/shm", f"lbsim_m{os.getpid()}_{{}}"),
+                              n=B)
+        try:
+            tv, _, ts = pub.export()
+        finally:
+            pub.close()
+        np.testing.assert_array_equal(tv, want, err_msg=f"step {k}")
+        np.testing.assert_array_equal(ts, ts_w)
+        zero_bins.append(float((tv[..., 0] == 0).mean()))
+    if vpp:  # bins stay zero until a sample lands in them: fewer with every step
+        assert zero_bins[0] > zero_bins[-1] and zero_bins[0] > 0.05
+    env.close()
+    ora.close()
 
 
 @pytest.mark.gpu
