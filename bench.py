@@ -428,7 +428,7 @@ def graph_leg_child(args, kernel_ms, timeout_s: float = 420.0):
     context; it builds the same workload from the same arguments."""
     import subprocess
     argv = [sys.executable, os.path.abspath(__file__)] + [a for a in sys.argv[1:]] + \
-        ["--graph-child", repr(kernel_ms), "--no-cpu-baseline", "--prewarm-ms", "0"]
+        ["--graph-child", repr(kernel_ms), "--no-cpu-baseline"]
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK")}
     try:
@@ -591,7 +591,12 @@ def main():
     if args.workload == "rollout":
         common["autoreset_mode"] = args.autoreset_mode
     if args.graph_child is not None:  # the graph leg alone, in its own process (graph_leg_child)
+        # the same pre-warm as the eager leg (a scratch env, --prewarm-ms): without it the child's
+        # 20 replayed steps ran on a cold GPU's clocks (r06f: 0.283 ms/step against 0.262 eager
+        # on the same next-step kernels)
+        pw = prewarm_scratch(args, dev, B, S, common)
         res = graph_leg(args, dev, shard, B, S, dict(common), args.graph_child)
+        res["prewarm"] = pw
         print(json.dumps(res), flush=True)
         return
     prewarm = prewarm_scratch(args, dev, B, S, common)

@@ -1832,14 +1832,14 @@ __device__ __forceinline__ bool observe_chunk_full(const DevState& st, const Sim
 // S) of env b.  Split handles (lost-FIN, DevState::res_count_dur) give the duration reservoir its
 // own count and timestamps, hence its own decay weights: reservoir r then uses weight row r (S <= 2
 // per call), else the server's row r >> 1.
-template <bool US>
+template <bool US, bool SPLIT>
 __device__ __forceinline__ void observe_chunk_general(const DevState& st, const SimParams& p,
                                                       size_t b, int s_base, int S, ObsScratch& sc,
                                                       float* obs_out, int lane) {
   const size_t srow = b * (size_t)p.S + (size_t)s_base;  // first (env, server) of the chunk
   const int R = 2 * S;
   const int g = lane >> 3, j = lane & 7;
-  const bool split = US && st.res_count_dur != nullptr;
+  const bool split = US && SPLIT && st.res_count_dur != nullptr;
   const int wsh = split ? 0 : 1;  // reservoir r's weight row: r >> wsh
   // ---- phase 1: reservoirs into LDS, decay weights relative to each server's newest sample.
   //      Loads of 4 servers are issued before any is consumed (memory-level parallelism).
@@ -2093,7 +2093,9 @@ __device__ __forceinline__ void observe_chunk_general(const DevState& st, const 
 }
 
 
-template <bool US, bool INC, bool REGS = true>
+// SPLIT = false: the caller never sees a split (lost-FIN) handle -- the paired observe and the
+// one-wave-per-env forms -- and the split code is compiled out of it.
+template <bool US, bool INC, bool REGS = true, bool SPLIT = true>
 __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParams& p, size_t b,
                                               int s_base, int S, ObsScratch& sc, float* obs_out,
                                               int lane) {
@@ -2125,10 +2127,11 @@ __device__ __forceinline__ void observe_chunk(const DevState& st, const SimParam
   }
   // split handles: two servers (four weight rows) per pass; one call site (one inlined copy of
   // the general path: two cost observe_pair_kernel 9 more VGPR spills, 92 -> 102 us, r06f)
-  const int step = (US && st.res_count_dur != nullptr) ? 2 : S;
+  const int step = (US && SPLIT && st.res_count_dur != nullptr) ? 2 : S;
 #pragma clang loop unroll(disable)
   for (int h = 0; h < S; h += step)
-    observe_chunk_general<US>(st, p, b, s_base + h, S - h < step ? S - h : step, sc, obs_out, lane);
+    observe_chunk_general<US, SPLIT>(st, p, b, s_base + h, S - h < step ? S - h : step, sc,
+                                     obs_out, lane);
 }
 
 // ================================================================ reward (rewards.py)
@@ -2511,7 +2514,7 @@ __device__ __forceinline__ void observe_rows_paired(const DevState& st, const Si
   }
   for (int e = 0; e < nenv; ++e) {
     for (int s0 = 0; s0 < S; s0 += kObsChunk)
-      observe_chunk<true, INC, LBSIM_OBS_PAIR_FALLBACK_REGS != 0>(
+      observe_chunk<true, INC, LBSIM_OBS_PAIR_FALLBACK_REGS != 0, false>(
           st, p, b0 + (size_t)e, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk, sc,
           obs_out + e * S * NF, lane);
   }
@@ -2548,7 +2551,7 @@ __device__ __forceinline__ void observe_rows_paired_wide(const DevState& st, con
     return;
   }
   for (int c = s0; c < s0 + 8; c += kObsChunk)
-    observe_chunk<true, INC, LBSIM_OBS_PAIR_FALLBACK_REGS != 0>(st, p, b, c, kObsChunk, sc,
+    observe_chunk<true, INC, LBSIM_OBS_PAIR_FALLBACK_REGS != 0, false>(st, p, b, c, kObsChunk, sc,
                                                                  obs_env, lane);
 }
 
@@ -2798,7 +2801,7 @@ __device__ __forceinline__ void observe_env_wave(const DevState& st, const SimPa
                                                  float* s_obs, float* s_act, int lane) {
   const int S = p.S;
   if constexpr (MAXS <= kObsChunk) {  // one chunk: straight-line code, no loop-carried s0
-    observe_chunk<true, true>(st, p, b, 0, S, sc, s_obs, lane);
+    observe_chunk<true, true, true, false>(st, p, b, 0, S, sc, s_obs, lane);
   } else if (LBSIM_STEP_WAVE_PAIRED && MAXS <= 8 && st.res_dur == nullptr) {
     // paired records: the env's S <= 8 rows in one pass (observe_rows_paired)
     observe_rows_paired<true>(st, p, b, 1, sc, s_obs, lane);
@@ -2810,8 +2813,8 @@ __device__ __forceinline__ void observe_env_wave(const DevState& st, const SimPa
       size_t bb = b;
       int ln = lane;
       asm volatile("" : "+s"(bb), "+v"(ln));
-      observe_chunk<true, true>(st, p, bb, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk, sc, s_obs,
-                                ln);
+      observe_chunk<true, true, true, false>(st, p, bb, s0, S - s0 < kObsChunk ? S - s0 : kObsChunk,
+                                             sc, s_obs, ln);
     }
   }
   observe_outputs<MAXS, kModeStep, true>(st, p, out, b, s_obs, s_act, lane, 64);
