@@ -31,6 +31,10 @@
 namespace lbk {
 
 constexpr int kGroupWL = 8;  // LDS queue window per server: 64 lanes x 8 x 8 B = 4 KiB per wave
+// kModeStepNR: the Philox round keys formed inside the draw-ahead block (group_event_loop KEYS)
+#ifndef LBSIM_DYN_NR_KEYS
+#define LBSIM_DYN_NR_KEYS 1
+#endif
 
 // Reductions over the aligned G-lane group (G <= 16: one DPP row).  Lanes read only within their
 // group, so groups that left the event loop (inactive lanes) are never read.  mov_dpp with
@@ -810,8 +814,8 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
     const int nsteps = rs ? p.warmup_steps : 1;
     const float w = rs ? 1.0f : w_own;
     for (int k = 0; k < nsteps; ++k)
-      sim_step_group<G, POLICY, TRACE, true, FULL>(st, p, E, V, b, s, gbase, w, wall, win, atab,
-                                                   acache);
+      sim_step_group<G, POLICY, TRACE, LBSIM_DYN_NR_KEYS != 0, FULL>(st, p, E, V, b, s, gbase, w,
+                                                                     wall, win, atab, acache);
     if (rs) reset_out(-1);
   }
 
