@@ -31,9 +31,12 @@
 namespace lbk {
 
 constexpr int kGroupWL = 8;  // LDS queue window per server: 64 lanes x 8 x 8 B = 4 KiB per wave
-// kModeStepNR: the Philox round keys formed inside the draw-ahead block (group_event_loop KEYS)
+// kModeStepNR: 1 = the Philox round keys formed inside the draw-ahead block (group_event_loop
+// KEYS: 120 VGPRs, no spills); 0 = hoisted as in the plain step (126 VGPRs at the 4-wave cap, 4
+// spilled): 152.1-152.8 -> 150.6 us at 65536 x 4 (profiles/r06i/) -- the plain kernel shed the
+// full handles' code, so the hoisted keys fit the budget again
 #ifndef LBSIM_DYN_NR_KEYS
-#define LBSIM_DYN_NR_KEYS 1
+#define LBSIM_DYN_NR_KEYS 0
 #endif
 
 // Reductions over the aligned G-lane group (G <= 16: one DPP row).  Lanes read only within their
@@ -268,9 +271,8 @@ __device__ __forceinline__ GroupConst group_const(const SimParams& p, uint32_t b
 
 // The event loop of sim_step_group (section 2).  FAST (wave-uniform): every SED score finite, so no
 // NaN fallback division and no NaN ballot.  KEYS: the Philox round keys are formed inside the
-// draw-ahead block (kModeStepNR: the compiler otherwise hoists them into 20 loop-long VGPRs,
-// which took that kernel past the 4-wave budget); the plain step lets them be hoisted (measured
-// 4 us faster at 65536 x 4 than forming them in the block, profiles/r06c/).
+// draw-ahead block instead of being hoisted into 20 loop-long VGPRs (LBSIM_DYN_NR_KEYS for
+// kModeStepNR; the plain step hoists them: 4 us faster at 65536 x 4, profiles/r06c/).
 // FULL: the handle's features beyond the plain simulator -- n_flow_on_mode VPP's lost-flow counts,
 // a duration plane (duration_mode SERVICE), lost-FIN deferral (split reservoirs), reservoir_mode
 // VPP -- compiled only into dynamics_group_full_kernel, so none of their registers weigh on the
