@@ -264,6 +264,12 @@ typedef struct lbsim_step_outputs {
   float* state;            /* [B, 4S + 10] f32 get_state(): zeros, episode step / max_steps, A */
   int32_t num_agents;      /* A                                                               */
   int32_t servers_per_agent; /* k                                                             */
+  /* Completion word (one-env handles, B = 1, lbsim_step_ex only; NULL = none): the step launch
+   * stores done_value to *done_word (device-accessible host memory) after every other output of
+   * the step, with a system-scope release, so a host polling the word sees the outputs complete
+   * without a stream synchronisation (the single-env facade's step, problem-04 Trainer path). */
+  uint32_t* done_word;
+  uint32_t done_value;
 } lbsim_step_outputs_t;
 
 /* lbsim_step with every output optional except obs, reward and done. */

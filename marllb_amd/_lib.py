@@ -89,6 +89,8 @@ class StepOutputs(ctypes.Structure):
         ("state", ctypes.c_void_p),
         ("num_agents", ctypes.c_int32),
         ("servers_per_agent", ctypes.c_int32),
+        ("done_word", ctypes.c_void_p),
+        ("done_value", ctypes.c_uint32),
     ]
 
 

@@ -428,6 +428,8 @@ ObsOutputs obs_outputs(const lbsim_step_outputs_t* out, bool reset) {
     o.done = out->done;
     o.ep_len = out->episode_length;
     o.ep_ret = out->episode_return;
+    o.done_word = out->done_word;
+    o.done_value = out->done_value;
   }
   o.agent_obs = out->agent_obs;
   o.state = out->state;
@@ -697,6 +699,8 @@ int lbsim_step_ex(lbsim_t* h, const void* action, int action_dtype,
   }
   if (facade_bad(h, out)) return fail(h, LBSIM_EINVAL, "agent_obs / state need num_agents * "
                                                        "servers_per_agent == num_servers");
+  if (out->done_word != nullptr && h->B != 1)
+    return fail(h, LBSIM_EINVAL, "done_word needs a one-env handle (num_envs = 1)");
   DeviceGuard g(h->device);
   LaunchLog log(h, 0);
   const hipStream_t s = (hipStream_t)stream;

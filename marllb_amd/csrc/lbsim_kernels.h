@@ -2569,6 +2569,10 @@ struct ObsOutputs {
   float* agent_obs;
   float* state;
   int num_agents, servers_per_agent;
+  // one-env handles: the step's completion word (lbsim_step_outputs_t::done_word), stored after
+  // every other output with a system-scope release (observe_outputs)
+  uint32_t* done_word;
+  uint32_t done_value;
 };
 
 // One wave per 4-server chunk (kObsChunk), all chunks of an env in one workgroup: S = 4 -> one
@@ -2675,6 +2679,14 @@ __device__ __forceinline__ void observe_outputs(const DevState& st, const SimPar
         so[sd - 1] = (float)A;
       }
     }
+  }
+  if (out.done_word != nullptr) {  // one-env handles: the completion word, after every output
+    if (nthr == 64) wave_sync();
+    else __syncthreads();  // block-uniform
+    __threadfence_system();
+    if (tid == 0)
+      __hip_atomic_store(out.done_word, out.done_value, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

@@ -26,6 +26,10 @@ import numpy as np
 from . import _lib
 from .spaces import Box, MultiDiscrete
 
+# the single-env facade's step polls its completion word for at most this long before a stream
+# synchronisation (a step that runs longer, or a device fault, then goes through the runtime)
+_POLL_S = 0.05
+
 NF = 11  # observation columns per server (env.py:46-48)
 
 # env.py:377-381 — observation column order (column 10 is named flow_duration_avg_decay there)
@@ -607,6 +611,7 @@ class LoadBalanceEnv:
             max_steps=max_steps, normalize_obs=normalize_obs and not self._host_norm, seed=seed,
             **sim_kwargs)
         self._io = None
+        self._seq = 0
 
     # ---- spaces (env.py:156-184)
     def _setup_spaces(self):
@@ -625,10 +630,15 @@ class LoadBalanceEnv:
             act_dt = torch.int64 if self.action_type == "discrete" else torch.float32
             act_h = torch.zeros(self.num_servers, dtype=act_dt, pin_memory=True)
             done_h = torch.zeros(8, dtype=torch.uint8, pin_memory=True)
+            # the step's completion word (lbsim_step_outputs_t::done_word): polled instead of a
+            # stream synchronisation
+            flag_h = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self._flag = (flag_h, flag_h.numpy().view(np.uint32))
             out = _lib.StepOutputs()
             base = host.data_ptr()
             out.obs, out.raw_obs, out.reward = base, base + 4 * n, base + 8 * n
             out.done = done_h.data_ptr()
+            out.done_word = flag_h.data_ptr()
             stream = torch.cuda.current_stream(self._vec.device)
             dt = _lib.DTYPE_I64 if self.action_type == "discrete" else _lib.DTYPE_F32
             self._io = (host, host.numpy(), act_h, act_h.numpy(), done_h, out, stream,
@@ -658,11 +668,25 @@ class LoadBalanceEnv:
         hview, aview, stream, sptr, dt, n, aptr, outref = (io[1], io[3], io[6], io[7], io[8],
                                                            io[9], io[10], io[11])
         aview[:] = idx_or_w
+        # the launch stores this step's sequence number into the pinned completion word after
+        # every other output (system-scope release): spin on it instead of a stream sync, whose
+        # wake-up costs several us; past _POLL_S a plain synchronisation (which reports faults)
+        seq = self._seq = (self._seq + 1) & 0xFFFFFFFF or 1
+        io[5].done_value = seq
         rc = v.handle.lib.lbsim_step_ex(v.handle.h, aptr, dt, outref, sptr)
         if rc != _lib.OK:
             v.handle.check(rc)
         v._step_bound += 1
-        stream.synchronize()
+        fv = self._flag[1]
+        t0 = None
+        while fv[0] != seq:
+            if t0 is None:
+                t0 = time.perf_counter()
+            elif time.perf_counter() - t0 > _POLL_S:
+                stream.synchronize()
+                if fv[0] != seq:
+                    raise RuntimeError("lbsim step finished without its completion word")
+                break
         S = self.num_servers
         obs = hview[:n].reshape(S, NF).copy()
         raw = hview[n:2 * n].reshape(S, NF).copy()
