@@ -61,19 +61,19 @@ def build_library(force: bool = False, verbose: bool = False, jobs: int = 0,
                   variant: str | None = None, defines: tuple = (), only: tuple = ()) -> str:
     """Build liblbsim.so, or with `variant` an A/B build with extra `defines` into
     marllb_amd/exp/liblbsim_<variant>.so (loaded through LBSIM_LIBRARY, see _lib.py).  `only`
-    (object names, e.g. "dyn_step.o"): a variant compiles just those units and links the main
-    build's objects for the rest."""
+    (object names, e.g. "dyn_step.o"): compile just those units (a variant's own, or the main
+    build's when no variant is named) and link the main build's objects for the rest."""
     out, objdir = OUT, OBJDIR
     if variant:
         out = os.path.join(HERE, "exp", f"liblbsim_{variant}.so")
         objdir = os.path.join(ROOT, "build", f"lbsim_{variant}")
-    elif not force and up_to_date():
+    elif not force and not only and up_to_date():
         return OUT
     os.makedirs(objdir, exist_ok=True)
     os.makedirs(os.path.dirname(out), exist_ok=True)
     jobs = jobs or min(len(UNITS), os.cpu_count() or 1, 16)
     units = [(src, [*defs, *defines], os.path.join(objdir, obj)) for src, defs, obj in UNITS
-             if not (variant and only) or obj in only]
+             if not only or obj in only]
     with ThreadPoolExecutor(jobs) as ex:
         built = dict(zip([u[2] for u in units], ex.map(lambda u: _compile(u, verbose), units)))
     objs = [built.get(os.path.join(objdir, obj), os.path.join(OBJDIR, obj)) for _, _, obj in UNITS]

@@ -35,6 +35,15 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f4 splat4(float v) { return f4{v, v, v, v}; }
 
+// Timing diagnostic only (wrong results): LBSIM_EXP_L1W=1 makes every k-block past the first two
+// re-read one of the tile's first two weight blocks, so the weight stream fits in L1 and the run
+// shows what streaming the weights from L2 costs the policy kernels.
+#if LBSIM_EXP_L1W
+#define LBSIM_EXP_WBLK(n) ((n) & 1)
+#else
+#define LBSIM_EXP_WBLK(n) (n)
+#endif
+
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // acc[m] += X[rows 16m .. 16m+15, cols col0 .. col0 + 16 nkb) . W^T for one 16-column output tile
@@ -52,7 +61,7 @@ __device__ __forceinline__ void mma_tile(f4 (&acc)[MT], const float* lds, int ld
   for (int kb = 0; kb < nkb; ++kb) {
     const int n2 = kb + 2 < nkb ? kb + 2 : nkb - 1;
     const int n1 = kb + 1 < nkb ? kb + 1 : nkb - 1;
-    const f4 b2 = wp[n2 * 64 + lane];
+    const f4 b2 = wp[LBSIM_EXP_WBLK(n2) * 64 + lane];
     f4 an[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) an[m] = *(const f4*)(arow + m * 16 * ld + n1 * 16);
@@ -107,7 +116,7 @@ __device__ __forceinline__ void mma_multi(f4 (&acc)[NB][MT], const float* lds, i
     const int n1 = kb + 1 < nkb ? kb + 1 : nkb - 1;
     f4 b2[NB];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) b2[j] = wp[j][n2 * 64 + lane];
+    for (int j = 0; j < NB; ++j) b2[j] = wp[j][LBSIM_EXP_WBLK(n2) * 64 + lane];
     f4 an[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) an[m] = *(const f4*)(arow + m * 16 * ld + n1 * 16);
