@@ -179,8 +179,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dyn-mapping", default="auto", choices=["auto", "env", "server"],
                     help="dynamics kernel mapping: one lane per env / per server (same results)")
-    ap.add_argument("--graph-steps", type=int, default=5,
-                    help="steps captured per graph in the graph leg (one replay = that many steps)")
+    ap.add_argument("--graph-steps", type=int, default=20,
+                    help="steps captured per graph in the graph leg (one replay = that many steps: "
+                         "a replay costs ~27 us besides its kernels -- torch's two RNG-offset fill "
+                         "kernels and the launch -- so 20 steps amortise it to ~1.4 us per step, "
+                         "profiles/r06l/)")
     ap.add_argument("--no-graph", action="store_true",
                     help="skip the graph leg (N=1: the same workload with one step captured in a "
                          "hipGraph and replayed, reported beside `value` as `graph`)")

@@ -44,6 +44,23 @@ __device__ __forceinline__ f4 splat4(float v) { return f4{v, v, v, v}; }
 #define LBSIM_EXP_WBLK(n) (n)
 #endif
 
+// Timing diagnostic only (LBSIM_EXP_PHASES=1, pol.o of an A/B build): lane 0 of wave 0 of every
+// gridDim / 64-th workgroup records the 100 MHz clock at the kernel's phase boundaries into
+// lbsim_exp_ts[sample][phase] (read by lbsim_exp_phase_read, tools/policy_phases.py).
+#if LBSIM_EXP_PHASES
+__device__ unsigned long long lbsim_exp_ts[64 * 16];
+#define LB_PHASE(i)                                                                        \
+  do {                                                                                      \
+    const unsigned st_ = gridDim.x >= 64u ? gridDim.x / 64u : 1u;                           \
+    if (threadIdx.x == 0 && blockIdx.x % st_ == 0u && blockIdx.x / st_ < 64u)               \
+      lbsim_exp_ts[(blockIdx.x / st_) * 16u + (i)] = __builtin_amdgcn_s_memrealtime();     \
+  } while (0)
+#else
+#define LB_PHASE(i) \
+  do {              \
+  } while (0)
+#endif
+
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // acc[m] += X[rows 16m .. 16m+15, cols col0 .. col0 + 16 nkb) . W^T for one 16-column output tile
@@ -51,10 +68,9 @@ __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf
 // latency), A fragments one block ahead (LDS latency); the clamped tail re-reads the last block.
 template <int MT>
 __device__ __forceinline__ void mma_tile(f4 (&acc)[MT], const float* lds, int ld, int col0,
-                                         const f4* __restrict__ wp, int nkb, int lane) {
+                                         const f4* __restrict__ wp, int nkb, int lane, f4 b0,
+                                         f4 b1) {
   const float* arow = lds + (lane & 15) * ld + col0 + 4 * (lane >> 4);
-  f4 b0 = wp[lane];
-  f4 b1 = wp[(nkb > 1 ? 64 : 0) + lane];
   f4 a[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) a[m] = *(const f4*)(arow + m * 16 * ld);
@@ -75,6 +91,11 @@ __device__ __forceinline__ void mma_tile(f4 (&acc)[MT], const float* lds, int ld
     b0 = b1;
     b1 = b2;
   }
+}
+template <int MT>
+__device__ __forceinline__ void mma_tile(f4 (&acc)[MT], const float* lds, int ld, int col0,
+                                         const f4* __restrict__ wp, int nkb, int lane) {
+  mma_tile<MT>(acc, lds, ld, col0, wp, nkb, lane, wp[lane], wp[(nkb > 1 ? 64 : 0) + lane]);
 }
 
 // The first two k-blocks' B fragments of NB tiles, loaded ahead of mma_multi: a caller issues
@@ -142,16 +163,17 @@ __device__ __forceinline__ void mma_multi(f4 (&acc)[NB][MT], const float* lds, i
   mma_multi<MT, NB>(acc, lds, ld, col0, wp, nkb, lane, mma_prime<NB>(wp, nkb, lane));
 }
 
-// Dense layer, accumulate phase: wave w owns output tiles nt = w, w + 4, ... < ntiles, all in
-// one mma_multi pass (a wave with fewer tiles recomputes the last one; dense_store skips it).
-template <int MT, int NTW>
+// Dense layer, accumulate phase: wave w owns output tiles nt = w, w + WS, ... < ntiles (WS = the
+// waves sharing the layer), all in one mma_multi pass (a wave with fewer tiles recomputes the last
+// one; dense_store skips it).
+template <int MT, int NTW, int WS = 4>
 __device__ __forceinline__ void dense_acc(f4 (&acc)[NTW][MT], const float* lds, int ld, int col0,
                                           const float* __restrict__ w, int nkb, int ntiles,
                                           const float* __restrict__ bias, int wave, int lane) {
   const f4* wp[NTW];
 #pragma unroll
   for (int j = 0; j < NTW; ++j) {
-    const int nt = wave + 4 * j < ntiles ? wave + 4 * j : ntiles - 1;
+    const int nt = wave + WS * j < ntiles ? wave + WS * j : ntiles - 1;
     wp[j] = (const f4*)w + (size_t)nt * nkb * 64;
     const float bv = bias[nt * 16 + (lane & 15)];
 #pragma unroll
@@ -196,12 +218,12 @@ __device__ __forceinline__ void splitk_out(const float* lds, int ld, const float
 }
 
 // Dense layer, store phase (after a barrier): out[row][col0 + 16 nt + c] = act(acc, 16 nt + c).
-template <int MT, int NTW, class Act>
+template <int MT, int NTW, class Act, int WS = 4>
 __device__ __forceinline__ void dense_store(const f4 (&acc)[NTW][MT], float* lds, int ld, int col0,
                                             int ntiles, int wave, int lane, Act act) {
 #pragma unroll
   for (int j = 0; j < NTW; ++j) {
-    const int nt = wave + 4 * j;
+    const int nt = wave + WS * j;
     if (nt < ntiles) {
       const int c = nt * 16 + (lane & 15);
 #pragma unroll
@@ -285,9 +307,10 @@ __device__ __forceinline__ void gru_store(const f4 (&hn)[(H / 16 + 3) / 4][MT], 
 
 // Stage rows [row0, row0 + R) of a [B, n] matrix (row stride src_ld) into LDS cols [col0, col0 +
 // npad), zero past n, past B and (if reset_mask) for rows whose mask byte is set.  Eight elements
-// per thread per pass, all eight loads issued before the LDS stores: the policy kernels' staging
-// sits on their critical path (QMIX runs one round of workgroups), so its HBM latency is paid once
-// per eight elements, not once per element.
+// per thread per pass: the eight values are loaded from clamped in-range addresses with no
+// condition, then the eight mask bytes, and only then selected, so the sixteen loads are in flight
+// together (a load behind each row's mask byte waited for every earlier load: one HBM round trip
+// per element instead of one per pass, profiles/r06n/).
 __device__ __forceinline__ void stage_rows(float* lds, int ld, int col0, const float* src,
                                            int64_t src_ld, int n, int npad, int R, int64_t row0,
                                            int64_t B, const uint8_t* reset_mask) {
@@ -295,18 +318,28 @@ __device__ __forceinline__ void stage_rows(float* lds, int ld, int col0, const f
   for (int e0 = (int)threadIdx.x; e0 < total; e0 += 8 * nthr) {
     float v[8];
     int at[8];
+    int64_t bc[8];
+    bool ok[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int e = e0 + i * nthr;
       const int r = e / npad, c = e - r * npad;
       const int64_t b = row0 + r;
       at[i] = e < total ? r * ld + col0 + c : -1;
-      v[i] = (e < total && c < n && b < B && !(reset_mask && reset_mask[b])) ? src[b * src_ld + c]
-                                                                               : 0.0f;
+      ok[i] = e < total && c < n && b < B;
+      bc[i] = b < B ? b : B - 1;
+      v[i] = src[bc[i] * src_ld + (ok[i] ? c : 0)];
+    }
+    if (reset_mask != nullptr) {
+      uint8_t m[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) m[i] = reset_mask[bc[i]];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ok[i] = ok[i] && m[i] == 0;
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-      if (at[i] >= 0) lds[at[i]] = v[i];
+      if (at[i] >= 0) lds[at[i]] = ok[i] ? v[i] : 0.0f;
   }
 }
 
@@ -331,25 +364,39 @@ struct SacActorArgs {
 };
 
 // The SAC tile's input rows in one pass with no index division: thread t < kxp stages state
-// column t, kxp <= t < kxp + H hidden column t - kxp, each for all R rows (R independent loads in
-// flight per thread; a row's loads are contiguous across the threads).
+// column t, kxp <= t < kxp + H hidden column t - kxp, each for all R rows.  Every row's value is
+// loaded from a clamped in-range address with no condition, then (hidden columns) every row's
+// reset byte, then the selects: the R + R loads are in flight together.  (Loading each hidden value
+// behind its row's reset byte made every byte load wait for all earlier loads -- R HBM round trips,
+// 20 of a workgroup's 67 us, profiles/r06m/.)
 template <int R, int H>
 __device__ __forceinline__ void stage_sac_rows(float* lds, const SacActorArgs& p, int64_t row0) {
   const int t = threadIdx.x, kxp = p.kxp, ld = p.ld;
   for (int c = t; c < kxp + H; c += blockDim.x) {
     const bool st = c < kxp;
-    const float* src = st ? p.state + c : p.hidden + (c - kxp);
-    const int64_t stride = st ? p.I : H;
     const bool col_ok = !st || c < p.I;
+    const float* src = st ? p.state + (col_ok ? c : 0) : p.hidden + (c - kxp);
+    const int64_t stride = st ? p.I : H;
+    int64_t bc[R];
     float v[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int64_t b = row0 + r;
-      const bool live = col_ok && b < p.B && (st || !(p.reset && p.reset[b]));
-      v[r] = live ? src[b * stride] : 0.0f;
+      bc[r] = b < p.B ? b : p.B - 1;
+      v[r] = src[bc[r] * stride];
+    }
+    bool keep[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) keep[r] = col_ok && row0 + r < p.B;
+    if (!st && p.reset != nullptr) {
+      uint8_t m[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) m[r] = p.reset[bc[r]];
+#pragma unroll
+      for (int r = 0; r < R; ++r) keep[r] = keep[r] && m[r] == 0;
     }
 #pragma unroll
-    for (int r = 0; r < R; ++r) lds[r * ld + c] = v[r];
+    for (int r = 0; r < R; ++r) lds[r * ld + c] = keep[r] ? v[r] : 0.0f;
   }
 }
 
@@ -365,6 +412,7 @@ __global__ void __launch_bounds__(256, LBSIM_SAC_WPE) sac_actor_kernel(SacActorA
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t row0 = (int64_t)blockIdx.x * R;
   const int ld = p.ld, kxp = p.kxp;
+  LB_PHASE(0);
 #if LBSIM_SAC_OLD_STAGE
   stage_rows(lds, ld, 0, p.state, p.I, p.I, kxp, R, row0, p.B, nullptr);
   stage_rows(lds, ld, kxp, p.hidden, H, H, H, R, row0, p.B, p.reset);
@@ -372,26 +420,32 @@ __global__ void __launch_bounds__(256, LBSIM_SAC_WPE) sac_actor_kernel(SacActorA
   stage_sac_rows<R, H>(lds, p, row0);
 #endif
   __syncthreads();
+  LB_PHASE(1);
   {
     f4 hn[(H / 16 + 3) / 4][MT];
     gru_tile<MT, H>(hn, lds, ld, kxp, p.w_ih, p.w_hh, p.b_ih, p.b_hh, wave, lane);
+    LB_PHASE(2);
     __syncthreads();
     gru_store<MT, H>(hn, lds, ld, kxp, p.hidden, H, row0, p.B, wave, lane);
   }
   __syncthreads();
+  LB_PHASE(3);
   {
     constexpr int NT = F / 16, NTW = (NT + 3) / 4;
     f4 acc[NTW][MT];
     dense_acc<MT, NTW>(acc, lds, ld, kxp, p.w1, H / 16, NT, p.b1, wave, lane);
+    LB_PHASE(4);
     __syncthreads();
     dense_store<MT, NTW>(acc, lds, ld, 0, NT, wave, lane, ReluAct{});
   }
   __syncthreads();
+  LB_PHASE(5);
   // heads [mean | log_std] (2A <= 32 columns), K split over the waves; y over the first 2A
   // columns of the tile
   splitk_out<MT>(lds, ld, p.wh, p.bh, F / 16, (2 * p.A + 15) / 16, lds + R * ld, lds, ld,
                  2 * p.A, wave, lane);
   __syncthreads();
+  LB_PHASE(6);
   const int A = p.A;
   for (int e = threadIdx.x; e < R * A; e += blockDim.x) {
     const int r = e / A, a = e - r * A;
@@ -411,6 +465,7 @@ __global__ void __launch_bounds__(256, LBSIM_SAC_WPE) sac_actor_kernel(SacActorA
     p.action[b * A + a] = tanhf(x) * p.scale + p.bias;
     if (p.log_std) p.log_std[b * A + a] = ls;
   }
+  LB_PHASE(7);
 }
 
 // ------------------------------------------------------------------------------ QMIX policy
@@ -445,15 +500,36 @@ struct QmixMixAct {
   }
 };
 
-// QMixingNetwork.forward (mixing_network.py:78-117) of the tile, all 4 waves, after the agents:
-// chosen[R][A] holds the chosen Q-values; the LDS tile [R][p.ld] is free.
+// QMixingNetwork.forward (mixing_network.py:78-117) of the tile, by the workgroup's NW waves (4:
+// qmix_policy_kernel / the wave kernel, 8: the pair kernel), after the agents: chosen[R][A] holds
+// the chosen Q-values; the LDS tile [R][p.ld] is free.
 // pre: the state rows already staged (qmix_agent_pair_kernel loads them at its start, so their
 // HBM latency hides behind the agents), [R][pre_ld]; else they are staged here.
-template <int MT>
+// With 8 waves (round 6, profiles/r06n/): every wave takes part in both GEMM layers (2 first-layer
+// tiles, <= 2 second-layer tiles each instead of 4 / 3 on waves 0-3), the second layer's first
+// weight blocks are requested before the first layer's barrier, and the ELU tail runs one thread
+// per (row, embedding unit) with a 32-lane sum (it ran 4 threads per row on one wave: 4.1 us).
+#ifndef LBSIM_MIX_PRIME
+#define LBSIM_MIX_PRIME 1
+#endif
+// waves per SIMD the pair kernel is built for: 4 = two 8-wave workgroups per CU (<= 128 VGPRs)
+#ifndef LBSIM_QMIX_PAIR_WPE
+#define LBSIM_QMIX_PAIR_WPE 4
+#endif
+#ifndef LBSIM_MIX_NW
+#define LBSIM_MIX_NW 8
+#endif
+#ifndef LBSIM_MIX_TAIL
+#define LBSIM_MIX_TAIL 1
+#endif
+template <int MT, int NW = 4>
 __device__ __forceinline__ void qmix_mixer(const QmixArgs& p, float* lds, const float* chosen,
                                            int64_t row0, int wave, int lane,
                                            const float* pre = nullptr, int pre_ld = 0) {
+  static_assert(NW == 4 || NW == 8, "4- or 8-wave workgroups");
   constexpr int R = 16 * MT;
+  constexpr int J1 = 16 / NW;  // first-layer tiles per wave (3 he + E <= 256 columns)
+  constexpr int J2 = 16 / NW;  // second-layer tiles per wave (A E + E + 16 <= 256 columns)
   const int ld = p.ld, A = p.A;
   if (pre == nullptr) {
     stage_rows(lds, ld, 0, p.state, p.Ds, p.Ds, p.ksp, R, row0, p.B, nullptr);
@@ -462,44 +538,61 @@ __device__ __forceinline__ void qmix_mixer(const QmixArgs& p, float* lds, const 
   const float* x0 = pre != nullptr ? pre : lds;
   const int x0_ld = pre != nullptr ? pre_ld : ld;
   const int he = p.he, E = p.E;
-  const bool mw = wave < 4;  // the mixer's GEMMs run on waves 0-3 (8-wave workgroups: the others
-                             // only meet the barriers)
+  const bool mw = wave < NW;  // the mixer's GEMM waves (a larger workgroup's others only meet
+                              // the barriers)
+  // second layers: w1 tiles (A E / 16) from cols [0, he), w2 tiles (E / 16) from [he, 2 he),
+  // b2 (one tile) from [2 he, 3 he); outputs to cols [0, A E), [A E, A E + E), A E + E
+  const int n1 = A * E / 16, n2 = E / 16, ntot = n1 + n2 + 1, kb = he / 16;
+  const f4* w2p[J2];
+  const float* b2p[J2];
+  int c2[J2];
+  f4 pb0[J2], pb1[J2];
+#pragma unroll
+  for (int j = 0; j < J2; ++j) {
+    const int t0 = wave + NW * j, t = t0 < ntot ? t0 : ntot - 1;
+    const float* w;
+    if (t < n1) {
+      w = p.mw1, b2p[j] = p.mbw1, c2[j] = 0;
+    } else if (t < n1 + n2) {
+      w = p.mw2, b2p[j] = p.mbw2, c2[j] = he;
+    } else {
+      w = p.mb2, b2p[j] = p.mbb2, c2[j] = 2 * he;
+    }
+    const int tt = t < n1 ? t : (t < n1 + n2 ? t - n1 : 0);
+    w2p[j] = (const f4*)w + (size_t)tt * kb * 64;
+    b2p[j] += tt * 16;
+    if (NW == 8 && LBSIM_MIX_PRIME && mw) {  // requested now: their latency hides behind the first layer
+      pb0[j] = w2p[j][lane];
+      pb1[j] = w2p[j][(kb > 1 ? 64 : 0) + lane];
+    }
+  }
   {
     const int nt0 = (3 * he + E) / 16;  // <= 16
-    f4 acc[4][MT];
-    if (mw) dense_acc<MT, 4>(acc, x0, x0_ld, 0, p.m0, p.ksp / 16, nt0, p.mb0, wave, lane);
+    f4 acc[J1][MT];
+    if (mw) dense_acc<MT, J1, NW>(acc, x0, x0_ld, 0, p.m0, p.ksp / 16, nt0, p.mb0, wave, lane);
     __syncthreads();
-    if (mw) dense_store<MT, 4>(acc, lds, ld, 0, nt0, wave, lane, QmixMixAct{3 * he});
+    if (mw) dense_store<MT, J1, QmixMixAct, NW>(acc, lds, ld, 0, nt0, wave, lane, QmixMixAct{3 * he});
   }
   __syncthreads();
+  LB_PHASE(8);
   {
-    // second layers: w1 tiles (A E / 16) from cols [0, he), w2 tiles (E / 16) from [he, 2 he),
-    // b2 (one tile) from [2 he, 3 he); outputs to cols [0, A E), [A E, A E + E), A E + E
-    const int n1 = A * E / 16, n2 = E / 16, ntot = n1 + n2 + 1, kb = he / 16;
-    f4 acc[4][MT];
+    f4 acc[J2][MT];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int t = wave + 4 * j;
+    for (int j = 0; j < J2; ++j) {
+      const int t = wave + NW * j;
       if (!mw || t >= ntot) continue;
-      const float* w;
-      const float* bias;
-      int col0, tt;
-      if (t < n1) {
-        w = p.mw1, bias = p.mbw1, col0 = 0, tt = t;
-      } else if (t < n1 + n2) {
-        w = p.mw2, bias = p.mbw2, col0 = he, tt = t - n1;
-      } else {
-        w = p.mb2, bias = p.mbb2, col0 = 2 * he, tt = 0;
-      }
-      const float bv = bias[tt * 16 + (lane & 15)];
+      const float bv = b2p[j][lane & 15];
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[j][m] = splat4(bv);
-      mma_tile<MT>(acc[j], lds, ld, col0, (const f4*)w + (size_t)tt * kb * 64, kb, lane);
+      if (NW == 8 && LBSIM_MIX_PRIME)
+        mma_tile<MT>(acc[j], lds, ld, c2[j], w2p[j], kb, lane, pb0[j], pb1[j]);
+      else
+        mma_tile<MT>(acc[j], lds, ld, c2[j], w2p[j], kb, lane);
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int t = wave + 4 * j;
+    for (int j = 0; j < J2; ++j) {
+      const int t = wave + NW * j;
       if (!mw || t >= ntot) continue;
       const bool is_abs = t < n1 + n2;  // |W1|, |W2| (mixing_network.py:96,105)
       const int c = t * 16 + (lane & 15);
@@ -513,10 +606,28 @@ __device__ __forceinline__ void qmix_mixer(const QmixArgs& p, float* lds, const 
     }
   }
   __syncthreads();
-  // tail: hidden_e = elu(b1_e + sum_a q_a |w1[a E + e]|), Q_tot = sum_e hidden_e |w2_e| + b2;
+  LB_PHASE(9);
+  // tail: hidden_e = elu(b1_e + sum_a q_a |w1[a E + e]|), Q_tot = sum_e hidden_e |w2_e| + b2
+  const int b1c = 3 * he, w2c = A * E, b2c = A * E + E;
+  if (LBSIM_MIX_TAIL && NW * 64 == R * 32 && E == 32) {
+    // one thread per (row, unit): rows r = tid / 32 of the wave's two halves, a 32-lane sum
+    const int r = (int)threadIdx.x >> 5, u = (int)threadIdx.x & 31;
+    const float* row = lds + r * ld;
+    float h = 0.0f;
+    for (int a = 0; a < A; ++a) h += chosen[r * A + a] * row[a * E + u];
+    h += row[b1c + u];
+    h = h > 0.0f ? h : expm1f(h);
+    float acc = h * row[w2c + u];
+    acc += __shfl_xor(acc, 16);
+    acc += __shfl_xor(acc, 8);
+    acc += __shfl_xor(acc, 4);
+    acc += __shfl_xor(acc, 2);
+    acc += __shfl_xor(acc, 1);
+    if (u == 0 && row0 + r < p.B) p.q_tot[row0 + r] = acc + row[b2c];
+    return;
+  }
   // 4 threads per row, E / 4 embedding units each, combined by shuffles (R * 4 is a multiple of
   // 64, so every wave is either fully inside the loop or fully outside it)
-  const int b1c = 3 * he, w2c = A * E, b2c = A * E + E;
   for (int e0 = threadIdx.x; e0 < R * 4; e0 += blockDim.x) {
     const int r = e0 >> 2, part = e0 & 3;
     const float* row = lds + r * ld;
@@ -744,7 +855,7 @@ __global__ void __launch_bounds__(256) qmix_agent_wave_kernel(QmixArgs p) {
 // four per SIMD instead of two to hide the MFMA and L2 latency.  The pair shares the agent's LDS
 // region; every layer boundary is a workgroup barrier (all agents run the same layer sequence).
 template <int H, int F>
-__global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
+__global__ void __launch_bounds__(512, LBSIM_QMIX_PAIR_WPE) qmix_agent_pair_kernel(QmixArgs p) {
   const uint32_t step = p.step_dev != nullptr ? *p.step_dev : p.step;
   extern __shared__ float lds[];
   constexpr int R = 16, UT = H / 16, NT = F / 16;
@@ -753,6 +864,7 @@ __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
   const int a = wave >> 1, h = wave & 1;
   const int64_t row0 = (int64_t)blockIdx.x * R;
   const int lda = p.lda, kxp = p.kxp, A = p.A, NQ = p.n_act;
+  LB_PHASE(0);
   float* mine = lds + a * R * lda;
   float* qv = lds + 4 * R * lda;    // [A][R][16]
   float* chosen = qv + A * R * 16;  // [R][A]
@@ -780,34 +892,83 @@ __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
     eps_d = philox4x32_10(u32x4{(uint32_t)(row0 + lane), step, (uint32_t)a, 4u << 24}, p.key0,
                           p.key1);
   // one round of 512 workgroups: the staging's HBM latency is exposed, so every thread issues all
-  // its loads before its LDS stores (column-owner form, no index division): obs column c = t2 (+
-  // 128 k) of the 16 rows, hidden column t2 mod H of 16 H / 128 rows
-  if (p.sld > 0) stage_rows(pre, p.sld, 0, p.state, p.Ds, p.Ds, p.ksp, R, row0, p.B, nullptr);
-  for (int c = t2; c < kxp; c += 128) {  // obs rows of agent a, zero padded
-    float v[R];
+  // its loads -- obs column t2 of the 16 rows (kxp <= 128), hidden column t2 mod H of 16 H / 128
+  // rows and their reset bytes, the mixer's state rows -- before any LDS store: values from
+  // clamped in-range addresses with no condition, selects at the stores (one HBM round trip; the
+  // three loops one after the other waited out three, and a hidden load behind its row's reset byte
+  // waited for every earlier load, profiles/r06m/ r06n/)
+  static_assert(128 % H == 0 && R * H % 128 == 0, "hidden staging: whole rows per thread group");
+  constexpr int RH = R * H / 128;  // hidden rows per thread
+  const bool obs1 = kxp <= 128;    // one obs column per thread (else the loop below)
+  const bool ocol = t2 < p.I;
+  float vo[R];
+  if (obs1) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const int64_t b = row0 + r;
-      v[r] = (c < p.I && b < p.B) ? p.obs[(b * A + a) * p.I + c] : 0.0f;
+      const int64_t b = row0 + r, bc = b < p.B ? b : p.B - 1;
+      vo[r] = p.obs[(bc * A + a) * p.I + (ocol ? t2 : 0)];
     }
-#pragma unroll
-    for (int r = 0; r < R; ++r) mine[r * lda + c] = v[r];
   }
-  {
-    static_assert(128 % H == 0 && R * H % 128 == 0, "hidden staging: whole rows per thread group");
-    constexpr int RH = R * H / 128;  // rows per thread
-    const int c = t2 % H, rh0 = (t2 / H) * RH;
-    float v[RH];
+  const int hc = t2 % H, rh0 = (t2 / H) * RH;
+  float vh[RH];
+  int64_t bch[RH];
 #pragma unroll
-    for (int i = 0; i < RH; ++i) {  // hidden rows (zeros for reset envs)
-      const int64_t b = row0 + rh0 + i;
-      const bool live = b < p.B && !(p.reset && p.reset[b]);
-      v[i] = live ? p.hidden[(b * A + a) * H + c] : 0.0f;
+  for (int i = 0; i < RH; ++i) {
+    const int64_t b = row0 + rh0 + i;
+    bch[i] = b < p.B ? b : p.B - 1;
+    vh[i] = p.hidden[(bch[i] * A + a) * H + hc];
+  }
+  // the mixer's state rows (up to 3 elements per thread), stored to LDS with the rest
+  constexpr int NSR = 3;
+  const bool pre3 = p.sld > 0 && R * p.ksp <= NSR * 512;
+  const int tid = (int)threadIdx.x, tots = pre3 ? R * p.ksp : 0;
+  float vs[NSR];
+  int sat[NSR];
+#pragma unroll
+  for (int k = 0; k < NSR; ++k) {
+    const int e = tid + 512 * k, r = e / p.ksp, c = e - r * p.ksp;
+    const int64_t b = row0 + r, bc = b < p.B ? b : p.B - 1;
+    const bool ok = e < tots && c < p.Ds && b < p.B;
+    sat[k] = e < tots ? (ok ? r * p.sld + c : -(r * p.sld + c) - 1) : INT32_MIN;
+    vs[k] = p.state[bc * p.Ds + (ok ? c : 0)];
+  }
+  // the reset bytes last: their compares (hoisted into the branch) wait for every load above,
+  // which are all in flight by then -- one HBM round trip for the whole staging
+  bool keep[RH];
+#pragma unroll
+  for (int i = 0; i < RH; ++i) keep[i] = row0 + rh0 + i < p.B;
+  if (p.reset != nullptr) {
+    uint8_t m[RH];
+#pragma unroll
+    for (int i = 0; i < RH; ++i) m[i] = p.reset[bch[i]];
+#pragma unroll
+    for (int i = 0; i < RH; ++i) keep[i] = keep[i] && m[i] == 0;
+  }
+  if (obs1) {
+    if (t2 < kxp)
+#pragma unroll
+      for (int r = 0; r < R; ++r) mine[r * lda + t2] = (ocol && row0 + r < p.B) ? vo[r] : 0.0f;
+  } else {
+    for (int c = t2; c < kxp; c += 128) {  // obs rows of agent a, zero padded (kxp > 128)
+      const bool col_ok = c < p.I;
+      float v[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int64_t b = row0 + r, bc = b < p.B ? b : p.B - 1;
+        v[r] = p.obs[(bc * A + a) * p.I + (col_ok ? c : 0)];
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) mine[r * lda + c] = (col_ok && row0 + r < p.B) ? v[r] : 0.0f;
     }
-#pragma unroll
-    for (int i = 0; i < RH; ++i) mine[(rh0 + i) * lda + kxp + c] = v[i];
   }
+#pragma unroll
+  for (int i = 0; i < RH; ++i) mine[(rh0 + i) * lda + kxp + hc] = keep[i] ? vh[i] : 0.0f;
+#pragma unroll
+  for (int k = 0; k < NSR; ++k)
+    if (sat[k] != INT32_MIN) pre[sat[k] >= 0 ? sat[k] : -sat[k] - 1] = sat[k] >= 0 ? vs[k] : 0.0f;
+  if (p.sld > 0 && !pre3) stage_rows(pre, p.sld, 0, p.state, p.Ds, p.Ds, p.ksp, R, row0, p.B, nullptr);
   __syncthreads();
+  LB_PHASE(1);
   const float* bi = p.b_ih + a * 3 * H;
   const float* bh = p.b_hh + a * 3 * H;
   f4 hn[UT / 2][1];
@@ -851,6 +1012,7 @@ __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
     fc_wp(0, wp);
     bp_fc = mma_prime<4>(wp, H / 16, lane);
   }
+  LB_PHASE(2);
   __syncthreads();  // both halves have read the old hidden state
 #pragma unroll
   for (int uu = 0; uu < UT / 2; ++uu)
@@ -861,6 +1023,7 @@ __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
       if (row0 + r < p.B) p.hidden[((row0 + r) * A + a) * H + col] = hn[uu][0][i];
     }
   __syncthreads();
+  LB_PHASE(3);
 #pragma unroll
   for (int layer = 0; layer < 2; ++layer) {  // fc1 (H -> F) then fc2 (F -> F), ReLU
     const int col0 = layer == 0 ? kxp : 0, nkb = layer == 0 ? H / 16 : F / 16;
@@ -886,6 +1049,7 @@ __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
             v > 0.0f ? v : 0.0f;
       }
     __syncthreads();
+    LB_PHASE(4 + layer);
   }
   // fc3 -> Q-values (<= 16 actions: one tile), k-blocks [h NT/2, (h+1) NT/2); the halves meet in LDS
   {
@@ -904,6 +1068,7 @@ __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
       }
   }
   __syncthreads();
+  LB_PHASE(6);
   if (h == 0 && lane < R) {  // epsilon-greedy for (env lane, agent a), as qmix_policy_kernel
     const int r = lane;
     const int64_t b = row0 + r;
@@ -925,7 +1090,9 @@ __global__ void __launch_bounds__(512) qmix_agent_pair_kernel(QmixArgs p) {
     }
   }
   __syncthreads();
-  qmix_mixer<1>(p, lds, chosen, row0, wave, lane, p.sld > 0 ? pre : nullptr, p.sld);
+  LB_PHASE(7);
+  qmix_mixer<1, LBSIM_MIX_NW>(p, lds, chosen, row0, wave, lane, p.sld > 0 ? pre : nullptr, p.sld);
+  LB_PHASE(10);
 }
 
 }  // namespace lbk

@@ -36,3 +36,13 @@ int launch_qmix_policy(QmixArgs& a, int64_t B, int form, int mt, size_t lds, hip
 }
 
 }  // namespace lbk
+
+#if LBSIM_EXP_PHASES
+// timing diagnostic (lbsim_fused.h LB_PHASE): the last policy launch's phase clocks, 64 x 16 u64
+extern "C" int lbsim_exp_phase_read(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(lbk::lbsim_exp_ts), sizeof(lbk::lbsim_exp_ts)) ==
+                 hipSuccess
+             ? 0
+             : -1;
+}
+#endif

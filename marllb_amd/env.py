@@ -612,6 +612,8 @@ class LoadBalanceEnv:
             **sim_kwargs)
         self._io = None
         self._seq = 0
+        self._dw32 = None  # (discrete_weights as a tuple, the same as float32 values in a list)
+        self._active_lut: Dict[bytes, List[int]] = {}
 
     # ---- spaces (env.py:156-184)
     def _setup_spaces(self):
@@ -781,6 +783,8 @@ class LoadBalanceEnv:
         return obs, self._last_raw, self._shm_reward(self._last_raw), obs_dict
 
     def step(self, action) -> Tuple[np.ndarray, float, bool, Dict[str, Any]]:
+        if self._plumb is None and not (self.use_shm and self.shm is not None):
+            return self._step_sim(action)
         self.current_step += 1
         weights = self._action_to_weights(action)  # IndexError on a bad index, as env.py:346
         if self._plumb is not None:  # env.py:255-286, simulation mode
@@ -812,6 +816,50 @@ class LoadBalanceEnv:
             "step": self.current_step,
             "weights": weights.tolist(),
             "active_servers": active,
+            "episode_return": self.episode_return,
+        }
+        if done:
+            info["episode"] = {"r": self.episode_return, "l": self.current_step}
+        return next_obs, reward, done, info
+
+    def _step_sim(self, action) -> Tuple[np.ndarray, float, bool, Dict[str, Any]]:
+        """step() on the GPU simulator (no SHM, no plumbing): the same results and info as the
+        general path, with its host bookkeeping in list form (the problem-04 Trainer calls this
+        once per simulated step and waits for it)."""
+        self.current_step += 1
+        if self.action_type == "discrete":
+            # env.py:346: discrete_weights[int(a)] (IndexError on a bad index, negative indices as
+            # Python's), reported as the float32 values the reference's np.array holds
+            idx = np.asarray(action).reshape(-1)
+            il = idx.tolist()
+            dw = self.discrete_weights
+            key = tuple(dw)
+            if self._dw32 is None or self._dw32[0] != key:
+                self._dw32 = (key, np.asarray(dw, dtype=np.float32).tolist())
+            w32 = self._dw32[1]
+            weights = [w32[int(a)] for a in il]
+            act = idx if idx.dtype == np.int64 else idx.astype(np.int64)
+        else:
+            wa = action_to_weights(action, self.action_type, self.discrete_weights,
+                                   self.min_weight, self.max_weight)
+            weights = wa.tolist()
+            act = np.asarray(action).reshape(-1).astype(np.float32)
+        next_obs, raw, reward = self._sim_step(act)
+        self._last_raw = raw
+        self._last_obs_dict = None  # built when render asks (env.py:391-423)
+        self._last_obs_step = self.current_step
+        self.episode_rewards.append(reward)
+        self.episode_return += reward
+        done = self.current_step >= self.max_steps
+        # env.py:410-413 (active = any feature > 0), one lookup per activity pattern
+        pat = (raw > 0).any(1).tobytes()
+        act_l = self._active_lut.get(pat)
+        if act_l is None:
+            act_l = self._active_lut[pat] = np.flatnonzero(np.frombuffer(pat, np.bool_)).tolist()
+        info = {
+            "step": self.current_step,
+            "weights": weights,
+            "active_servers": list(act_l),
             "episode_return": self.episode_return,
         }
         if done:
