@@ -372,6 +372,11 @@ struct SacActorArgs {
 template <int R, int H>
 __device__ __forceinline__ void stage_sac_rows(float* lds, const SacActorArgs& p, int64_t row0) {
   const int t = threadIdx.x, kxp = p.kxp, ld = p.ld;
+#if LBSIM_EXP_NOSTAGE  // timing diagnostic (wrong results): no HBM reads in the staging
+  for (int c = t; c < kxp + H; c += blockDim.x)
+    for (int r = 0; r < R; ++r) lds[r * ld + c] = 0.01f * (float)c;
+  return;
+#endif
   for (int c = t; c < kxp + H; c += blockDim.x) {
     const bool st = c < kxp;
     const bool col_ok = !st || c < p.I;
@@ -419,33 +424,34 @@ __global__ void __launch_bounds__(256, LBSIM_SAC_WPE) sac_actor_kernel(SacActorA
 #else
   stage_sac_rows<R, H>(lds, p, row0);
 #endif
-  __syncthreads();
   LB_PHASE(1);
+  __syncthreads();
+  LB_PHASE(2);
   {
     f4 hn[(H / 16 + 3) / 4][MT];
     gru_tile<MT, H>(hn, lds, ld, kxp, p.w_ih, p.w_hh, p.b_ih, p.b_hh, wave, lane);
-    LB_PHASE(2);
+    LB_PHASE(3);
     __syncthreads();
     gru_store<MT, H>(hn, lds, ld, kxp, p.hidden, H, row0, p.B, wave, lane);
   }
   __syncthreads();
-  LB_PHASE(3);
+  LB_PHASE(4);
   {
     constexpr int NT = F / 16, NTW = (NT + 3) / 4;
     f4 acc[NTW][MT];
     dense_acc<MT, NTW>(acc, lds, ld, kxp, p.w1, H / 16, NT, p.b1, wave, lane);
-    LB_PHASE(4);
+    LB_PHASE(5);
     __syncthreads();
     dense_store<MT, NTW>(acc, lds, ld, 0, NT, wave, lane, ReluAct{});
   }
   __syncthreads();
-  LB_PHASE(5);
+  LB_PHASE(6);
   // heads [mean | log_std] (2A <= 32 columns), K split over the waves; y over the first 2A
   // columns of the tile
   splitk_out<MT>(lds, ld, p.wh, p.bh, F / 16, (2 * p.A + 15) / 16, lds + R * ld, lds, ld,
                  2 * p.A, wave, lane);
   __syncthreads();
-  LB_PHASE(6);
+  LB_PHASE(7);
   const int A = p.A;
   for (int e = threadIdx.x; e < R * A; e += blockDim.x) {
     const int r = e / A, a = e - r * A;
@@ -465,7 +471,7 @@ __global__ void __launch_bounds__(256, LBSIM_SAC_WPE) sac_actor_kernel(SacActorA
     p.action[b * A + a] = tanhf(x) * p.scale + p.bias;
     if (p.log_std) p.log_std[b * A + a] = ls;
   }
-  LB_PHASE(7);
+  LB_PHASE(8);
 }
 
 // ------------------------------------------------------------------------------ QMIX policy
@@ -574,7 +580,7 @@ __device__ __forceinline__ void qmix_mixer(const QmixArgs& p, float* lds, const 
     if (mw) dense_store<MT, J1, QmixMixAct, NW>(acc, lds, ld, 0, nt0, wave, lane, QmixMixAct{3 * he});
   }
   __syncthreads();
-  LB_PHASE(8);
+  LB_PHASE(9);
   {
     f4 acc[J2][MT];
 #pragma unroll
@@ -606,7 +612,7 @@ __device__ __forceinline__ void qmix_mixer(const QmixArgs& p, float* lds, const 
     }
   }
   __syncthreads();
-  LB_PHASE(9);
+  LB_PHASE(10);
   // tail: hidden_e = elu(b1_e + sum_a q_a |w1[a E + e]|), Q_tot = sum_e hidden_e |w2_e| + b2
   const int b1c = 3 * he, w2c = A * E, b2c = A * E + E;
   if (LBSIM_MIX_TAIL && NW * 64 == R * 32 && E == 32) {
@@ -967,8 +973,9 @@ __global__ void __launch_bounds__(512, LBSIM_QMIX_PAIR_WPE) qmix_agent_pair_kern
   for (int k = 0; k < NSR; ++k)
     if (sat[k] != INT32_MIN) pre[sat[k] >= 0 ? sat[k] : -sat[k] - 1] = sat[k] >= 0 ? vs[k] : 0.0f;
   if (p.sld > 0 && !pre3) stage_rows(pre, p.sld, 0, p.state, p.Ds, p.Ds, p.ksp, R, row0, p.B, nullptr);
-  __syncthreads();
   LB_PHASE(1);
+  __syncthreads();
+  LB_PHASE(2);
   const float* bi = p.b_ih + a * 3 * H;
   const float* bh = p.b_hh + a * 3 * H;
   f4 hn[UT / 2][1];
@@ -1012,7 +1019,7 @@ __global__ void __launch_bounds__(512, LBSIM_QMIX_PAIR_WPE) qmix_agent_pair_kern
     fc_wp(0, wp);
     bp_fc = mma_prime<4>(wp, H / 16, lane);
   }
-  LB_PHASE(2);
+  LB_PHASE(3);
   __syncthreads();  // both halves have read the old hidden state
 #pragma unroll
   for (int uu = 0; uu < UT / 2; ++uu)
@@ -1023,7 +1030,7 @@ __global__ void __launch_bounds__(512, LBSIM_QMIX_PAIR_WPE) qmix_agent_pair_kern
       if (row0 + r < p.B) p.hidden[((row0 + r) * A + a) * H + col] = hn[uu][0][i];
     }
   __syncthreads();
-  LB_PHASE(3);
+  LB_PHASE(4);
 #pragma unroll
   for (int layer = 0; layer < 2; ++layer) {  // fc1 (H -> F) then fc2 (F -> F), ReLU
     const int col0 = layer == 0 ? kxp : 0, nkb = layer == 0 ? H / 16 : F / 16;
@@ -1049,7 +1056,7 @@ __global__ void __launch_bounds__(512, LBSIM_QMIX_PAIR_WPE) qmix_agent_pair_kern
             v > 0.0f ? v : 0.0f;
       }
     __syncthreads();
-    LB_PHASE(4 + layer);
+    LB_PHASE(5 + layer);
   }
   // fc3 -> Q-values (<= 16 actions: one tile), k-blocks [h NT/2, (h+1) NT/2); the halves meet in LDS
   {
@@ -1068,7 +1075,7 @@ __global__ void __launch_bounds__(512, LBSIM_QMIX_PAIR_WPE) qmix_agent_pair_kern
       }
   }
   __syncthreads();
-  LB_PHASE(6);
+  LB_PHASE(7);
   if (h == 0 && lane < R) {  // epsilon-greedy for (env lane, agent a), as qmix_policy_kernel
     const int r = lane;
     const int64_t b = row0 + r;
@@ -1090,9 +1097,9 @@ __global__ void __launch_bounds__(512, LBSIM_QMIX_PAIR_WPE) qmix_agent_pair_kern
     }
   }
   __syncthreads();
-  LB_PHASE(7);
+  LB_PHASE(8);
   qmix_mixer<1, LBSIM_MIX_NW>(p, lds, chosen, row0, wave, lane, p.sld > 0 ? pre : nullptr, p.sld);
-  LB_PHASE(10);
+  LB_PHASE(11);
 }
 
 }  // namespace lbk

@@ -17,10 +17,10 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-NAMES = {"sac-gru": ["start", "staged", "gru_mma", "gru_stored", "fc1_mma", "fc1_stored",
-                     "heads", "sample"],
-         "qmix": ["start", "staged", "gru", "gru_stored", "fc1", "fc2", "fc3", "eps_greedy",
-                  "mix_l1", "mix_l2", "mix_tail"]}
+NAMES = {"sac-gru": ["start", "staged_local", "staged", "gru_mma", "gru_stored", "fc1_mma",
+                     "fc1_stored", "heads", "sample"],
+         "qmix": ["start", "staged_local", "staged", "gru", "gru_stored", "fc1", "fc2", "fc3",
+                  "eps_greedy", "mix_l1", "mix_l2", "mix_tail"]}
 
 
 def main():
