@@ -549,14 +549,15 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
     V.qcap = fails ? 0 : (recovers ? Q : V.qcap);
   }
 
-  // ---- 1. this lane's carried-in flows that complete in this step: samples in FIFO order
+  // ---- 1. this lane's carried-in flows that complete in this step: samples in FIFO order.  The
+  //      window's entries (LDS) in one loop and the rare ones past it (HBM ring) in another: one
+  //      loop over both read each entry through a flat load, and its vmcnt wait -- the counter
+  //      gfx950 shares between loads and stores -- waited for the previous insert's record store
+  //      every flow (profiles/r06o/)
   if (V.act && V.cnt > 0 && V.head_tc <= dt) {
     int32_t prev = V.last;
     uint32_t rc = V.rcnt;
-    int32_t etc = V.head_tc;
-    int32_t eta = wslot(V.lh)->y;
-    int i = 0;
-    for (;;) {
+    auto insert = [&](int32_t etc, int32_t eta) {
       if (FULL && p.split) {  // lost-FIN: split reservoirs and deferred guesses (split_complete)
         split_complete(st, p, V, sb, E.gid, E.episode, s, etc, eta,
                        dur_sample(p, etc, eta, eta > prev ? eta : prev),
@@ -582,18 +583,27 @@ __device__ __forceinline__ void sim_step_group(const DevState& st, const SimPara
         rc = count_inc(rc);
       }
       prev = etc;
-      if (++i >= V.cnt) break;
-      int2 e;
-      if (i < WL) {
-        e = *wslot((V.lh + i) & (WL - 1));
-      } else {  // rare: beyond the window
-        int pos = V.head + i;
-        pos = pos >= Q ? pos - Q : pos;
-        e = my_ring[(uint32_t)pos];
+    };
+    const int nwin = V.cnt < WL ? V.cnt : WL;
+    int i = 0;
+    bool past = false;  // an entry completing after dt was reached
+    for (; i < nwin; ++i) {
+      const int2 e = *wslot((V.lh + i) & (WL - 1));
+      if (e.x > dt) {
+        past = true;
+        break;
       }
-      etc = e.x;
-      eta = e.y;
-      if (etc > dt) break;
+      insert(e.x, e.y);
+    }
+    if (!past) {  // rare: queued beyond the window
+      int pos = V.head + i;
+      pos = pos >= Q ? pos - Q : pos;
+      for (; i < V.cnt; ++i) {
+        const int2 e = my_ring[(uint32_t)pos];
+        if (e.x > dt) break;
+        insert(e.x, e.y);
+        pos = pos + 1 == Q ? 0 : pos + 1;
+      }
     }
     V.rcnt = rc;
   }
@@ -729,6 +739,14 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
     for (int k = 0; k < G; ++k) wall[k] = 1.0f;
   };
   auto load_in = [&]() {  // the env and this lane's server from HBM, the step's weights
+    // Two HBM round trips: every word of the env and of the lane's server is requested before any
+    // is waited for (lanes past S read server 0's words and ignore them: no branch whose compares
+    // would wait inside it), then the queued entries of the 8-entry window at the head those words
+    // give, all at once (the tail and the head time are among them unless the queue is longer).
+    // The load-then-wait chain this replaces (hc, then one window entry after the other, then
+    // the discrete weight table) was ~6 round trips at the start of every wave of a one-round
+    // grid (profiles/r06o/).
+    const uint32_t sbl = V.act ? sb : b * (uint32_t)S;
     E.episode = st.episode[b];
     E.clock = st.clock[b];
     E.dropped = st.dropped[b];
@@ -737,49 +755,63 @@ __device__ __forceinline__ void dyn_group_wave(const DevState& st, const SimPara
     E.next_work = st.next_work[b];
     E.u2 = st.next_u2[b];
     E.u3 = st.next_u3[b];
-    V.cnt = 0;
-    V.head_tc = 0;
-    V.head = 0;
-    V.tail = 0;
-    V.last = kLastNone;
-    V.rcnt = 0u;
+    const uint32_t hc = st.hc[sbl];
+    const int32_t last = st.last_tc[sbl];
+    const uint32_t rcnt = st.res_count[sbl];
+    const float aw = action_weight_sel(p, action, action_dtype, (size_t)sbl);
     V.qcap = Q;
-    V.big = false;
     V.lost = 0;
     V.rcnt_d = 0u;
     V.phead = 0;
     V.pcnt = 0;
     V.pdue = 0u;
     if (FULL && p.split) lfo_base = st.lf_over[b];
-    if (V.act) {
-      if (st.down != nullptr && st.down[sb] != 0u) V.qcap = 0;
-      if (FULL && p.leak) V.lost = (int32_t)st.lost_on[sb];
-      if (FULL && p.split) {
+    if (FULL && V.act) {
+      if (p.leak) V.lost = (int32_t)st.lost_on[sb];
+      if (p.split) {
         V.rcnt_d = st.res_count_dur[sb];
         const uint32_t ph = st.pend_hc[sb];
         V.phead = (int32_t)(ph & 0xFFFFu);
         V.pcnt = (int32_t)(ph >> 16);
         if (V.pcnt > 0) V.pdue = st.pend[(size_t)sb * (uint32_t)p.pend_P + (uint32_t)V.phead].x;
       }
-      const uint32_t hc = st.hc[sb];
-      V.head = (int)(hc & kHcHead);
-      V.big = (hc & kHcBig) != 0u;
-      V.cnt = (int32_t)(hc >> 16);
-      V.last = st.last_tc[sb];
-      V.rcnt = st.res_count[sb];
-      for (int i = 0; i < WL && i < V.cnt; ++i) {
-        int pos = V.head + i;
-        if (pos >= Q) pos -= Q;
-        win[i * 64 + lane] = st.ring[sb * (uint32_t)Q + (uint32_t)pos];
-      }
-      if (V.cnt > 0) {
-        int tp = V.head + V.cnt - 1;
-        if (tp >= Q) tp -= Q;
-        V.tail = st.ring[sb * (uint32_t)Q + (uint32_t)tp].x;
-        V.head_tc = st.ring[sb * (uint32_t)Q + (uint32_t)V.head].x;
-      }
-      w_own = action_weight(p, action, action_dtype, (size_t)sb);
     }
+    if (st.down != nullptr && V.act && st.down[sb] != 0u) V.qcap = 0;  // (fail_prob handles)
+    const int head = V.act ? (int)(hc & kHcHead) : 0;
+    const int cnt = V.act ? (int32_t)(hc >> 16) : 0;
+    // (only the cnt queued entries: all 8 in every lane read 17 MB more at 65536 x 4, at the
+    // moment every wave of the one-round grid loads its state -- 5 us slower, profiles/r06o/)
+    int2 wv[WL];
+    const int2* const row = st.ring + sbl * (uint32_t)Q;
+#pragma unroll
+    for (int i = 0; i < WL; ++i) wv[i] = make_int2(0, 0);
+#pragma unroll
+    for (int i = 0; i < WL; ++i) {
+      if (i < cnt) {
+        int pos = head + i;
+        pos = pos >= Q ? pos - Q : pos;
+        wv[i] = row[pos];
+      }
+    }
+    V.head = head;
+    V.big = V.act && (hc & kHcBig) != 0u;
+    V.cnt = cnt;
+    V.last = V.act ? last : kLastNone;
+    V.rcnt = V.act ? rcnt : 0u;
+#pragma unroll
+    for (int i = 0; i < WL; ++i)
+      if (i < cnt) win[i * 64 + lane] = wv[i];
+    int32_t tail = wv[0].x;
+#pragma unroll
+    for (int i = 1; i < WL; ++i) tail = cnt == i + 1 ? wv[i].x : tail;
+    if (cnt > WL) {  // a longer queue: its tail entry past the window
+      int tp = head + cnt - 1;
+      if (tp >= Q) tp -= Q;
+      tail = row[tp].x;
+    }
+    V.tail = cnt > 0 ? tail : 0;
+    V.head_tc = cnt > 0 ? wv[0].x : 0;
+    if (V.act) w_own = aw;
     if constexpr (alias) {
 #pragma unroll
       for (int k = 0; k < G; ++k)

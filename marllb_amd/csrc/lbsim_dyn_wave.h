@@ -599,18 +599,34 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
     E.next_work = st.next_work[b];
     E.u2 = st.next_u2[b];
     E.u3 = st.next_u3[b];
-    // ring lanes: this lane's ring positions, live if within [head, head + count)
+    // every load first, from clamped in-range addresses (the ring lanes' slots and their servers'
+    // head / count words, the server lane's own words and action), then the selects: one HBM
+    // round trip (branches around the loads waited inside them, and the discrete weight came from
+    // a table behind the action's load, profiles/r06o/)
+    int2 e[NG];
+    uint32_t hcg[NG];
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       const int srv = 2 * g + (lane >> 5);
-      if (srv < S && rpos < Q) {  // the slot and its server's head / count, loaded together
-        const int2 e = st.ring[(size_t)(b * (uint32_t)S + (uint32_t)srv) * (size_t)Q + rpos];
-        const uint32_t hc = st.hc[b * (uint32_t)S + (uint32_t)srv];
-        const int head = (int)(hc & kHcHead), cnt = (int)(hc >> 16);
+      const bool ok = srv < S && rpos < Q;
+      const uint32_t sv = b * (uint32_t)S + (uint32_t)(ok ? srv : 0);
+      e[g] = st.ring[(size_t)sv * (size_t)Q + (ok ? rpos : 0)];
+      hcg[g] = st.hc[sv];
+    }
+    const uint32_t sbl = V.act ? sb : b * (uint32_t)S;
+    const uint32_t hc = st.hc[sbl];
+    const int32_t last = st.last_tc[sbl];
+    const uint32_t rcnt = st.res_count[sbl];
+    const float aw = action_weight_sel(p, action, action_dtype, (size_t)sbl);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {  // ring lanes: live if within [head, head + count)
+      const int srv = 2 * g + (lane >> 5);
+      if (srv < S && rpos < Q) {
+        const int head = (int)(hcg[g] & kHcHead), cnt = (int)(hcg[g] >> 16);
         int rel = rpos - head;
         rel = rel < 0 ? rel + Q : rel;
-        R.tc[g] = rel < cnt ? e.x : kDead;
-        R.ta[g] = e.y;
+        R.tc[g] = rel < cnt ? e[g].x : kDead;
+        R.ta[g] = e[g].y;
       }
     }
     V.cnt0 = 0;
@@ -619,15 +635,14 @@ __device__ __forceinline__ bool dyn_wave_env(const DevState& st, const SimParams
     V.last = kLastNone;
     V.rcnt = 0u;
     if (V.act) {
-      const uint32_t hc = st.hc[sb];
       const int head = (int)(hc & kHcHead);
       V.cnt0 = (int32_t)(hc >> 16);
       Ld.big[lane] = (hc & kHcBig) ? 1u : 0u;
       const int wp = head + V.cnt0;
       V.wp = wp >= Q ? wp - Q : wp;
-      V.last = st.last_tc[sb];
-      V.rcnt = st.res_count[sb];
-      w_own = action_weight(p, action, action_dtype, (size_t)sb);
+      V.last = last;
+      V.rcnt = rcnt;
+      w_own = aw;
     }
     {  // tail = t_complete of the last queued flow, from the ring lanes (no dependent load)
       const int tp = V.wp == 0 ? Q - 1 : V.wp - 1;

@@ -1212,6 +1212,25 @@ __device__ __forceinline__ float action_weight(const SimParams& p, const void* a
   return a < p.min_w ? p.min_w : (a > p.max_w ? p.max_w : a);
 }
 
+// action_weight with the discrete table read from kernel arguments by index-compare selects (no
+// per-lane load from the argument segment behind the action's own load: one HBM round trip)
+__device__ __forceinline__ float action_weight_sel(const SimParams& p, const void* action,
+                                                   int dtype, size_t idx) {
+  if (p.action_type == 0) {
+    int64_t a = (dtype == 1) ? ((const int64_t*)action)[idx]
+                             : (int64_t)((const int32_t*)action)[idx];
+    if (a < 0) a += p.num_discrete;  // python negative indexing
+    if (a < 0) a = 0;
+    if (a >= p.num_discrete) a = p.num_discrete - 1;
+    float w = p.dw[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) w = a == k ? p.dw[k] : w;
+    return w;
+  }
+  const float a = ((const float*)action)[idx];
+  return a < p.min_w ? p.min_w : (a > p.max_w ? p.max_w : a);
+}
+
 // Waves per workgroup of dynamics_kernel.  Every wave runs a long, issue-bound event loop, so a
 // SIMD holding two waves finishes twice as late.  With one-wave workgroups the dispatcher stacked
 // some CUs (up to 6 fit by LDS) while others had room: at 65536 x 4 (1024 waves on 1024 SIMDs) the
