@@ -496,15 +496,18 @@ int fused_ld(int need) { return ((need - 4 + 63) / 64) * 64 + 4; }
 int round16(int x) { return (x + 15) / 16 * 16; }
 constexpr size_t kFusedLdsMax = 160 * 1024;
 
-// Envs per workgroup = 16 MT.  MT = 1 measured best for both kernels (profiles/r01s3a: SAC-GRU
-// 65536 x 8 0.231 / 0.267 / 0.352 ms at MT = 1 / 2 / 4 -- the MT = 4 tile needs 290 VGPRs, one
-// wave per SIMD; QMIX 8192 x 16 0.121 / 0.157 / 0.251 ms).  LBSIM_FUSED_MT = 1 | 2 | 4 forces it.
-int fused_mt(int64_t) {
+// Envs per workgroup = 16 MT.  QMIX's tile kernel: MT = 1 (8192 x 16 0.121 / 0.157 / 0.251 ms at
+// MT = 1 / 2 / 4, profiles/r01s3a).  The SAC actor: MT = 2 since round 6 -- with its staging one
+// HBM round trip (r06n), a 32-env tile halves the weight stream per env, and the weight stream is
+// what the staging waited behind: 187-188 -> 179.3-179.7 us at 65536 x 8, 0.53 -> 0.556 of the
+// f32 MFMA peak (profiles/r06q/; round 1, with the staging serialised, MT = 2 was the slower:
+// 0.231 vs 0.267 ms).  LBSIM_FUSED_MT = 1 | 2 | 4 forces it for both.
+int fused_mt(int64_t, int dflt = 1) {
   static const int forced = [] {
     const char* s = std::getenv("LBSIM_FUSED_MT");
     return s ? std::atoi(s) : 0;
   }();
-  return (forced == 2 || forced == 4) ? forced : 1;
+  return (forced == 1 || forced == 2 || forced == 4) ? forced : dflt;
 }
 
 }  // namespace
@@ -890,7 +893,7 @@ int lbsim_sac_actor_step(const lbsim_sac_actor_t* n, const float* state, float* 
   a.key1 = (uint32_t)(seed >> 32);
   a.step = step;
   a.step_dev = n->step_dev;
-  int mt = fused_mt(B);
+  int mt = fused_mt(B, 2);
   // the [R][ld] tile + split-K scratch of the heads ([4][nt][R][16], nt = ceil(2A / 16)): at A = 8
   // 20.6 KB per 16-env tile, 7 tiles per CU
   const int nt_heads = (2 * a.A + 15) / 16;

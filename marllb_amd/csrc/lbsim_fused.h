@@ -518,6 +518,10 @@ struct QmixMixAct {
 #ifndef LBSIM_MIX_PRIME
 #define LBSIM_MIX_PRIME 1
 #endif
+// 1: the pair kernel's first GRU weights requested after its staging loads (A/B)
+#ifndef LBSIM_QMIX_PRIME_LATE
+#define LBSIM_QMIX_PRIME_LATE 0
+#endif
 // waves per SIMD the pair kernel is built for: 4 = two 8-wave workgroups per CU (<= 128 VGPRs)
 #ifndef LBSIM_QMIX_PAIR_WPE
 #define LBSIM_QMIX_PAIR_WPE 4
@@ -888,7 +892,7 @@ __global__ void __launch_bounds__(512, LBSIM_QMIX_PAIR_WPE) qmix_agent_pair_kern
   // the first GRU pass's weights, the epsilon-greedy draw (independent of the network) and the
   // mixer's state rows go out first: their latency hides behind the staging
   BPrime<3> bp_gru;
-  {
+  if (!LBSIM_QMIX_PRIME_LATE) {
     const f4* wx[3];
     gru_wx(h, wx);
     bp_gru = mma_prime<3>(wx, kbx, lane);
@@ -937,6 +941,11 @@ __global__ void __launch_bounds__(512, LBSIM_QMIX_PAIR_WPE) qmix_agent_pair_kern
     const bool ok = e < tots && c < p.Ds && b < p.B;
     sat[k] = e < tots ? (ok ? r * p.sld + c : -(r * p.sld + c) - 1) : INT32_MIN;
     vs[k] = p.state[bc * p.Ds + (ok ? c : 0)];
+  }
+  if (LBSIM_QMIX_PRIME_LATE) {  // the weights after the HBM rows (every workgroup reads the same
+    const f4* wx[3];            // lines: L2-channel hot spots)
+    gru_wx(h, wx);
+    bp_gru = mma_prime<3>(wx, kbx, lane);
   }
   // the reset bytes last: their compares (hoisted into the branch) wait for every load above,
   // which are all in flight by then -- one HBM round trip for the whole staging

@@ -189,12 +189,13 @@ def test_qmix_policy_kernel_wide_obs_matches_modules():
 @pytest.mark.gpu
 @pytest.mark.parametrize("env", [{"LBSIM_QMIX_KERNEL": "wave"},
                                  {"LBSIM_QMIX_KERNEL": "tile"},
+                                 {"LBSIM_FUSED_MT": "1"},
                                  {"LBSIM_FUSED_MT": "2", "LBSIM_QMIX_KERNEL": "tile"},
                                  {"LBSIM_FUSED_MT": "4", "LBSIM_QMIX_KERNEL": "tile"}])
 def test_other_tile_forms_match_modules(env):
-    """The one-wave-per-agent and layer-split QMIX kernels and the 32 / 64-env tiles (selected once
-    per process by the environment, so checked in a child process) pass the same parity tests as
-    the default two-waves-per-agent kernel."""
+    """The one-wave-per-agent and layer-split QMIX kernels, the 16 / 32 / 64-env tiles (SAC's
+    default is 32 since round 6, the QMIX tile kernel's 16; selected once per process by the
+    environment, so checked in a child process) pass the same parity tests as the defaults."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
