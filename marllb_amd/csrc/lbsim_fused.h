@@ -36,8 +36,8 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f4 splat4(float v) { return f4{v, v, v, v}; }
 
 // Timing diagnostic only (wrong results): LBSIM_EXP_L1W=1 makes every k-block past the first two
-// re-read one of the tile's first two weight blocks, so the weight stream fits in L1 and the run
-// shows what streaming the weights from L2 costs the policy kernels.
+// re-read one of the tile's first two weight blocks: fewer distinct weight bytes, the same stream
+// of weight requests (a CU's ~24 waves' blocks still overflow its L1; profiles/r06k/).
 #if LBSIM_EXP_L1W
 #define LBSIM_EXP_WBLK(n) ((n) & 1)
 #else
@@ -518,6 +518,10 @@ struct QmixMixAct {
 #ifndef LBSIM_MIX_PRIME
 #define LBSIM_MIX_PRIME 1
 #endif
+// 1: the pair kernel's epsilon-greedy inside the mixer's first layer (no barrier of its own)
+#ifndef LBSIM_QMIX_EPS_IN_MIXER
+#define LBSIM_QMIX_EPS_IN_MIXER 1
+#endif
 // 1: the pair kernel's first GRU weights requested after its staging loads (A/B)
 #ifndef LBSIM_QMIX_PRIME_LATE
 #define LBSIM_QMIX_PRIME_LATE 0
@@ -532,10 +536,14 @@ struct QmixMixAct {
 #ifndef LBSIM_MIX_TAIL
 #define LBSIM_MIX_TAIL 1
 #endif
-template <int MT, int NW = 4>
+struct NoOp {
+  __device__ void operator()() const {}
+};
+template <int MT, int NW = 4, class Pre1 = NoOp>
 __device__ __forceinline__ void qmix_mixer(const QmixArgs& p, float* lds, const float* chosen,
                                            int64_t row0, int wave, int lane,
-                                           const float* pre = nullptr, int pre_ld = 0) {
+                                           const float* pre = nullptr, int pre_ld = 0,
+                                           Pre1 pre1 = NoOp{}) {
   static_assert(NW == 4 || NW == 8, "4- or 8-wave workgroups");
   constexpr int R = 16 * MT;
   constexpr int J1 = 16 / NW;  // first-layer tiles per wave (3 he + E <= 256 columns)
@@ -580,6 +588,7 @@ __device__ __forceinline__ void qmix_mixer(const QmixArgs& p, float* lds, const 
     const int nt0 = (3 * he + E) / 16;  // <= 16
     f4 acc[J1][MT];
     if (mw) dense_acc<MT, J1, NW>(acc, x0, x0_ld, 0, p.m0, p.ksp / 16, nt0, p.mb0, wave, lane);
+    pre1();  // (the pair kernel's epsilon-greedy: chosen is read by the tail only)
     __syncthreads();
     if (mw) dense_store<MT, J1, QmixMixAct, NW>(acc, lds, ld, 0, nt0, wave, lane, QmixMixAct{3 * he});
   }
@@ -1085,29 +1094,42 @@ __global__ void __launch_bounds__(512, LBSIM_QMIX_PAIR_WPE) qmix_agent_pair_kern
   }
   __syncthreads();
   LB_PHASE(7);
-  if (h == 0 && lane < R) {  // epsilon-greedy for (env lane, agent a), as qmix_policy_kernel
-    const int r = lane;
-    const int64_t b = row0 + r;
-    const float* q = qv + (a * R + r) * 16;
-    int g = 0;
-    for (int j = 1; j < NQ; ++j)
-      if (q[j] > q[g]) g = j;
-    const u32x4 d = eps_d;  // drawn at the start
-    const float u = (float)(d.x >> 8) * 5.9604644775390625e-8f;
-    const int act = u < p.epsilon ? (int)(((uint64_t)d.y * (uint32_t)NQ) >> 32) : g;
-    chosen[r * A + a] = q[act];
-    if (b < p.B) {
-      p.actions[b * A + a] = act;
-      if (p.server_actions)
-        for (int j = 0; j < p.k; ++j) p.server_actions[(b * A + a) * p.k + j] = act;
-      if (p.q_out)
-        for (int j = 0; j < NQ; ++j) p.q_out[(b * A + a) * NQ + j] = q[j];
-      if (p.q_chosen) p.q_chosen[b * A + a] = q[act];
+  // epsilon-greedy for (env lane, agent a), as qmix_policy_kernel.  Its results (chosen) are read
+  // only by the mixer's tail, so it runs inside the mixer's first layer, after that layer's GEMM
+  // and before its barrier (LBSIM_QMIX_EPS_IN_MIXER; it had a barrier interval of its own)
+  auto eps_greedy = [&]() {
+    if (h == 0 && lane < R) {
+      const int r = lane;
+      const int64_t b = row0 + r;
+      const float* q = qv + (a * R + r) * 16;
+      int g = 0;
+      for (int j = 1; j < NQ; ++j)
+        if (q[j] > q[g]) g = j;
+      const u32x4 d = eps_d;  // drawn at the start
+      const float u = (float)(d.x >> 8) * 5.9604644775390625e-8f;
+      const int act = u < p.epsilon ? (int)(((uint64_t)d.y * (uint32_t)NQ) >> 32) : g;
+      chosen[r * A + a] = q[act];
+      if (b < p.B) {
+        p.actions[b * A + a] = act;
+        if (p.server_actions)
+          for (int j = 0; j < p.k; ++j) p.server_actions[(b * A + a) * p.k + j] = act;
+        if (p.q_out)
+          for (int j = 0; j < NQ; ++j) p.q_out[(b * A + a) * NQ + j] = q[j];
+        if (p.q_chosen) p.q_chosen[b * A + a] = q[act];
+      }
     }
+  };
+  if (!LBSIM_QMIX_EPS_IN_MIXER) {
+    eps_greedy();
+    __syncthreads();
   }
-  __syncthreads();
   LB_PHASE(8);
-  qmix_mixer<1, LBSIM_MIX_NW>(p, lds, chosen, row0, wave, lane, p.sld > 0 ? pre : nullptr, p.sld);
+  if (LBSIM_QMIX_EPS_IN_MIXER)
+    qmix_mixer<1, LBSIM_MIX_NW>(p, lds, chosen, row0, wave, lane, p.sld > 0 ? pre : nullptr,
+                                p.sld, eps_greedy);
+  else
+    qmix_mixer<1, LBSIM_MIX_NW>(p, lds, chosen, row0, wave, lane, p.sld > 0 ? pre : nullptr,
+                                p.sld);
   LB_PHASE(11);
 }
 
