@@ -32,8 +32,9 @@
 extern "C" {
 #endif
 
-#define LBSIM_ABI_VERSION 9  /* 9: lost-FIN guesses deferred to their wrap-up time (split fct /  */
-                             /* duration reservoirs, pending rings), reservoir_mode VPP          */
+#define LBSIM_ABI_VERSION 10 /* 10: lbsim_step_outputs_t ends with done_word / done_value (the */
+                             /* one-env completion word); 9: lost-FIN guesses deferred to their */
+                             /* wrap-up time, reservoir_mode VPP                                 */
 #define LBSIM_MAX_SERVERS 64   /* S <= 64: BASELINE configs[4] read literally is 4 agents x 16 */
                                /* servers = 64 (S > 16: server-per-lane dynamics only)       */
 #define LBSIM_RESERVOIR_K 128  /* reservoir.py:31 capacity=128, reservoir.h:24               */

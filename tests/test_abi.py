@@ -19,7 +19,7 @@ def test_library_loads_and_exports_every_header_symbol():
 def test_version_and_layout_sizes():
     lib = _lib.load()
     assert lib.lbsim_version().startswith(b"lbsim")
-    assert lib.lbsim_abi_version() == 9
+    assert lib.lbsim_abi_version() == 10
     assert lib.lbsim_config_size() == ctypes.sizeof(_lib.LbsimConfig)
     assert lib.lbsim_step_outputs_size() == ctypes.sizeof(_lib.StepOutputs)
 
