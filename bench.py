@@ -185,7 +185,7 @@ def parse():
                          "kernels and the launch -- so 20 steps amortise it to ~1.4 us per step, "
                          "profiles/r06l/)")
     ap.add_argument("--no-graph", action="store_true",
-                    help="skip the graph leg (N=1: the same workload with one step captured in a "
+                    help="skip the graph leg (N=1: the same workload with --graph-steps steps captured in a "
                          "hipGraph and replayed, reported beside `value` as `graph`)")
     ap.add_argument("--async-groups", type=int, default=0,
                     help="rollout workload at N=1: after the headline, also time the same rollout "
@@ -357,7 +357,7 @@ def async_groups(args, dev, shard, B, S, common, groups):
 
 
 def graph_leg(args, dev, shard, B, S, common, kernel_ms):
-    """The same workload with one step captured into a torch.cuda.CUDAGraph (hipGraph) and
+    """The same workload with k = --graph-steps steps captured into one torch.cuda.CUDAGraph (hipGraph) and
     replayed: a fresh env in graph_mode with static buffers -- the random-policy rollout with
     next-step auto-reset (the resets run inside the step launches, so the captured step is the
     eager step's two launches and nothing else), the policy rollouts with the same-step masked
