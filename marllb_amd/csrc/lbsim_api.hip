@@ -897,7 +897,10 @@ int lbsim_sac_actor_step(const lbsim_sac_actor_t* n, const float* state, float* 
   // the [R][ld] tile + split-K scratch of the heads ([4][nt][R][16], nt = ceil(2A / 16)): at A = 8
   // 20.6 KB per 16-env tile, 7 tiles per CU
   const int nt_heads = (2 * a.A + 15) / 16;
-  auto lds_of = [&](int m) { return (size_t)16 * m * (a.ld + 64 * nt_heads) * 4; };
+  // (the 32-env tile's heads keep two partials per row, not four: LBSIM_SAC_SPLIT_M, lbsim_fused.h)
+  auto lds_of = [&](int m) {
+    return (size_t)16 * m * (a.ld + (m == 2 && LBSIM_SAC_SPLIT_M ? 32 : 64) * nt_heads) * 4;
+  };
   while (mt > 1 && lds_of(mt) > kFusedLdsMax) mt >>= 1;
   const size_t lds = lds_of(mt);
   const hipStream_t s = (hipStream_t)stream;

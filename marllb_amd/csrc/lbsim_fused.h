@@ -217,6 +217,36 @@ __device__ __forceinline__ void splitk_out(const float* lds, int ld, const float
   }
 }
 
+// splitk_out for a 32-row tile (MT = 2): wave w runs M-tile w >> 1 over the k-blocks of half
+// (w & 1), so the scratch holds two partials per row ([2][nt][32][16]) instead of four -- the
+// SAC tile's LDS is then 37.4 KB, four workgroups per CU where the four-partial scratch (41.5 KB)
+// fit three (LBSIM_SAC_SPLIT_M).  Contains a barrier; the caller barriers again before reading dst.
+__device__ __forceinline__ void splitk_out_m2(const float* lds, int ld, const float* __restrict__ w,
+                                              const float* __restrict__ bias, int nkb, int nt,
+                                              float* scratch, float* dst, int dld, int ncols,
+                                              int wave, int lane) {
+  constexpr int R = 32;
+  const int m = wave >> 1, kh = wave & 1;
+  const int k0 = kh * nkb / 2, k1 = (kh + 1) * nkb / 2;
+  for (int t = 0; t < nt; ++t) {
+    f4 acc[1] = {splat4(0.0f)};
+    if (k1 > k0)
+      mma_tile<1>(acc, lds + m * 16 * ld, ld, k0 * 16, (const f4*)w + ((size_t)t * nkb + k0) * 64,
+                  k1 - k0, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      scratch[((kh * nt + t) * R + m * 16 + 4 * (lane >> 4) + i) * 16 + (lane & 15)] = acc[0][i];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < R * ncols; e += blockDim.x) {
+    const int r = e / ncols, c = e - r * ncols, t = c >> 4, cc = c & 15;
+    float v = bias[c];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) v += scratch[((q * nt + t) * R + r) * 16 + cc];
+    dst[r * dld + c] = v;
+  }
+}
+
 // Dense layer, store phase (after a barrier): out[row][col0 + 16 nt + c] = act(acc, 16 nt + c).
 template <int MT, int NTW, class Act, int WS = 4>
 __device__ __forceinline__ void dense_store(const f4 (&acc)[NTW][MT], float* lds, int ld, int col0,
@@ -408,6 +438,11 @@ __device__ __forceinline__ void stage_sac_rows(float* lds, const SacActorArgs& p
 #ifndef LBSIM_SAC_WPE
 #define LBSIM_SAC_WPE 1
 #endif
+// 1: the 32-env SAC tile's heads split their K over 2 waves per M-tile (splitk_out_m2), the LDS
+// scratch halved (lbsim_api.hip sac_lds_bytes must agree)
+#ifndef LBSIM_SAC_SPLIT_M
+#define LBSIM_SAC_SPLIT_M 1
+#endif
 
 template <int MT, int H, int F>
 __global__ void __launch_bounds__(256, LBSIM_SAC_WPE) sac_actor_kernel(SacActorArgs p) {
@@ -448,8 +483,12 @@ __global__ void __launch_bounds__(256, LBSIM_SAC_WPE) sac_actor_kernel(SacActorA
   LB_PHASE(6);
   // heads [mean | log_std] (2A <= 32 columns), K split over the waves; y over the first 2A
   // columns of the tile
-  splitk_out<MT>(lds, ld, p.wh, p.bh, F / 16, (2 * p.A + 15) / 16, lds + R * ld, lds, ld,
-                 2 * p.A, wave, lane);
+  if constexpr (MT == 2 && LBSIM_SAC_SPLIT_M)
+    splitk_out_m2(lds, ld, p.wh, p.bh, F / 16, (2 * p.A + 15) / 16, lds + R * ld, lds, ld,
+                  2 * p.A, wave, lane);
+  else
+    splitk_out<MT>(lds, ld, p.wh, p.bh, F / 16, (2 * p.A + 15) / 16, lds + R * ld, lds, ld,
+                   2 * p.A, wave, lane);
   __syncthreads();
   LB_PHASE(7);
   const int A = p.A;
