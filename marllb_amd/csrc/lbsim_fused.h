@@ -561,6 +561,11 @@ struct QmixMixAct {
 #ifndef LBSIM_QMIX_EPS_IN_MIXER
 #define LBSIM_QMIX_EPS_IN_MIXER 1
 #endif
+// 1: the pair kernel's obs rows loaded straight into LDS and waited for after the GRU's hidden
+// pass, which then runs first (see qmix_agent_pair_kernel)
+#ifndef LBSIM_QMIX_ASYNC_OBS
+#define LBSIM_QMIX_ASYNC_OBS 0
+#endif
 // 1: the pair kernel's first GRU weights requested after its staging loads (A/B)
 #ifndef LBSIM_QMIX_PRIME_LATE
 #define LBSIM_QMIX_PRIME_LATE 0
@@ -940,10 +945,16 @@ __global__ void __launch_bounds__(512, LBSIM_QMIX_PAIR_WPE) qmix_agent_pair_kern
   // the first GRU pass's weights, the epsilon-greedy draw (independent of the network) and the
   // mixer's state rows go out first: their latency hides behind the staging
   BPrime<3> bp_gru;
+  auto gru_wy = [&](int u, const f4* (&wy)[3]) {
+    wy[0] = wh + (size_t)u * UT * 64;
+    wy[1] = wh + (size_t)(UT + u) * UT * 64;
+    wy[2] = wh + (size_t)(2 * UT + u) * UT * 64;
+  };
   if (!LBSIM_QMIX_PRIME_LATE) {
     const f4* wx[3];
-    gru_wx(h, wx);
-    bp_gru = mma_prime<3>(wx, kbx, lane);
+    if (LBSIM_QMIX_ASYNC_OBS) gru_wy(h, wx);  // the hidden pass runs first
+    else gru_wx(h, wx);
+    bp_gru = mma_prime<3>(wx, LBSIM_QMIX_ASYNC_OBS ? UT : kbx, lane);
   }
   u32x4 eps_d{};
   if (h == 0 && lane < R)
@@ -957,7 +968,26 @@ __global__ void __launch_bounds__(512, LBSIM_QMIX_PAIR_WPE) qmix_agent_pair_kern
   // waited for every earlier load, profiles/r06m/ r06n/)
   static_assert(128 % H == 0 && R * H % 128 == 0, "hidden staging: whole rows per thread group");
   constexpr int RH = R * H / 128;  // hidden rows per thread
-  const bool obs1 = kxp <= 128;    // one obs column per thread (else the loop below)
+  // LBSIM_QMIX_ASYNC_OBS: the obs rows go straight into LDS (global_load_lds, no VGPRs) when a
+  // row is whole 64-column blocks (I == kxp, a multiple of 64, <= 128: 4 x 4's 128), and are waited
+  // for only before the GRU's input pass -- the hidden pass runs first, on the hidden rows staged
+  // below, while the obs rows (2/3 of the 27.6 MB burst at 8192 x 16) are still arriving
+  const bool obs_async = LBSIM_QMIX_ASYNC_OBS && p.I == kxp && kxp % 64 == 0 && kxp <= 128;
+  if (obs_async) {
+    typedef __attribute__((address_space(1))) void gvoid;
+    typedef __attribute__((address_space(3))) void lvoid;
+    const int nq = kxp / 64;
+#pragma unroll
+    for (int i = 0; i < R / 2; ++i) {  // wave h: rows 8 h .. 8 h + 7
+      const int r = h * (R / 2) + i;
+      const int64_t b = row0 + r, bc = b < p.B ? b : p.B - 1;
+      for (int q = 0; q < nq; ++q)
+        __builtin_amdgcn_global_load_lds(
+            (gvoid*)(p.obs + (bc * A + a) * p.I + q * 64 + lane),
+            (lvoid*)(mine + r * lda + q * 64), 4, 0, 0);
+    }
+  }
+  const bool obs1 = kxp <= 128 && !obs_async;  // one obs column per thread (else the loop below)
   const bool ocol = t2 < p.I;
   float vo[R];
   if (obs1) {
@@ -992,8 +1022,9 @@ __global__ void __launch_bounds__(512, LBSIM_QMIX_PAIR_WPE) qmix_agent_pair_kern
   }
   if (LBSIM_QMIX_PRIME_LATE) {  // the weights after the HBM rows (every workgroup reads the same
     const f4* wx[3];            // lines: L2-channel hot spots)
-    gru_wx(h, wx);
-    bp_gru = mma_prime<3>(wx, kbx, lane);
+    if (LBSIM_QMIX_ASYNC_OBS) gru_wy(h, wx);
+    else gru_wx(h, wx);
+    bp_gru = mma_prime<3>(wx, LBSIM_QMIX_ASYNC_OBS ? UT : kbx, lane);
   }
   // the reset bytes last: their compares (hoisted into the branch) wait for every load above,
   // which are all in flight by then -- one HBM round trip for the whole staging
@@ -1007,7 +1038,9 @@ __global__ void __launch_bounds__(512, LBSIM_QMIX_PAIR_WPE) qmix_agent_pair_kern
 #pragma unroll
     for (int i = 0; i < RH; ++i) keep[i] = keep[i] && m[i] == 0;
   }
-  if (obs1) {
+  if (obs_async) {
+    // (rows past B read the last env's row: their outputs are never stored)
+  } else if (obs1) {
     if (t2 < kxp)
 #pragma unroll
       for (int r = 0; r < R; ++r) mine[r * lda + t2] = (ocol && row0 + r < p.B) ? vo[r] : 0.0f;
@@ -1047,11 +1080,21 @@ __global__ void __launch_bounds__(512, LBSIM_QMIX_PAIR_WPE) qmix_agent_pair_kern
     g[3][0] = splat4(bh[2 * H + col]);
     const f4* wx[3];
     gru_wx(u, wx);
-    const f4* const wy[3] = {wh + (size_t)u * UT * 64, wh + (size_t)(UT + u) * UT * 64,
-                             wh + (size_t)(2 * UT + u) * UT * 64};
-    mma_multi<1, 3>(*reinterpret_cast<f4(*)[3][1]>(&g[0]), mine, lda, 0, wx, kbx, lane,
-                    uu == 0 ? bp_gru : mma_prime<3>(wx, kbx, lane));
-    mma_multi<1, 3>(*reinterpret_cast<f4(*)[3][1]>(&g[1]), mine, lda, kxp, wy, UT, lane);
+    const f4* wy[3];
+    gru_wy(u, wy);
+    if (LBSIM_QMIX_ASYNC_OBS) {  // hidden part first (r, z, n_h), then the input part
+      mma_multi<1, 3>(*reinterpret_cast<f4(*)[3][1]>(&g[1]), mine, lda, kxp, wy, UT, lane,
+                      uu == 0 ? bp_gru : mma_prime<3>(wy, UT, lane));
+      if (uu == 0 && obs_async) {  // the obs rows landed in LDS, every wave's
+        __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+        __syncthreads();
+      }
+      mma_multi<1, 3>(*reinterpret_cast<f4(*)[3][1]>(&g[0]), mine, lda, 0, wx, kbx, lane);
+    } else {
+      mma_multi<1, 3>(*reinterpret_cast<f4(*)[3][1]>(&g[0]), mine, lda, 0, wx, kbx, lane,
+                      uu == 0 ? bp_gru : mma_prime<3>(wx, kbx, lane));
+      mma_multi<1, 3>(*reinterpret_cast<f4(*)[3][1]>(&g[1]), mine, lda, kxp, wy, UT, lane);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float hp = mine[(4 * (lane >> 4) + i) * lda + kxp + col];
