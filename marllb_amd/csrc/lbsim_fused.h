@@ -564,7 +564,7 @@ struct QmixMixAct {
 // 1: the pair kernel's obs rows loaded straight into LDS and waited for after the GRU's hidden
 // pass, which then runs first (see qmix_agent_pair_kernel)
 #ifndef LBSIM_QMIX_ASYNC_OBS
-#define LBSIM_QMIX_ASYNC_OBS 0
+#define LBSIM_QMIX_ASYNC_OBS 1
 #endif
 // 1: the pair kernel's first GRU weights requested after its staging loads (A/B)
 #ifndef LBSIM_QMIX_PRIME_LATE
